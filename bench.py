@@ -1,0 +1,197 @@
+"""Headline benchmark: BLAKE2f compressions/s, witness fill + constraint eval, 2^18 batch of
+12-round compressions per GPU (BASELINE.json configs[2]; configs[4] with --mix).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+One step = fill (record + fill kernels) then eval of the whole per-GPU batch; inputs and the
+trace stay resident in HBM. N > 1: every rank runs its own 2^18 shard (weak scaling); the
+step ends with one all_reduce of the verdict counters and one RCCL all_gather of the h'
+outputs. Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "zk-odst_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+ADVICE_COLS = 10
+ROW_BYTES = 4 * (ADVICE_COLS + 1)  # 10 advice u32 + 1 fixed u32
+INPUT_BYTES = 216
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(rounds, mix, target_s):
+    """Time the CPU oracle (oracle/, a C port of the same fill + eval) on a bounded sample of
+    the same workload, all host threads it is given. Test infrastructure: the checker."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from b2f import synth
+
+    threads = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
+
+    def run(n):
+        x = synth.batch(n, rounds=rounds, rounds_mix=mix, seed=0xC0FFEE)
+        ox = np.frombuffer(x.tobytes(), dtype=oracle.INPUT_DTYPE).copy()
+        t0 = time.perf_counter()
+        adv, fixed, h_out, off = oracle.fill(ox, nthreads=threads)
+        rep = oracle.evaluate(adv, fixed, off, nthreads=threads)
+        dt = time.perf_counter() - t0
+        assert rep["first_failure"] == 2**64 - 1
+        return dt
+
+    n = 4 * threads
+    dt = run(n)
+    n2 = int(min(max(n, n * target_s / max(dt, 1e-3)), 16384))
+    dt2 = run(n2)
+    return {"value": n2 / dt2, "unit": "compressions/s", "cores": threads, "kind": "port",
+            "sample": "%d x %s-round compressions, oracle fill + eval (%.1f s wall, %d threads)"
+                      % (n2, "mixed" if mix else rounds, dt2, threads)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1 << 18, help="instances per GPU")
+    ap.add_argument("--rounds", type=int, default=12)
+    ap.add_argument("--mix", action="store_true", help="rounds uniform in {1,4,12} (config 5)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import b2f
+    from b2f import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    mix = [1, 4, 12] if args.mix else None
+    n = args.batch
+    x = synth.batch(n, rounds=args.rounds, rounds_mix=mix, first=rank * n)
+    batch = b2f.DeviceBatch(x, device="cuda:%d" % local)
+    eng = b2f.Engine(local)
+    stream = torch.cuda.current_stream().cuda_stream
+    rows = batch.used_rows
+    log("rank %d: %d instances, %d rows, trace %.1f GB" % (rank, n, rows, rows * ROW_BYTES / 1e9))
+
+    if world > 1:
+        gathered = torch.empty((world * n, 8), dtype=torch.int64, device=batch.h_out.device)
+        verdict = torch.empty(20, dtype=torch.int64, device=batch.h_out.device)
+
+    def step():
+        batch.fill(eng, stream)
+        batch.evaluate(eng, stream)
+        if world > 1:
+            r = batch.report.view(torch.int64)
+            verdict[:18].copy_(r[:18])
+            first = r[18]
+            verdict[18] = torch.where(first == -1, torch.iinfo(torch.int64).max, first)
+            dist.all_reduce(verdict[:18], op=dist.ReduceOp.SUM)
+            dist.all_reduce(verdict[18:19], op=dist.ReduceOp.MIN)
+            dist.all_gather_into_tensor(gathered, batch.h_out)
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync(stream)
+    rep = batch.report_dict()
+    if rep["first_failure"] != 2**64 - 1:
+        raise SystemExit("eval flagged the trace: %s" % rep)
+
+    eng.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ktimes = eng.kernel_times()
+    eng.sync(stream)
+    rep = batch.report_dict()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=batch.h_out.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        if int(verdict[18].item()) != torch.iinfo(torch.int64).max or int(verdict[:18].sum()) != 0:
+            raise SystemExit("eval flagged a shard")
+    if rep["first_failure"] != 2**64 - 1:
+        raise SystemExit("eval flagged the trace: %s" % rep)
+
+    value = world * n * args.steps / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # roofline: algorithmic bytes per launch / average launch duration (HIP events)
+    fill_bytes = n * INPUT_BYTES + rows * ROW_BYTES      # inputs read + trace written
+    eval_bytes = rows * ROW_BYTES + 8 * (n + 1)          # trace + offsets read
+    kern = {}
+    for name, nbytes in (("fill", fill_bytes), ("eval", eval_bytes), ("record", None)):
+        tot, cnt = ktimes[name]
+        avg = tot / max(cnt, 1)
+        kern[name] = {"avg_ms": round(avg, 4), "launches": cnt}
+        if nbytes:
+            gbs = nbytes / (avg * 1e-3) / 1e9
+            kern[name].update({"bytes_per_launch": nbytes, "achieved_GBs": round(gbs, 1),
+                               "frac": round(gbs / HBM_PEAK_GBS, 4)})
+    dom = "eval" if kern["eval"]["avg_ms"] >= kern["fill"]["avg_ms"] else "fill"
+    traffic = None
+    try:
+        with open(args.traffic) as fh:
+            tr = json.load(fh)
+        key = "%s_%d_%s" % (dom, n, "mix" if mix else args.rounds)
+        traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    roof = {"bound": "hbm", "achieved": kern[dom]["achieved_GBs"], "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": kern[dom]["frac"], "traffic": traffic, "kernel": dom}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.rounds, mix, args.cpu_seconds)
+
+    if rank == 0:
+        workload = ("%d x %s-round BLAKE2f compressions per GPU: Table16 witness fill + "
+                    "constraint eval (LAYOUT v1)" % (n, "{1,4,12}-mixed" if mix else args.rounds))
+        out = {"metric": "BLAKE2f compressions/sec (witness+constraint eval), 2^18 batch, "
+                         "1/2/4/8 GPU",
+               "value": round(value, 1), "unit": "compressions/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+               "data": "synthetic (seeded splitmix64 h/m/t/f)",
+               "config": {"workload": workload, "batch_per_gpu": n,
+                          "rounds": "mix{1,4,12}" if mix else args.rounds,
+                          "rows_per_gpu": rows, "trace_bytes_per_gpu": rows * ROW_BYTES,
+                          "parallelism": "dp%d (instance shards)" % world},
+               "roofline": roof, "cpu_baseline": cpu, "kernels": kern,
+               "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

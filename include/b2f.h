@@ -1,0 +1,148 @@
+/*
+ * b2f.h -- C ABI of the MI355X (gfx950) BLAKE2f Table16 witness-fill and constraint-eval
+ * engine. Plain pointers and sizes only; no torch or HIP types in the signatures
+ * (`stream` is an opaque hipStream_t, NULL = the default stream).
+ *
+ * Drop-in point: the reference's gadget boundary `Blake2fInstructions<F>`
+ * (blake2f-circuit/src/blake2f.rs:40-72), implemented by `Table16Chip`
+ * (blake2f-circuit/src/blake2f/table16.rs:338-384), whose region drivers
+ * `CompressionConfig::{initialize_with_iv, initialize_with_state, compress, digest}`
+ * (table16/compression.rs:1078-1149) assign the trace cell by cell; and the batch entry the
+ * reference sketches, `Blake2fChip::construct(config, Vec<Blake2fWitness>)` +
+ * `chip.load(&mut layouter)` checked by `MockProver::run(k, ..).verify()`
+ * (blake2f.rs:250-303, commented out there). One b2f_fill call assigns every region of a
+ * batch of independent compressions; one b2f_eval call is the MockProver check of the
+ * resulting trace. The trace contract is docs/LAYOUT.md (LAYOUT v1).
+ *
+ * Threading: one context per device, externally synchronized. `*_dev` calls are
+ * stream-ordered and asynchronous; b2f_sync() waits and returns any device-side error.
+ * Host-pointer calls block. No call aborts; errors come back as B2F_* status codes with a
+ * message in b2f_last_error(). They map onto halo2's plonk::Error at a Rust call site:
+ * B2F_ERR_ROWS -> NotEnoughRowsAvailable, the others -> Synthesis.
+ */
+#ifndef B2F_H
+#define B2F_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define B2F_API __attribute__((visibility("default")))
+
+#define B2F_NUM_ADVICE 10      /* a_0..a_9, table16.rs:281-309 */
+#define B2F_NUM_GATES 16       /* selector bits, docs/LAYOUT.md §4 */
+#define B2F_CODE_LOOKUP 16
+#define B2F_CODE_COPY 17
+#define B2F_MAX_ROUNDS (1u << 20)
+
+/* Status codes */
+#define B2F_OK 0
+#define B2F_ERR_ARG 1       /* null pointer, misaligned buffer, total_rows % 4 != 0 */
+#define B2F_ERR_ROUNDS 2    /* rounds > B2F_MAX_ROUNDS */
+#define B2F_ERR_ROWS 3      /* buffers hold fewer rows than the batch needs */
+#define B2F_ERR_HIP 4       /* HIP runtime error */
+#define B2F_ERR_LAYOUT 5    /* offsets are not the prefix sums of R(rounds_i) */
+#define B2F_ERR_INPUT 6     /* malformed EIP-152 input (length != 213 or f not 0/1) */
+
+/* One EIP-152 compression: the reference's Blake2fWitness{rounds, h, m, t, f}
+ * (blake2f.rs:208-239), 216 bytes, naturally aligned. f must be 0 or 1. */
+typedef struct {
+    uint64_t h[8];
+    uint64_t m[16];
+    uint64_t t[2];
+    uint32_t rounds;
+    uint32_t f;
+} b2f_input;
+
+/* MockProver-equivalent verdict (docs/LAYOUT.md §6). first_failure = min over all failures
+ * of (row << 8) | code (code = selector bit 0..15, B2F_CODE_LOOKUP, B2F_CODE_COPY),
+ * UINT64_MAX when every constraint holds. */
+typedef struct {
+    uint64_t gate_failures[B2F_NUM_GATES];
+    uint64_t lookup_failures;
+    uint64_t copy_failures;
+    uint64_t first_failure;
+    uint64_t rows_checked;
+} b2f_eval_report;
+
+typedef struct b2f_ctx b2f_ctx;
+
+B2F_API int b2f_version(void);
+
+/* Rows of one instance, R(rounds) = 228 + 416*rounds (LAYOUT.md §5). Replaces the SHA row
+ * map of compression_util.rs:32-205. Returns 0 when rounds > B2F_MAX_ROUNDS. */
+B2F_API uint64_t b2f_layout_rows(uint32_t rounds);
+
+/* offsets[0..n]: row offset of every instance region, i.e. where each `assign_region` of
+ * compression.rs:1084/1120/1140 lands in the batch. Host function. */
+B2F_API int b2f_layout_offsets(const b2f_input* in, size_t n, uint64_t* offsets);
+
+/* halo2 advice-column index of a_i in the reference's allocation order
+ * (table16.rs:281-294: a_5, a_3, a_4, a_6, a_7, a_8, a_9, a_0, a_1, a_2); -1 if i > 9. */
+B2F_API int b2f_halo2_column_index(int a_i);
+
+/* Parse one 213-byte EIP-152 precompile input (rounds u32 BE | h 64 B | m 128 B | t 16 B |
+ * f 1 B; words little-endian), the format of the reference KAT (blake2f.rs:193-247). */
+B2F_API int b2f_parse_eip152(const uint8_t* raw, size_t len, b2f_input* out);
+
+/* Context bound to one HIP device (owns scratch, events, the device status words). */
+B2F_API b2f_ctx* b2f_create(int device);
+B2F_API void b2f_destroy(b2f_ctx* ctx);
+B2F_API const char* b2f_last_error(const b2f_ctx* ctx);
+
+/* Witness fill, device pointers. Replaces CompressionConfig::{initialize_with_iv,
+ * compress, digest} (compression.rs:1078-1149) with their helpers
+ * (compression_util.rs:208-890, subregion_initial.rs:11-155, SpreadVar::with_lookup
+ * spread_table.rs:257-285, AssignedBits::assign_bits table16.rs:136-167) for n instances.
+ *   d_in        n records (16-B aligned)
+ *   d_offsets   n+1 row offsets (b2f_layout_offsets)
+ *   total_rows  rows of the buffers (>= offsets[n], multiple of 4); rows past offsets[n]
+ *               are written as zeros
+ *   d_advice    column-major uint32 [10][total_rows] (16-B aligned); cell a_c of row r at
+ *               d_advice[c * total_rows + r]
+ *   d_fixed     uint32 [total_rows]: selector mask (bits 0..15) | constant k_0 << 16
+ *   d_h_out     n * 8 uint64 compression outputs h' (may be NULL)
+ * Asynchronous on `stream`. */
+B2F_API int b2f_fill_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
+                         const uint64_t* d_offsets, uint64_t total_rows, uint32_t* d_advice,
+                         uint32_t* d_fixed, uint64_t* d_h_out, void* stream);
+
+/* Constraint evaluation over a trace, device pointers: the `MockProver::verify` of
+ * blake2f.rs:301-302 -- every gate of compression.rs:604-1056 (as re-derived in
+ * LAYOUT.md §4), the spread lookup of spread_table.rs:443-453 on every row, and every
+ * copy constraint (`copy_advice`). d_report is overwritten. Asynchronous on `stream`. */
+B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t* d_fixed,
+                         const uint64_t* d_offsets, size_t n, uint64_t total_rows,
+                         b2f_eval_report* d_report, void* stream);
+
+/* Wait for `stream` and return the first device-side error of the fill/eval calls issued
+ * since the previous b2f_sync (B2F_ERR_LAYOUT / B2F_ERR_ROUNDS), then clear it. */
+B2F_API int b2f_sync(b2f_ctx* ctx, void* stream);
+
+/* Host-pointer conveniences (allocate, copy, run, copy back; blocking). b2f_fill sizes the
+ * trace to exactly offsets[n] rows; advice must hold 10*offsets[n] and fixed offsets[n]. */
+B2F_API int b2f_fill(b2f_ctx* ctx, const b2f_input* in, size_t n, uint32_t* advice,
+                     uint32_t* fixed, uint64_t* h_out);
+B2F_API int b2f_eval(b2f_ctx* ctx, const uint32_t* advice, const uint32_t* fixed,
+                     const uint64_t* offsets, size_t n, uint64_t total_rows,
+                     b2f_eval_report* report);
+
+/* Per-kernel timing with HIP events recorded on the launch stream around every kernel the
+ * fill/eval calls launch (no host synchronization while recording). b2f_set_timing(ctx, 1)
+ * clears the log and starts recording; b2f_kernel_times waits for the recorded events and
+ * returns, per kernel kind, the summed duration (ms) and the launch count, then clears the
+ * log. Kinds: */
+#define B2F_KERNEL_RECORD 0 /* BLAKE2f compression + half-round states (fill, part 1) */
+#define B2F_KERNEL_FILL 1   /* trace expansion (fill, part 2) */
+#define B2F_KERNEL_EVAL 2   /* constraint evaluation */
+#define B2F_NUM_KERNELS 3
+B2F_API int b2f_set_timing(b2f_ctx* ctx, int enable);
+B2F_API int b2f_kernel_times(b2f_ctx* ctx, double* total_ms, uint32_t* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* B2F_H */

@@ -1,0 +1,75 @@
+/*
+ * b2f_oracle.h -- CPU restatement of the reference BLAKE2f Table16 chip's witness fill and
+ * MockProver check, per docs/LAYOUT.md (LAYOUT v1).
+ *
+ * TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the timed CPU baseline.
+ * The product path (zk-odst_amd/, include/b2f.h) never links or calls it.
+ *
+ * Parity status: BLAKE2f final states pinned to the reference KAT
+ * (blake2f-circuit/src/blake2f.rs:193-247), to hashlib.blake2b and to rounds=0 vectors
+ * (tests/golden/). The trace layout restates docs/LAYOUT.md; the reference's own layout
+ * cannot be built or run, so the layout itself is pinned only by
+ * its spread-table fixtures (spread_table.rs:684-724) and by the gate/lookup/copy
+ * verdict of this oracle's own eval.
+ */
+#ifndef B2F_ORACLE_H
+#define B2F_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Mirrors one EIP-152 compression record (blake2f.rs:208-239). */
+typedef struct {
+    uint64_t h[8];
+    uint64_t m[16];
+    uint64_t t[2];
+    uint32_t rounds;
+    uint32_t f;
+} orc_input;
+
+#define ORC_NCOLS 10
+#define ORC_NGATES 16
+#define ORC_CODE_LOOKUP 16
+#define ORC_CODE_COPY 17
+
+typedef struct {
+    uint64_t gate_failures[ORC_NGATES];
+    uint64_t lookup_failures;
+    uint64_t copy_failures;
+    uint64_t first_failure;  /* min((row << 8) | code), UINT64_MAX if none */
+    uint64_t rows_checked;
+} orc_report;
+
+/* R(rounds) = 228 + 416 * rounds (LAYOUT.md §5). */
+uint64_t orc_rows(uint32_t rounds);
+/* offsets[0..n] prefix sums of R(rounds_i). */
+void orc_offsets(const orc_input* in, size_t n, uint64_t* offsets);
+/* Copy constraints of one instance: writes up to cap (dst_row, dst_col, src_row, src_col)
+ * quadruples (instance-relative rows); returns the count. */
+size_t orc_copies(uint32_t rounds, uint32_t* out4, size_t cap);
+
+/* RFC 7693 / EIP-152 compression F (README.md:1-97), any rounds. */
+void orc_compress(uint32_t rounds, const uint64_t h[8], const uint64_t m[16],
+                  const uint64_t t[2], uint32_t f, uint64_t out[8]);
+
+/* Fill the trace: advice is column-major [10][total_rows], fixed is [total_rows]. Both are
+ * overwritten in full (cells this layout does not use are 0). h_out may be NULL.
+ * nthreads <= 0 means OpenMP default. Returns 0, or -1 on inconsistent offsets. */
+int orc_fill(const orc_input* in, size_t n, const uint64_t* offsets, uint64_t total_rows,
+             uint32_t* advice, uint32_t* fixed, uint64_t* h_out, int nthreads);
+
+/* MockProver-equivalent check of a trace (LAYOUT.md §6). Returns 0, or -1 when an
+ * instance's row count is not R(rounds) for any rounds. */
+int orc_eval(const uint32_t* advice, const uint32_t* fixed, const uint64_t* offsets, size_t n,
+             uint64_t total_rows, orc_report* rep, int nthreads);
+
+int orc_max_threads(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,130 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle_b2f.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker or the timed CPU baseline. The product package
+(zk-odst_amd/b2f) never imports this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle_b2f.so")
+
+NCOLS = 10
+NGATES = 16
+CODE_LOOKUP = 16
+CODE_COPY = 17
+
+# orc_input (b2f_oracle.h) as a numpy record: 216 bytes
+INPUT_DTYPE = np.dtype([("h", "<u8", (8,)), ("m", "<u8", (16,)), ("t", "<u8", (2,)),
+                        ("rounds", "<u4"), ("f", "<u4")])
+assert INPUT_DTYPE.itemsize == 216
+
+
+class Report(ctypes.Structure):
+    _fields_ = [("gate_failures", ctypes.c_uint64 * NGATES),
+                ("lookup_failures", ctypes.c_uint64),
+                ("copy_failures", ctypes.c_uint64),
+                ("first_failure", ctypes.c_uint64),
+                ("rows_checked", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {"gate_failures": list(self.gate_failures),
+                "lookup_failures": self.lookup_failures,
+                "copy_failures": self.copy_failures,
+                "first_failure": self.first_failure,
+                "rows_checked": self.rows_checked}
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        L.orc_rows.argtypes = [ctypes.c_uint32]
+        L.orc_rows.restype = ctypes.c_uint64
+        L.orc_offsets.argtypes = [P, ctypes.c_size_t, P]
+        L.orc_copies.argtypes = [ctypes.c_uint32, P, ctypes.c_size_t]
+        L.orc_copies.restype = ctypes.c_size_t
+        L.orc_compress.argtypes = [ctypes.c_uint32, P, P, P, ctypes.c_uint32, P]
+        L.orc_fill.argtypes = [P, ctypes.c_size_t, P, ctypes.c_uint64, P, P, P, ctypes.c_int]
+        L.orc_fill.restype = ctypes.c_int
+        L.orc_eval.argtypes = [P, P, P, ctypes.c_size_t, ctypes.c_uint64, P, ctypes.c_int]
+        L.orc_eval.restype = ctypes.c_int
+        L.orc_max_threads.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def rows(rounds):
+    return int(lib().orc_rows(rounds))
+
+
+def offsets(inputs):
+    inputs = np.ascontiguousarray(inputs, dtype=INPUT_DTYPE)
+    off = np.zeros(len(inputs) + 1, dtype=np.uint64)
+    lib().orc_offsets(_p(inputs), len(inputs), _p(off))
+    return off
+
+
+def copies(rounds):
+    n = lib().orc_copies(rounds, None, 0)
+    out = np.zeros((n, 4), dtype=np.uint32)
+    lib().orc_copies(rounds, _p(out), n)
+    return out
+
+
+def compress(rounds, h, m, t, f):
+    h = np.ascontiguousarray(h, dtype=np.uint64)
+    m = np.ascontiguousarray(m, dtype=np.uint64)
+    t = np.ascontiguousarray(t, dtype=np.uint64)
+    out = np.zeros(8, dtype=np.uint64)
+    lib().orc_compress(rounds, _p(h), _p(m), _p(t), int(bool(f)), _p(out))
+    return out
+
+
+def fill(inputs, total_rows=None, nthreads=0):
+    """Returns (advice [10, total_rows] u32, fixed [total_rows] u32, h_out [n, 8] u64, offsets)."""
+    inputs = np.ascontiguousarray(inputs, dtype=INPUT_DTYPE)
+    off = offsets(inputs)
+    total = int(off[-1]) if total_rows is None else int(total_rows)
+    adv = np.empty((NCOLS, total), dtype=np.uint32)
+    fixed = np.empty(total, dtype=np.uint32)
+    h_out = np.zeros((len(inputs), 8), dtype=np.uint64)
+    rc = lib().orc_fill(_p(inputs), len(inputs), _p(off), total, _p(adv), _p(fixed), _p(h_out),
+                        nthreads)
+    if rc != 0:
+        raise ValueError("orc_fill: inconsistent offsets")
+    return adv, fixed, h_out, off
+
+
+def evaluate(adv, fixed, off, nthreads=0):
+    adv = np.ascontiguousarray(adv, dtype=np.uint32)
+    fixed = np.ascontiguousarray(fixed, dtype=np.uint32)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    rep = Report()
+    rc = lib().orc_eval(_p(adv), _p(fixed), _p(off), len(off) - 1, adv.shape[1],
+                        ctypes.byref(rep), nthreads)
+    if rc != 0:
+        raise ValueError("orc_eval: offsets are not a LAYOUT v1 row map")
+    return rep.as_dict()
+
+
+def max_threads():
+    return int(lib().orc_max_threads())

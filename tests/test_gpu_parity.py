@@ -1,0 +1,161 @@
+"""GPU parity: the HIP fill/eval (through the C ABI) against the CPU oracle, bit for bit.
+
+Every test here needs an MI355X (`-m gpu`)."""
+import numpy as np
+import pytest
+
+from conftest import random_inputs, words
+
+pytestmark = pytest.mark.gpu
+
+
+def _as_oracle(x, orc):
+    return np.frombuffer(x.tobytes(), dtype=orc.INPUT_DTYPE).copy()
+
+
+@pytest.mark.parametrize("rounds_choices,n,seed", [((12,), 8, 1), ((0, 1, 4, 12), 97, 2),
+                                                   ((1,), 33, 3), ((13, 20, 25), 11, 4)])
+def test_fill_bitexact_vs_oracle(engine, orc, rounds_choices, n, seed):
+    x = random_inputs(n, rounds_choices, seed)
+    adv, fixed, h_out, off = engine.fill_host(x)
+    oadv, ofixed, oh, ooff = orc.fill(_as_oracle(x, orc))
+    assert np.array_equal(off, ooff)
+    for c in range(10):
+        bad = np.nonzero(adv[c] != oadv[c])[0]
+        assert bad.size == 0, "column a_%d differs at rows %s" % (c, bad[:10])
+    assert np.array_equal(fixed, ofixed)
+    assert np.array_equal(h_out, oh)
+
+
+def test_eval_clean_matches_oracle(engine, orc):
+    x = random_inputs(50, (0, 1, 4, 12), 5)
+    adv, fixed, h_out, off = engine.fill_host(x)
+    rep = engine.eval_host(adv, fixed, off)
+    assert rep == orc.evaluate(adv, fixed, off)
+    assert rep["first_failure"] == 2**64 - 1 and rep["rows_checked"] == int(off[-1])
+    assert sum(rep["gate_failures"]) == rep["lookup_failures"] == rep["copy_failures"] == 0
+
+
+def test_eval_corruptions_match_oracle(engine, orc):
+    """Flip cells all over the trace; the GPU verdict must equal the oracle's exactly."""
+    x = random_inputs(6, (0, 1, 2), 6)
+    adv, fixed, h_out, off = engine.fill_host(x)
+    rng = np.random.default_rng(7)
+    total = adv.shape[1]
+    cases = [(c, r) for c in range(10) for r in rng.integers(0, total, 40)]
+    flagged = 0
+    for c, r in cases:
+        a2 = adv.copy()
+        a2[c, r] ^= np.uint32(1 << int(rng.integers(0, 20)))
+        g = engine.eval_host(a2, fixed, off)
+        o = orc.evaluate(a2, fixed, off)
+        assert g == o, (c, r, g, o)
+        flagged += g["first_failure"] != 2**64 - 1
+    assert flagged > len(cases) // 3
+    # selector / constant corruption in the fixed column
+    for r in rng.integers(0, total, 40):
+        f2 = fixed.copy()
+        f2[r] ^= np.uint32(1 << int(rng.integers(0, 32)))
+        assert engine.eval_host(adv, f2, off) == orc.evaluate(adv, f2, off)
+
+
+def test_h_out_golden(engine, golden):
+    import b2f
+
+    kat = golden["kat"]
+    x = np.zeros(1, dtype=b2f.INPUT_DTYPE)
+    x["h"], x["m"], x["t"] = words(kat["h"]), words(kat["m"]), words(kat["t"])
+    x["f"], x["rounds"] = kat["f"], kat["rounds"]
+    _, _, h_out, _ = engine.fill_host(x)
+    assert h_out[0].astype("<u8").tobytes().hex() == kat["expected"]
+    for case in golden["rounds0"]:
+        x = np.zeros(1, dtype=b2f.INPUT_DTYPE)
+        x["h"], x["m"], x["t"] = words(case["h"]), words(case["m"]), words(case["t"])
+        x["f"], x["rounds"] = case["f"], 0
+        _, _, h_out, _ = engine.fill_host(x)
+        assert h_out[0].astype("<u8").tobytes().hex() == case["expected"]
+
+
+def test_hash_chains_golden(engine, golden):
+    """hashlib.blake2b digests as chains of GPU compressions (f = 0 on inner blocks)."""
+    import b2f
+
+    cases = golden["hash_cases"]
+    states = [words(c["h"]) for c in cases]
+    depth = max(len(c["chain"]) for c in cases)
+    for step in range(depth):
+        live = [i for i, c in enumerate(cases) if step < len(c["chain"])]
+        x = np.zeros(len(live), dtype=b2f.INPUT_DTYPE)
+        for j, i in enumerate(live):
+            blk = cases[i]["chain"][step]
+            x[j]["h"], x[j]["m"], x[j]["t"] = states[i], words(blk["m"]), words(blk["t"])
+            x[j]["f"], x[j]["rounds"] = blk["f"], blk["rounds"]
+        adv, fixed, h_out, off = engine.fill_host(x)
+        assert engine.eval_host(adv, fixed, off)["first_failure"] == 2**64 - 1
+        for j, i in enumerate(live):
+            states[i] = h_out[j]
+    for i, c in enumerate(cases):
+        got = states[i].astype("<u8").tobytes()[: c["digest_size"]].hex()
+        assert got == c["digest"], c["name"]
+
+
+def test_layout_errors(engine):
+    import b2f
+    import torch
+
+    x = random_inputs(4, (1,), 8)
+    batch = b2f.DeviceBatch(x)
+    batch.offsets[2] += 4  # not a LAYOUT v1 prefix sum any more
+    batch.fill(engine)
+    with pytest.raises(b2f.B2FError) as ei:
+        engine.sync(torch.cuda.current_stream().cuda_stream)
+    assert ei.value.code == 5
+    with pytest.raises(b2f.B2FError):
+        engine.fill_dev(batch.inputs.data_ptr(), 4, batch.offsets.data_ptr(), 6,
+                        batch.advice.data_ptr(), batch.fixed.data_ptr(), 0)
+
+
+def test_device_batch_2p16_bitexact(engine, orc):
+    """BASELINE config 2: 2^16 x 12 rounds, full column diff against the oracle, streamed
+    in chunks of instances so host memory stays bounded."""
+    import b2f
+    import torch
+
+    from b2f import synth
+
+    n = 1 << 16
+    x = synth.batch(n, rounds=12)
+    batch = b2f.DeviceBatch(x)
+    batch.fill(engine)
+    batch.evaluate(engine)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    rep = batch.report_dict()
+    assert rep["first_failure"] == 2**64 - 1 and sum(rep["gate_failures"]) == 0
+    h_out = batch.host_h_out()
+    off = batch.offsets_host
+    chunk = 4096
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        oadv, ofixed, oh, ooff = orc.fill(_as_oracle(x[s:e], orc))
+        r0, r1 = int(off[s]), int(off[e])
+        gadv = batch.advice[:, r0:r1].cpu().numpy().view(np.uint32)
+        gfx = batch.fixed[r0:r1].cpu().numpy().view(np.uint32)
+        assert np.array_equal(gadv, oadv), "advice differs in instances [%d, %d)" % (s, e)
+        assert np.array_equal(gfx, ofixed)
+        assert np.array_equal(h_out[s:e], oh)
+
+
+def test_padded_tail_rows_zero(engine, orc):
+    import b2f
+    import torch
+
+    x = random_inputs(3, (1,), 9)
+    batch = b2f.DeviceBatch(x, total_rows=int(b2f.offsets(x)[-1]) + 64)
+    batch.advice.fill_(-1)
+    batch.fill(engine)
+    batch.evaluate(engine)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    adv, fixed = batch.host_trace()
+    used = batch.used_rows
+    assert not adv[:, used:].any() and not fixed[used:].any()
+    assert batch.report_dict() == orc.evaluate(adv, fixed, batch.offsets_host)

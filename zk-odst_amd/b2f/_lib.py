@@ -1,0 +1,111 @@
+"""ctypes binding of the C ABI in include/b2f.h (libb2f.so, built in-tree by
+__graft_entry__.build() / `make -C zk-odst_amd`).
+
+There is no fallback: if the HIP library is missing or fails to load, every entry point
+raises. The product path never touches oracle/.
+"""
+import ctypes
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # zk-odst_amd/
+LIB_PATH = os.path.join(PKG_ROOT, "libb2f.so")
+HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "b2f.h")
+
+NUM_ADVICE = 10
+NUM_GATES = 16
+CODE_LOOKUP = 16
+CODE_COPY = 17
+MAX_ROUNDS = 1 << 20
+KERNEL_NAMES = ["record", "fill", "eval"]  # B2F_KERNEL_RECORD/FILL/EVAL
+
+OK, ERR_ARG, ERR_ROUNDS, ERR_ROWS, ERR_HIP, ERR_LAYOUT, ERR_INPUT = range(7)
+STATUS_NAMES = {OK: "OK", ERR_ARG: "B2F_ERR_ARG", ERR_ROUNDS: "B2F_ERR_ROUNDS",
+                ERR_ROWS: "B2F_ERR_ROWS", ERR_HIP: "B2F_ERR_HIP", ERR_LAYOUT: "B2F_ERR_LAYOUT",
+                ERR_INPUT: "B2F_ERR_INPUT"}
+
+
+class B2FError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s: %s" % (STATUS_NAMES.get(code, code), msg))
+        self.code = code
+
+
+class EvalReport(ctypes.Structure):
+    _fields_ = [("gate_failures", ctypes.c_uint64 * NUM_GATES),
+                ("lookup_failures", ctypes.c_uint64),
+                ("copy_failures", ctypes.c_uint64),
+                ("first_failure", ctypes.c_uint64),
+                ("rows_checked", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {"gate_failures": list(self.gate_failures),
+                "lookup_failures": self.lookup_failures,
+                "copy_failures": self.copy_failures,
+                "first_failure": self.first_failure,
+                "rows_checked": self.rows_checked}
+
+
+REPORT_BYTES = ctypes.sizeof(EvalReport)
+
+# (name, restype, argtypes) for every function include/b2f.h declares.
+P = ctypes.c_void_p
+U64 = ctypes.c_uint64
+SIZE = ctypes.c_size_t
+I32 = ctypes.c_int
+SIGNATURES = [
+    ("b2f_version", I32, []),
+    ("b2f_layout_rows", U64, [ctypes.c_uint32]),
+    ("b2f_layout_offsets", I32, [P, SIZE, P]),
+    ("b2f_halo2_column_index", I32, [I32]),
+    ("b2f_parse_eip152", I32, [P, SIZE, P]),
+    ("b2f_create", P, [I32]),
+    ("b2f_destroy", None, [P]),
+    ("b2f_last_error", ctypes.c_char_p, [P]),
+    ("b2f_fill_dev", I32, [P, P, SIZE, P, U64, P, P, P, P]),
+    ("b2f_eval_dev", I32, [P, P, P, P, SIZE, U64, P, P]),
+    ("b2f_sync", I32, [P, P]),
+    ("b2f_fill", I32, [P, P, SIZE, P, P, P]),
+    ("b2f_eval", I32, [P, P, P, P, SIZE, U64, P]),
+    ("b2f_set_timing", I32, [P, I32]),
+    ("b2f_kernel_times", I32, [P, P, P]),
+]
+
+_lib = None
+
+
+def _share_hip_runtime_with_torch():
+    """One HIP runtime per process. PyTorch-ROCm ships its own libamdhip64 (soname
+    libamdhip64.so.7, the same soname /opt/rocm's has); if libb2f.so is loaded first, torch
+    later maps its own copy as a second runtime and then sees no GPUs. Importing torch
+    first makes the dynamic linker satisfy libb2f.so's libamdhip64.so.7 with torch's copy, so
+    torch tensors, torch streams and the b2f kernels share one runtime. Without torch in the
+    process, /opt/rocm's runtime is used."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
+def load():
+    """Load libb2f.so (raises OSError with a build hint when it is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError("libb2f.so not found at %s: build it with "
+                      "`python -c 'import __graft_entry__ as g; g.build()'` or "
+                      "`make -C zk-odst_amd`" % LIB_PATH)
+    _share_hip_runtime_with_torch()
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(ctx, rc):
+    if rc != OK:
+        msg = load().b2f_last_error(ctx)
+        raise B2FError(rc, msg.decode() if msg else "")

@@ -1,0 +1,140 @@
+"""Engine: one b2f_ctx on one HIP device, plus torch-allocated device trace buffers.
+
+PyTorch is plumbing here (device memory, the stream handle); the work is the HIP kernels
+behind include/b2f.h.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .layout import INPUT_DTYPE, as_inputs, offsets as layout_offsets
+
+
+def _vp(x):
+    return ctypes.c_void_p(int(x))
+
+
+def _np_ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class Engine:
+    """Wraps b2f_create/b2f_destroy and the fill/eval entry points."""
+
+    def __init__(self, device=0):
+        self.lib = _lib.load()
+        self.device = int(device)
+        self.ctx = self.lib.b2f_create(self.device)
+        if not self.ctx:
+            raise _lib.B2FError(_lib.ERR_HIP, "b2f_create(%d) failed (no such HIP device?)" % device)
+
+    def close(self):
+        if self.ctx:
+            self.lib.b2f_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        _lib.check(self.ctx, rc)
+
+    # ---------------------------------------------------------------- host-pointer calls
+    def fill_host(self, inputs):
+        """inputs: INPUT_DTYPE records. Returns (advice[10, R] u32, fixed[R] u32,
+        h_out[n, 8] u64, offsets[n+1])."""
+        inputs = as_inputs(inputs)
+        off = layout_offsets(inputs)
+        total = int(off[-1])
+        adv = np.empty((_lib.NUM_ADVICE, total), dtype=np.uint32)
+        fixed = np.empty(total, dtype=np.uint32)
+        h_out = np.empty((len(inputs), 8), dtype=np.uint64)
+        self._check(self.lib.b2f_fill(self.ctx, _np_ptr(inputs), len(inputs), _np_ptr(adv),
+                                      _np_ptr(fixed), _np_ptr(h_out)))
+        return adv, fixed, h_out, off
+
+    def eval_host(self, adv, fixed, off):
+        adv = np.ascontiguousarray(adv, dtype=np.uint32)
+        fixed = np.ascontiguousarray(fixed, dtype=np.uint32)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        rep = _lib.EvalReport()
+        self._check(self.lib.b2f_eval(self.ctx, _np_ptr(adv), _np_ptr(fixed), _np_ptr(off),
+                                      len(off) - 1, adv.shape[1], ctypes.byref(rep)))
+        return rep.as_dict()
+
+    # ---------------------------------------------------------------- device-pointer calls
+    def fill_dev(self, d_in, n, d_off, total_rows, d_adv, d_fixed, d_h_out, stream=0):
+        self._check(self.lib.b2f_fill_dev(self.ctx, _vp(d_in), n, _vp(d_off), int(total_rows),
+                                          _vp(d_adv), _vp(d_fixed),
+                                          _vp(d_h_out) if d_h_out else None, _vp(stream)))
+
+    def eval_dev(self, d_adv, d_fixed, d_off, n, total_rows, d_report, stream=0):
+        self._check(self.lib.b2f_eval_dev(self.ctx, _vp(d_adv), _vp(d_fixed), _vp(d_off), n,
+                                          int(total_rows), _vp(d_report), _vp(stream)))
+
+    def sync(self, stream=0):
+        self._check(self.lib.b2f_sync(self.ctx, _vp(stream)))
+
+    def set_timing(self, enable=True):
+        self._check(self.lib.b2f_set_timing(self.ctx, 1 if enable else 0))
+
+    def kernel_times(self):
+        """{kernel: (total_ms, launches)} since set_timing(True) / the previous call."""
+        tot = (ctypes.c_double * 3)()
+        cnt = (ctypes.c_uint32 * 3)()
+        self._check(self.lib.b2f_kernel_times(self.ctx, tot, cnt))
+        return {name: (float(tot[i]), int(cnt[i])) for i, name in enumerate(_lib.KERNEL_NAMES)}
+
+
+class DeviceBatch:
+    """A batch resident on one GPU: inputs, offsets, the trace and the outputs, as torch
+    tensors (int32/int64 storage holding u32/u64 bit patterns)."""
+
+    def __init__(self, inputs, device="cuda:0", total_rows=None):
+        import torch
+
+        self.torch = torch
+        inputs = as_inputs(inputs)
+        self.n = len(inputs)
+        off = layout_offsets(inputs)
+        self.offsets_host = off
+        self.used_rows = int(off[-1])
+        self.total_rows = int(total_rows) if total_rows is not None else self.used_rows
+        if self.total_rows < self.used_rows or self.total_rows % 4:
+            raise _lib.B2FError(_lib.ERR_ROWS, "total_rows %d (need >= %d, multiple of 4)"
+                                % (self.total_rows, self.used_rows))
+        dev = torch.device(device)
+        raw = np.frombuffer(inputs.tobytes(), dtype=np.uint8)
+        self.inputs = torch.from_numpy(raw.copy()).to(dev)
+        self.offsets = torch.from_numpy(off.view(np.int64).copy()).to(dev)
+        self.advice = torch.empty((_lib.NUM_ADVICE, self.total_rows), dtype=torch.int32, device=dev)
+        self.fixed = torch.empty(self.total_rows, dtype=torch.int32, device=dev)
+        self.h_out = torch.empty((self.n, 8), dtype=torch.int64, device=dev)
+        self.report = torch.empty(_lib.REPORT_BYTES // 8, dtype=torch.int64, device=dev)
+
+    def fill(self, eng, stream=None):
+        s = stream if stream is not None else self.torch.cuda.current_stream().cuda_stream
+        eng.fill_dev(self.inputs.data_ptr(), self.n, self.offsets.data_ptr(), self.total_rows,
+                     self.advice.data_ptr(), self.fixed.data_ptr(), self.h_out.data_ptr(), s)
+
+    def evaluate(self, eng, stream=None):
+        s = stream if stream is not None else self.torch.cuda.current_stream().cuda_stream
+        eng.eval_dev(self.advice.data_ptr(), self.fixed.data_ptr(), self.offsets.data_ptr(),
+                     self.n, self.total_rows, self.report.data_ptr(), s)
+
+    def report_dict(self):
+        raw = self.report.cpu().numpy().view(np.uint64)
+        rep = _lib.EvalReport.from_buffer_copy(raw.tobytes())
+        return rep.as_dict()
+
+    def host_trace(self):
+        adv = self.advice.cpu().numpy().view(np.uint32)
+        fixed = self.fixed.cpu().numpy().view(np.uint32)
+        return adv, fixed
+
+    def host_h_out(self):
+        return self.h_out.cpu().numpy().view(np.uint64)
