@@ -1,0 +1,92 @@
+"""The C ABI library loads and exports every function include/b2f.h declares; the
+host-only entry points (no GPU needed) behave as documented."""
+import ctypes
+import re
+import struct
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, random_inputs
+
+
+def declared_functions():
+    src = open(ROOT + "/include/b2f.h").read()
+    return re.findall(r"B2F_API\s+[\w\s\*]+?\b(b2f_\w+)\s*\(", src)
+
+
+def test_all_declared_symbols_exported():
+    import b2f
+    from b2f import _lib
+
+    lib = b2f.load()
+    names = declared_functions()
+    assert len(names) >= 15
+    for name in names:
+        assert hasattr(lib, name), name
+    assert sorted(names) == sorted(n for n, _, _ in _lib.SIGNATURES)
+
+
+def test_layout_rows_and_offsets(orc):
+    import b2f
+
+    for r in (0, 1, 4, 12, 1000):
+        assert b2f.rows(r) == 228 + 416 * r == orc.rows(r)
+    with pytest.raises(b2f.B2FError):
+        b2f.rows((1 << 20) + 1)
+    x = random_inputs(17, (0, 1, 4, 12), 21)
+    ox = np.frombuffer(x.tobytes(), dtype=orc.INPUT_DTYPE).copy()
+    assert np.array_equal(b2f.offsets(x), orc.offsets(ox))
+
+
+def test_halo2_column_index():
+    import b2f
+
+    # table16.rs:281-294 allocation order: message_schedule (a_5), extras (a_3,a_4,a_6..a_9),
+    # then the lookup inputs a_0, a_1, a_2
+    assert [b2f.halo2_column_index(i) for i in range(10)] == [7, 8, 9, 1, 2, 0, 3, 4, 5, 6]
+    assert b2f.halo2_column_index(10) == -1
+
+
+def _eip152(rounds, h, m, t, f):
+    return (struct.pack(">I", rounds) + struct.pack("<8Q", *h) + struct.pack("<16Q", *m)
+            + struct.pack("<2Q", *t) + bytes([f]))
+
+
+def test_parse_eip152(golden):
+    import b2f
+
+    k = golden["kat"]
+    h = [int(w, 16) for w in k["h"]]
+    m = [int(w, 16) for w in k["m"]]
+    raw = _eip152(12, h, m, [3, 0], 1)
+    assert len(raw) == 213
+    rec = b2f.parse_eip152(raw)
+    assert rec["rounds"] == 12 and rec["f"] == 1 and list(rec["t"]) == [3, 0]
+    assert [int(v) for v in rec["h"]] == h and [int(v) for v in rec["m"]] == m
+    with pytest.raises(b2f.B2FError) as e:
+        b2f.parse_eip152(raw[:-1])
+    assert e.value.code == 6
+    with pytest.raises(b2f.B2FError):
+        b2f.parse_eip152(raw[:-1] + b"\x02")  # EIP-152: f must be 0 or 1
+
+
+def test_no_device_is_an_error_not_a_fallback():
+    """Without a GPU the engine refuses to start: there is no CPU fallback path."""
+    import torch
+
+    import b2f
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(b2f.B2FError):
+        b2f.Engine(0)
+
+
+def test_null_context_calls_fail_cleanly():
+    import b2f
+
+    lib = b2f.load()
+    assert lib.b2f_fill_dev(None, None, 0, None, 0, None, None, None, None) == 1
+    assert lib.b2f_eval(None, None, None, None, 0, 0, None) == 1
+    assert lib.b2f_last_error(None) == b"null context"

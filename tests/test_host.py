@@ -1,0 +1,62 @@
+"""Host-side logic of the b2f package (CPU only)."""
+import numpy as np
+import pytest
+
+from conftest import random_inputs
+
+
+def test_synth_is_deterministic_and_shardable():
+    from b2f import synth
+
+    a = synth.batch(100, rounds=12)
+    b = synth.batch(100, rounds=12)
+    assert a.tobytes() == b.tobytes()
+    whole = synth.batch(64, rounds_mix=[1, 4, 12])
+    parts = [synth.batch(16, rounds_mix=[1, 4, 12], first=16 * k) for k in range(4)]
+    assert np.concatenate(parts).tobytes() == whole.tobytes()
+    assert set(np.unique(whole["rounds"])) <= {1, 4, 12}
+    assert set(np.unique(whole["f"])) <= {0, 1}
+
+
+def test_split_fixed():
+    from b2f import split_fixed
+
+    fixed = np.array([1 | (0xbeef << 16), 1 << 15, 0, (1 << 14) | (7 << 16)], dtype=np.uint32)
+    sel, const = split_fixed(fixed)
+    assert sel.shape == (16, 4)
+    assert sel[0, 0] and sel[15, 1] and not sel[:, 2].any() and sel[14, 3]
+    assert list(const) == [0xbeef, 0, 0, 7]
+
+
+def test_chip_api_structure():
+    from b2f import chip
+
+    cfg = chip.Blake2fConfig.configure(None, chip.Blake2fTable.construct())
+    assert cfg.advice == ["a_%d" % i for i in range(10)]
+    assert cfg.halo2_index["a_5"] == 0 and cfg.halo2_index["a_2"] == 9
+    assert cfg.selectors[:12] == ["s_decompose_abcd", "s_decompose_efgh", "s_decompose_ijkl",
+                                  "s_spread_a1", "s_spread_b1", "s_spread_c1", "s_spread_d1",
+                                  "s_spread_a2", "s_spread_b2", "s_spread_c2", "s_spread_d2",
+                                  "s_digest"]
+    tag, dense, spread = chip.Blake2fTable.generate()
+    assert (tag[255], tag[256], tag[32767], tag[32768]) == (0, 1, 1, 2)
+    assert spread[0b101] == 0b10001 and spread[0xffff] == 0x55555555
+    x = random_inputs(1, (12,), 31)[0]
+    w = chip.Blake2fWitness(x["rounds"], x["h"], x["m"], x["t"], x["f"])
+    assert w.record().tobytes() == x.tobytes()
+    with pytest.raises(chip.Synthesis):
+        chip.Blake2fWitness(12, [0] * 7, [0] * 16, [0, 0], 0)
+
+
+def test_layouter_row_budget():
+    """NotEnoughRowsAvailable before any device work (k too small for the table or batch)."""
+    from b2f import chip
+
+    x = random_inputs(30, (12,), 32)
+    lay = chip.DeviceLayouter(k=16)
+    with pytest.raises(chip.NotEnoughRowsAvailable) as e:
+        lay.assign_batch(x, engine=None)
+    assert e.value.current_k == 16
+    lay = chip.DeviceLayouter(k=17)  # 131066 usable rows < 30 * 5220
+    with pytest.raises(chip.NotEnoughRowsAvailable):
+        lay.assign_batch(x, engine=None)

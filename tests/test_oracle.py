@@ -1,0 +1,132 @@
+"""The CPU oracle against the golden vectors (pinning it), and its own verdict logic.
+
+CPU only. The oracle is test infrastructure (oracle/b2f_oracle.h)."""
+import numpy as np
+import pytest
+
+from conftest import random_inputs, words
+
+
+def _orc_inputs(x, orc):
+    return np.frombuffer(x.tobytes(), dtype=orc.INPUT_DTYPE).copy()
+
+
+def test_reference_kat(orc, golden):
+    """blake2f.rs:193-247: rounds 12, "abc" -> ba80a53f..."""
+    k = golden["kat"]
+    out = orc.compress(k["rounds"], words(k["h"]), words(k["m"]), words(k["t"]), k["f"])
+    assert out.astype("<u8").tobytes().hex() == k["expected"]
+
+
+def test_rounds0_vectors(orc, golden):
+    for c in golden["rounds0"]:
+        out = orc.compress(0, words(c["h"]), words(c["m"]), words(c["t"]), c["f"])
+        assert out.astype("<u8").tobytes().hex() == c["expected"], c["name"]
+
+
+def test_hashlib_chains(orc, golden):
+    for c in golden["hash_cases"]:
+        h = words(c["h"])
+        for blk in c["chain"]:
+            h = orc.compress(blk["rounds"], h, words(blk["m"]), words(blk["t"]), blk["f"])
+        assert h.astype("<u8").tobytes()[: c["digest_size"]].hex() == c["digest"], c["name"]
+
+
+def test_fill_h_out_equals_compress(orc):
+    x = random_inputs(40, (0, 1, 2, 4, 10, 11, 12, 13), 11)
+    ox = _orc_inputs(x, orc)
+    adv, fixed, h_out, off = orc.fill(ox)
+    for i in range(len(x)):
+        ref = orc.compress(int(x["rounds"][i]), x["h"][i], x["m"][i], x["t"][i], int(x["f"][i]))
+        assert np.array_equal(h_out[i], ref)
+    # the digest cells (a_7, a_8 of each final XOR3 block) hold h' as u32 halves
+    for i in range(len(x)):
+        fb = int(off[i]) + 164 + 416 * int(x["rounds"][i])
+        for w in range(8):
+            lo, hi = int(adv[7, fb + 8 * w]), int(adv[8, fb + 8 * w])
+            assert lo | (hi << 32) == int(h_out[i][w])
+
+
+def test_row_and_copy_counts(orc):
+    for r in (0, 1, 4, 12, 25):
+        assert orc.rows(r) == 228 + 416 * r
+        assert len(orc.copies(r)) == 24 + 576 * r + 96
+    cp = orc.copies(2)
+    # every copy pair: destination is an operand column, source precedes it
+    assert set(cp[:, 1]) <= {3, 4, 5}
+    assert np.all(cp[:, 2] < cp[:, 0])
+    assert len({(int(a), int(b)) for a, b, _, _ in cp}) == len(cp)  # one source per cell
+
+
+def test_clean_trace_and_tail(orc):
+    x = random_inputs(10, (0, 1, 3), 12)
+    ox = _orc_inputs(x, orc)
+    adv, fixed, h_out, off = orc.fill(ox, total_rows=int(orc.offsets(ox)[-1]) + 8)
+    assert not adv[:, -8:].any() and not fixed[-8:].any()
+    rep = orc.evaluate(adv, fixed, off)
+    assert rep["first_failure"] == 2**64 - 1 and rep["rows_checked"] == adv.shape[1]
+
+
+def test_every_used_cell_is_constrained(orc):
+    """Flipping any non-zero cell of a one-round instance is flagged; the only cells that
+    are never flagged are the ones the layout leaves at 0."""
+    x = random_inputs(1, (1,), 13)
+    adv, fixed, h_out, off = orc.fill(_orc_inputs(x, orc))
+    for c in range(10):
+        for r in range(adv.shape[1]):
+            if adv[c, r] == 0:
+                continue
+            a2 = adv.copy()
+            a2[c, r] ^= 1
+            assert orc.evaluate(a2, fixed, off, nthreads=1)["first_failure"] != 2**64 - 1, (c, r)
+
+
+@pytest.mark.parametrize("col,row,code", [
+    (9, 164, 3),        # carry of the first a1 ADD3 -> s_spread_a1
+    (1, 0, 16),         # h_0 limb 0 dense -> lookup (reported before s_decompose_abcd, same row)
+    (3, 168, 17),       # d1 operand spread(d_0) -> copy
+    (7, 0, 0),          # input binding cell -> s_decompose_abcd
+])
+def test_first_failure_codes(orc, col, row, code):
+    x = random_inputs(1, (1,), 14)
+    adv, fixed, h_out, off = orc.fill(_orc_inputs(x, orc))
+    adv[col, row] += 1
+    rep = orc.evaluate(adv, fixed, off)
+    first = rep["first_failure"]
+    assert first >> 8 <= row
+    codes_at_row = first & 0xff
+    if code < 16:
+        assert rep["gate_failures"][code] >= 1
+    elif code == 16:
+        assert rep["lookup_failures"] >= 1
+    else:
+        assert rep["copy_failures"] >= 1
+    assert codes_at_row in range(18)
+
+
+def test_spread_table_rows(orc, golden):
+    """The reference's spread-table fixture rows (spread_table.rs:684-724) are table rows;
+    perturbing tag, dense or spread makes them non-members."""
+    rows = np.array(golden["spread_rows"], dtype=np.uint32)
+    n = (len(rows) + 3) & ~3
+    adv = np.zeros((10, n), dtype=np.uint32)
+    adv[0, :len(rows)], adv[1, :len(rows)], adv[2, :len(rows)] = rows.T
+    fixed = np.zeros(n, dtype=np.uint32)
+    off = np.zeros(1, dtype=np.uint64)
+    assert orc.evaluate(adv, fixed, off)["lookup_failures"] == 0
+    for col in (0, 1, 2):
+        bad = adv.copy()
+        bad[col, 3] += 1
+        assert orc.evaluate(bad, fixed, off)["lookup_failures"] == 1
+    bad = adv.copy()
+    bad[1, 0] = 1 << 16  # dense outside the table
+    assert orc.evaluate(bad, fixed, off)["lookup_failures"] == 1
+
+
+def test_bad_offsets_rejected(orc):
+    x = random_inputs(3, (1,), 15)
+    adv, fixed, h_out, off = orc.fill(_orc_inputs(x, orc))
+    off2 = off.copy()
+    off2[1] += 4
+    with pytest.raises(ValueError):
+        orc.evaluate(adv, fixed, off2)

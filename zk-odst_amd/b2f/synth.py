@@ -26,8 +26,9 @@ def batch(n, rounds=12, seed=DEFAULT_SEED, first=0, rounds_mix=None):
     the whole batch). rounds_mix: sequence of rounds values drawn uniformly per instance."""
     n = int(n)
     words_per = 8 + 16 + 2 + 2
-    z = _splitmix64(np.uint64(seed) + np.uint64(first * words_per) * np.uint64(0x9E3779B97F4A7C15),
-                    n * words_per).reshape(n, words_per)
+    with np.errstate(over="ignore"):
+        start = np.uint64(seed) + np.uint64(first * words_per) * np.uint64(0x9E3779B97F4A7C15)
+    z = _splitmix64(start, n * words_per).reshape(n, words_per)
     out = np.zeros(n, dtype=INPUT_DTYPE)
     out["h"] = z[:, 0:8]
     out["m"] = z[:, 8:24]

@@ -39,7 +39,7 @@ __constant__ uint64_t c_iv[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL,
                                  0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
 
 // SIGMA = table16.rs:32-44
-__constant__ uint8_t c_sigma[10][16] = {
+__constant__ __attribute__((aligned(16))) uint8_t c_sigma[10][16] = {
     {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
     {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
     {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
@@ -51,7 +51,7 @@ __constant__ uint8_t c_sigma[10][16] = {
     {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
     {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
 
-__constant__ uint8_t c_gidx[8][4] = {{0, 4, 8, 12}, {1, 5, 9, 13}, {2, 6, 10, 14},
+__constant__ __attribute__((aligned(16))) uint8_t c_gidx[8][4] = {{0, 4, 8, 12}, {1, 5, 9, 13}, {2, 6, 10, 14},
                                      {3, 7, 11, 15}, {0, 5, 10, 15}, {1, 6, 11, 12},
                                      {2, 7, 8, 13}, {3, 4, 9, 14}};
 
@@ -345,6 +345,46 @@ __device__ __forceinline__ void quad_cells(Quad& Q, const b2f_input* __restrict_
   }
 }
 
+constexpr int HIST = 384;                // >= 361 + quad alignment
+constexpr int WSTRIDE = HIST + TSTRIDE;  // 1424
+constexpr int NOFF = 9;                  // offsets of the first 8 instances of a tile (+1)
+
+// Per-tile instance context, written by tile_info_kernel (96 bytes = 6 x 16 B).
+struct TileInfo {
+  uint32_t first;      // instance holding the tile's first row (n: none)
+  uint32_t pad;
+  uint64_t off[NOFF];  // off[first + i], clamped to off[n]
+  uint64_t pad2[2];
+};
+static_assert(sizeof(TileInfo) == 96, "TileInfo is six 16-byte loads");
+
+// Per-tile instance context: the instance holding the tile's first row and the offsets of the
+// next 8 instances. One tiny prepass shared by the fill and eval launches of a call.
+__global__ void tile_info_kernel(const uint64_t* __restrict__ off, uint32_t n, uint64_t n_tiles,
+                                 TileInfo* __restrict__ ti) {
+  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tiles) return;
+  uint64_t row = t * TILE_ROWS;
+  TileInfo x;
+  x.first = row < off[n] ? find_instance(off, n, row) : n;
+  x.pad = 0;
+#pragma unroll
+  for (int i = 0; i < NOFF; i++) {
+    uint64_t idx = (uint64_t)x.first + i;
+    x.off[i] = off[idx < n ? idx : n];
+  }
+  x.pad2[0] = x.pad2[1] = 0;
+  ti[t] = x;
+}
+
+// MODE (diagnostics; the product uses FILL_FULL): bit 0 = compute the cells (else zeros),
+// bit 1 = non-temporal stores (else plain stores).
+enum { FILL_COMPUTE = 1, FILL_NT = 2, FILL_FULL = 3 };
+
+// Tiles of 1024 rows are dealt round-robin over the (persistent) workgroups, so at any time
+// the chip writes a narrow band of every column: one DRAM-friendly front per column instead
+// of one per workgroup.
+template <int MODE>
 __global__ void __launch_bounds__(BLOCK) fill_kernel(const b2f_input* __restrict__ in,
                                                     uint32_t n,
                                                     const uint64_t* __restrict__ off,
@@ -353,22 +393,19 @@ __global__ void __launch_bounds__(BLOCK) fill_kernel(const b2f_input* __restrict
                                                     uint32_t* __restrict__ adv,
                                                     uint32_t* __restrict__ fixed,
                                                     const int* __restrict__ status,
-                                                    uint64_t tiles_per_wg) {
+                                                    const TileInfo* __restrict__ tinfo,
+                                                    uint64_t n_tiles) {
   if (*status) return;  // the record kernel rejected the layout: write nothing
   const uint64_t total_quads = total_rows >> 2;
   const uint64_t used_rows = off[n];
-  uint64_t t0 = (uint64_t)blockIdx.x * tiles_per_wg;
-  uint64_t t1 = t0 + tiles_per_wg;
-  uint64_t q_first = t0 * BLOCK + threadIdx.x;
-  if (q_first >= total_quads) return;
-  uint32_t inst = find_instance(off, n, min(4 * q_first, used_rows ? used_rows - 1 : 0));
-  for (uint64_t t = t0; t < t1; t++) {
+  for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
     uint64_t gq = t * BLOCK + threadIdx.x;
     if (gq >= total_quads) break;
     uint64_t row = 4 * gq;
     Quad Q;
     zero(Q);
-    if (row < used_rows) {
+    if ((MODE & FILL_COMPUTE) && row < used_rows) {
+      uint32_t inst = tinfo[t].first;
       while (off[inst + 1] <= row) inst++;
       uint64_t o = off[inst];
       const b2f_input* x = in + inst;
@@ -377,36 +414,233 @@ __global__ void __launch_bounds__(BLOCK) fill_kernel(const b2f_input* __restrict
       quad_cells(Q, x, states, rounds, (uint32_t)((row - o) >> 2));
     }
 #pragma unroll
-    for (int c = 0; c < 10; c++) {
-      u32x4 v = {Q.c[c][0], Q.c[c][1], Q.c[c][2], Q.c[c][3]};
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(adv + (uint64_t)c * total_rows + row));
+    for (int c = 0; c < 11; c++) {
+      u32x4 v = c < 10 ? u32x4{Q.c[c][0], Q.c[c][1], Q.c[c][2], Q.c[c][3]}
+                       : u32x4{Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]};
+      u32x4* dst = reinterpret_cast<u32x4*>((c < 10 ? adv + (uint64_t)c * total_rows : fixed) + row);
+      if (MODE & FILL_NT) __builtin_nontemporal_store(v, dst);
+      else *dst = v;
     }
-    u32x4 f = {Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]};
-    __builtin_nontemporal_store(f, reinterpret_cast<u32x4*>(fixed + row));
   }
 }
 
 // --------------------------------------------------------------------------- eval kernel
+//
+// Software-pipelined over 1024-row tiles dealt round-robin to persistent workgroups (3 per
+// CU). While a workgroup checks tile t out of LDS, its loads for tile t + gridDim are already
+// in flight into registers; at the next iteration they are written to LDS behind one barrier.
+//
+// LDS per workgroup (one array, 16-byte aligned carve):
+//   W   the canonical columns a_1 a_2 a_7 a_8 (every copy source is one of them) for rows
+//       [tile0 - HIST, tile0 + TILE_ROWS + HALO): the tile plus a history window holding
+//       every state-word source (<= 361 rows back, see make_copy_table);
+//   G   the other gate columns a_0 a_3 a_4 a_5 a_6 for rows [tile0, tile0 + TILE_ROWS + HALO);
+//   CT  copy-source table (make_copy_table), SG SIGMA, INFO the tile's TileInfo,
+//   IC  init-region cache: a_1 | a_2 of rows 0..163 of the tile's first instance, the only
+//       instance whose init region (h, m, t, fmask, IV, v12..v14) can lie before the window.
+// a_9 and the fixed column are only read on their own row: kept in registers.
 
-struct EvalAcc {
-  uint32_t gate[B2F_NUM_GATES];
-  uint32_t lookup, copy;
-  uint64_t first;
+constexpr int L_W = 0;
+constexpr int L_G = L_W + 4 * WSTRIDE;
+constexpr int L_CT = L_G + 5 * TSTRIDE;
+constexpr int L_SG = L_CT + 8 * G_QUADS * 12;
+constexpr int L_INFO = L_SG + 40;
+constexpr int L_IC = L_INFO + 24;
+constexpr int L_ACC = L_IC + 2 * INIT_ROWS;  // 16 gate + lookup + copy counters, first (u64)
+constexpr int LDS_WORDS = L_ACC + 20 + 2;
+static_assert(L_INFO % 4 == 0 && L_IC % 4 == 0 && L_G % 4 == 0, "16-byte aligned carve");
+
+// Extra (non-own-quad) loads of a tile: 2 slots per thread.
+constexpr int X_HIST = 4 * (HIST / 4);          // 384: 96 quads x 4 canonical columns
+constexpr int X_HALO = X_HIST + 9 * (HALO_ROWS / 4);  // +36: 4 quads x 9 gate columns
+constexpr int X_INIT = X_HALO + 2 * INIT_QUADS;  // +82: 41 quads x (a_1, a_2)
+constexpr int X_INFO = X_INIT + 6;               // +6: TileInfo
+static_assert(X_INFO <= 2 * BLOCK, "two extra slots per thread");
+
+// copy-source descriptor (u16): bits 0-1 kind: 0 none, 1 in-G (bits 2-7 row from the G's first
+// row, bits 8-11 column), 2 state word at the half-round start (bits 2-3 role a/b/c/d, bits 4-5
+// limb, bit 6 spread), 3 message word (bit 2: y instead of x, bits 4-5 limb).
+struct DescTable {
+  uint16_t d[G_QUADS][4][3];
 };
+constexpr uint16_t d_ing(uint32_t rel, uint32_t col) { return (uint16_t)(1 | (rel << 2) | (col << 8)); }
+constexpr uint16_t d_state(uint32_t role, uint32_t k, uint32_t spread) {
+  return (uint16_t)(2 | (role << 2) | (k << 4) | (spread << 6));
+}
+constexpr uint16_t d_msg(uint32_t y, uint32_t k) { return (uint16_t)(3 | (y << 2) | (k << 4)); }
 
-__device__ __forceinline__ void note(EvalAcc& A, uint64_t row, uint32_t code) {
-  uint64_t key = (row << 8) | code;
-  A.first = key < A.first ? key : A.first;
+// LAYOUT.md §5 round table, operand by operand.
+constexpr DescTable make_desc() {
+  DescTable T{};
+  for (uint32_t k = 0; k < 4; k++) {
+    T.d[0][k][0] = d_state(0, k, 0);  // a1 = a + b + x
+    T.d[0][k][1] = d_state(1, k, 0);
+    T.d[0][k][2] = d_msg(0, k);
+    T.d[3][k][0] = d_state(2, k, 0);  // c1 = c + d1
+    T.d[3][k][1] = d_ing(4 + 2 * ((k + 2) & 3), A1);
+    T.d[7][k][0] = d_ing(0 + k, A1);  // a2 = a1 + b1 + y
+    T.d[7][k][1] = d_ing(16 + 3 * k, A7);
+    T.d[7][k][2] = d_msg(1, k);
+    T.d[10][k][0] = d_ing(12 + k, A1);  // c2 = c1 + d2
+    T.d[10][k][1] = d_ing(32 + 2 * ((k + 1) & 3), A1);
+  }
+  for (uint32_t p = 0; p < 2; p++)
+    for (uint32_t j = 0; j < 4; j += 2) {
+      uint32_t k = (4 * p + j) / 2;
+      T.d[1 + p][j][0] = d_state(3, k, 1);  // d1 = (d ^ a1) >>> 32
+      T.d[1 + p][j][1] = d_ing(0 + k, A2);
+      T.d[8 + p][j][0] = d_ing(4 + 2 * ((k + 2) & 3), A2);  // d2 = (d1 ^ a2) >>> 16
+      T.d[8 + p][j][1] = d_ing(28 + k, A2);
+      T.d[11 + p][j][0] = d_ing(16 + 3 * k, A8);  // b2 = (b1 ^ c2) >>> 63
+      T.d[11 + p][j][1] = d_ing(40 + k, A2);
+    }
+  for (uint32_t p = 0; p < 3; p++)
+    for (uint32_t j = 0; j < 4; j++) {
+      uint32_t R = 4 * p + j;
+      if (R % 3) continue;
+      uint32_t k = R / 3;
+      T.d[4 + p][j][0] = d_state(1, k, 1);  // b1 = (b ^ c1) >>> 24
+      T.d[4 + p][j][1] = d_ing(12 + k, A2);
+    }
+  return T;
 }
 
-// LDS tile accessor: column c (0..9 advice, 10 fixed), tile-local row r
-#define TC(c, r) T[(c) * TSTRIDE + (r)]
+// The copy sources of every operand cell of a round quad, resolved per G index g at compile
+// time (u32 per (g, quad, row, operand)):
+//   bits 0-1  kind (0 none, 1 in-G, 2 state word, 3 message word)
+//   bits 2-3  source column as W index (a_1 a_2 a_7 a_8 -> 0..3), for half-rounds >= 1
+//   bits 4-5  limb k, bit 6: message y instead of x
+//   bits 7-16 row offset from the consumer G's first row, +512 (in-G; state for hr >= 1)
+//   bits 17-24 row inside the instance's init region (state word at hr = 0)
+//   bits 25-26 source column (W index) at hr = 0
+// Rows of half-round hr start at 164 + 208 hr, G g at + 52 (g & 3); the producer of a state
+// word sits in the previous half-round, whose parity is fixed by g, so the offset from the
+// consumer's G is a constant of (g, role, limb).
+constexpr uint8_t kGidx[8][4] = {{0, 4, 8, 12}, {1, 5, 9, 13}, {2, 6, 10, 14}, {3, 7, 11, 15},
+                                 {0, 5, 10, 15}, {1, 6, 11, 12}, {2, 7, 8, 13}, {3, 4, 9, 14}};
+struct CopyTable {
+  uint32_t e[8][G_QUADS][4][3];
+};
+constexpr uint32_t wc_of(uint32_t col) { return col == A1 ? 0 : col == A2 ? 1 : col == A7 ? 2 : 3; }
+constexpr uint32_t pack_copy(uint32_t kind, uint32_t wc, uint32_t k, uint32_t y, int rel,
+                             uint32_t abs0, uint32_t wc0) {
+  return kind | (wc << 2) | (k << 4) | (y << 6) | ((uint32_t)(rel + 512) << 7) | (abs0 << 17) |
+         (wc0 << 25);
+}
+constexpr CopyTable make_copy_table() {
+  CopyTable T{};
+  DescTable D = make_desc();
+  for (uint32_t g = 0; g < 8; g++)
+    for (uint32_t p = 0; p < G_QUADS; p++)
+      for (uint32_t j = 0; j < 4; j++)
+        for (uint32_t c = 0; c < 3; c++) {
+          uint32_t d = D.d[p][j][c], kind = d & 3u, e = 0;
+          if (kind == 1) {
+            e = pack_copy(1, wc_of(d >> 8), 0, 0, (int)((d >> 2) & 63u), 0, 0);
+          } else if (kind == 2) {
+            uint32_t role = (d >> 2) & 3u, k = (d >> 4) & 3u, sp = (d >> 6) & 1u;
+            uint32_t w = kGidx[g][role], pos = w & 3u;
+            uint32_t prev_odd = g < 4 ? 1u : 0u;  // parity of half-round hr - 1
+            uint32_t gp = prev_odd ? ((pos - role) & 3u) : pos;
+            uint32_t off = role == 0 ? 28 + k : role == 1 ? 44 + 2 * k : role == 2 ? 40 + k
+                                                                         : 32 + 2 * ((k + 1) & 3u);
+            int rel = -208 + 52 * ((int)gp - (int)(g & 3u)) + (int)off;
+            uint32_t col = role == 1 ? (sp ? A8 : A7) : (sp ? A2 : A1);
+            uint32_t abs0 = w < 8 ? 4 * w + k
+                            : (w >= 12 && w < 15) ? 140 + 8 * (w - 12) + 2 * k
+                                                  : 108 + 4 * (w == 15 ? 7u : w - 8) + k;
+            e = pack_copy(2, wc_of(col), k, 0, rel, abs0, sp ? 1u : 0u);
+          } else if (kind == 3) {
+            e = pack_copy(3, 0, (d >> 4) & 3u, (d >> 2) & 1u, 0, 0, 0);
+          }
+          T.e[g][p][j][c] = e;
+        }
+  return T;
+}
+// The deepest state-word source (dst - src rows) must fit the history window.
+constexpr int max_copy_distance() {
+  CopyTable T = make_copy_table();
+  int m = 0;
+  for (uint32_t g = 0; g < 8; g++)
+    for (uint32_t p = 0; p < G_QUADS; p++)
+      for (uint32_t j = 0; j < 4; j++)
+        for (uint32_t c = 0; c < 3; c++)
+          if ((T.e[g][p][j][c] & 3u) == 2) {
+            int dst = 4 * (int)p + (int)j;  // the G's quads are contiguous from its first row
+            int rel = (int)((T.e[g][p][j][c] >> 7) & 1023u) - 512;
+            int dist = dst - rel;
+            m = dist > m ? dist : m;
+          }
+  return m;
+}
+static_assert(max_copy_distance() + 4 <= HIST, "history window too small for state sources");
 
-// Evaluate gate `s` at tile-local row r. Every identity of LAYOUT.md §4 is checked in an
-// exact integer form: linear identities as equalities in 64/128-bit arithmetic (all terms
-// are < 2^100), the root constraints c(c-1)(c-2), t(t-1), b(b-1) as range tests (equivalent
-// for non-negative integers < p).
-__device__ __forceinline__ bool gate_ok(const uint32_t* __restrict__ T, int s, uint32_t r) {
+__constant__ __attribute__((aligned(16))) CopyTable c_copy = make_copy_table();
+constexpr int COPY_WORDS = (int)(sizeof(CopyTable) / 4);  // 1248
+
+// Failure accounting. Failures are rare, so they go straight to LDS atomics (per-workgroup
+// counters, flushed once at the end) instead of occupying registers on the hot path.
+struct EvalAcc {
+  uint32_t* c;  // [0..15] gates, [16] lookup, [17] copy, [18..19] pad, [20..21] first (u64)
+  __device__ __forceinline__ void fail(uint64_t row, uint32_t code) {
+    atomicAdd(&c[code], 1u);
+    atomicMin(reinterpret_cast<unsigned long long*>(c + 20), (unsigned long long)((row << 8) | code));
+  }
+  __device__ __forceinline__ void fail_gates(uint64_t row, uint32_t mask) {
+    for (uint32_t m = mask; m; m &= m - 1) atomicAdd(&c[__builtin_ctz(m)], 1u);
+    atomicMin(reinterpret_cast<unsigned long long*>(c + 20),
+              (unsigned long long)((row << 8) | (uint32_t)__builtin_ctz(mask)));
+  }
+};
+
+// component j of a quad register (select chain: never an indexed access into a register array)
+__device__ __forceinline__ uint32_t comp(const uint4& v, int j) {
+  return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+
+// LDS cell accessor: column c, tile-local row r (r may reach TILE_ROWS + 11)
+struct Tile {
+  const uint32_t* L;
+  __device__ __forceinline__ uint32_t at(int c, uint32_t r) const {
+    switch (c) {
+      case A1: return L[L_W + 0 * WSTRIDE + HIST + r];
+      case A2: return L[L_W + 1 * WSTRIDE + HIST + r];
+      case A7: return L[L_W + 2 * WSTRIDE + HIST + r];
+      case A8: return L[L_W + 3 * WSTRIDE + HIST + r];
+      case A0: return L[L_G + 0 * TSTRIDE + r];
+      case A3: return L[L_G + 1 * TSTRIDE + r];
+      case A4: return L[L_G + 2 * TSTRIDE + r];
+      case A5: return L[L_G + 3 * TSTRIDE + r];
+      default: return L[L_G + 4 * TSTRIDE + r];  // A6
+    }
+  }
+  __device__ __forceinline__ uint4 quad(int c, uint32_t r) const {
+    return *reinterpret_cast<const uint4*>(&L[(c == A1 || c == A2 || c == A7 || c == A8)
+                                                  ? L_W + (c == A1 ? 0 : c == A2 ? 1 : c == A7 ? 2 : 3) * WSTRIDE + HIST + r
+                                                  : L_G + (c == A0 ? 0 : c - 2) * TSTRIDE + r]);
+  }
+};
+#define TC(c, r) T.at((c), (r))
+
+// LDS word offset of column c (a_0..a_8) at tile-local row r
+__device__ __forceinline__ int lds_cell(int c, int r) {
+  switch (c) {
+    case A1: return L_W + 0 * WSTRIDE + HIST + r;
+    case A2: return L_W + 1 * WSTRIDE + HIST + r;
+    case A7: return L_W + 2 * WSTRIDE + HIST + r;
+    case A8: return L_W + 3 * WSTRIDE + HIST + r;
+    case A0: return L_G + r;
+    default: return L_G + (c - 2) * TSTRIDE + r;  // A3..A6 -> 1..4
+  }
+}
+
+// Evaluate gate `s` on the block whose selector row is tile-local row r. Every identity of
+// LAYOUT.md §4 is checked in an exact integer form: linear identities as equalities in
+// 64/128-bit arithmetic (all terms are < 2^100), the root constraints c(c-1)(c-2), t(t-1),
+// b(b-1) as range tests (equivalent for non-negative integers < p). a9 and k0 are the
+// selector row's own a_9 and fixed cells.
+__device__ __forceinline__ bool gate_ok(const Tile& T, int s, uint32_t r, uint32_t a9,
+                                        uint32_t k0) {
   typedef unsigned __int128 u128;
   switch (s) {
     case S_ABCD:
@@ -417,7 +651,7 @@ __device__ __forceinline__ bool gate_ok(const uint32_t* __restrict__ T, int s, u
              (uint64_t)TC(A8, r) == (uint64_t)TC(A1, r + 4) + ((uint64_t)TC(A1, r + 6) << 16);
     case S_EFGH: {
       bool ok = true;
-#pragma unroll
+#pragma unroll 1
       for (uint32_t k = 0; k < 4; k++) {
         uint32_t k1 = (k + 1) & 3, k2 = (k + 2) & 3;
         ok &= (uint64_t)TC(A7, r + 3 * k) ==
@@ -429,7 +663,7 @@ __device__ __forceinline__ bool gate_ok(const uint32_t* __restrict__ T, int s, u
     }
     case S_IJKL: {
       bool ok = true;
-#pragma unroll
+#pragma unroll 1
       for (uint32_t k = 0; k < 4; k++) {
         uint32_t k3 = (k + 3) & 3;
         uint64_t zb = TC(A6, r + 2 * k3);
@@ -444,19 +678,18 @@ __device__ __forceinline__ bool gate_ok(const uint32_t* __restrict__ T, int s, u
     case S_C2: {
       bool three = (s == S_A1 || s == S_A2);
       u128 lhs = 0, rhs = 0;
-#pragma unroll
+#pragma unroll 1
       for (uint32_t k = 0; k < 4; k++) {
         uint64_t in = (uint64_t)TC(A3, r + k) + TC(A4, r + k) + (three ? TC(A5, r + k) : 0u);
         lhs += (u128)in << (16 * k);
         rhs += (u128)TC(A1, r + k) << (16 * k);
       }
-      uint32_t cy = TC(A9, r);
-      rhs += (u128)cy << 64;
-      return lhs == rhs && cy <= (three ? 2u : 1u);
+      rhs += (u128)a9 << 64;
+      return lhs == rhs && a9 <= (three ? 2u : 1u);
     }
     case S_B1: {
       bool ok = true;
-#pragma unroll
+#pragma unroll 1
       for (uint32_t k = 0; k < 4; k++) {
         uint32_t b = r + 3 * k;
         ok &= (uint64_t)TC(A3, b) + TC(A4, b) ==
@@ -469,7 +702,7 @@ __device__ __forceinline__ bool gate_ok(const uint32_t* __restrict__ T, int s, u
     case S_D2:
     case S_XOR: {
       bool ok = true;
-#pragma unroll
+#pragma unroll 1
       for (uint32_t k = 0; k < 4; k++) {
         uint32_t b = r + 2 * k;
         ok &= (uint64_t)TC(A3, b) + TC(A4, b) == (uint64_t)TC(A2, b) + 2 * (uint64_t)TC(A2, b + 1);
@@ -478,7 +711,7 @@ __device__ __forceinline__ bool gate_ok(const uint32_t* __restrict__ T, int s, u
     }
     case S_B2: {
       bool ok = true;
-#pragma unroll
+#pragma unroll 1
       for (uint32_t k = 0; k < 4; k++) {
         uint32_t b = r + 2 * k;
         uint32_t zb = TC(A6, b);
@@ -490,7 +723,7 @@ __device__ __forceinline__ bool gate_ok(const uint32_t* __restrict__ T, int s, u
     }
     case S_XOR3: {
       bool ok = true;
-#pragma unroll
+#pragma unroll 1
       for (uint32_t k = 0; k < 4; k++) {
         uint32_t b = r + 2 * k;
         ok &= (uint64_t)TC(A3, b) + TC(A4, b) + TC(A5, b) ==
@@ -499,11 +732,11 @@ __device__ __forceinline__ bool gate_ok(const uint32_t* __restrict__ T, int s, u
       return ok;
     }
     case S_CONST:
-      return TC(A1, r) == (TC(10, r) >> 16);
+      return TC(A1, r) == (k0 >> 16);
     case S_FMASK: {
       uint32_t f = TC(A5, r);
       bool ok = f <= 1u;
-#pragma unroll
+#pragma unroll 1
       for (uint32_t k = 0; k < 4; k++) ok &= (uint64_t)TC(A1, r + k) == 65535ull * f;
       return ok;
     }
@@ -511,199 +744,269 @@ __device__ __forceinline__ bool gate_ok(const uint32_t* __restrict__ T, int s, u
   return true;
 }
 
-// One copy constraint: operand cell (dcol, instance-local drow) == canonical (scol, srow).
-__device__ __forceinline__ void copy_check(EvalAcc& A, const uint32_t* __restrict__ T,
-                                           const uint32_t* __restrict__ adv,
-                                           uint64_t total_rows, uint64_t tile0, uint64_t o,
-                                           int dcol, uint32_t drow, int scol, uint32_t srow) {
-  uint64_t gd = o + drow, gs = o + srow;
-  uint32_t dv = TC(dcol, (uint32_t)(gd - tile0));  // the operand is in this thread's quad
-  uint32_t sv;
-  if (gs >= tile0 && gs < tile0 + TSTRIDE) sv = TC(scol, (uint32_t)(gs - tile0));
-  else sv = adv[(uint64_t)scol * total_rows + gs];
-  if (dv != sv) { A.copy++; note(A, gd, B2F_CODE_COPY); }
+// Copy-source lookup, all from LDS for a valid trace: rows inside the window come from W;
+// init-region words (h, m, t, fmask, IV, v12..v14) of the tile's first instance, which may
+// start before the window, from the init cache I (a_1 | a_2 of its rows 0..163). Anything
+// else (only reachable through a corrupted layout) is read from global memory.
+struct Src {
+  const uint32_t* W;
+  const uint32_t* I;
+  const uint32_t* adv;
+  uint64_t total_rows, wlo, ofirst;
+  // wc: source column as W index (a_1 a_2 a_7 a_8 -> 0 1 2 3)
+  __device__ __forceinline__ uint32_t at(uint64_t gs, uint32_t wc) const {
+    uint64_t d = gs - wlo;  // wraps for gs < wlo
+    if (d < (uint64_t)WSTRIDE) return W[wc * WSTRIDE + (uint32_t)d];
+    uint64_t e = gs - ofirst;
+    if (e < (uint64_t)INIT_ROWS && wc < 2) return I[wc * INIT_ROWS + (uint32_t)e];
+    uint32_t col = wc < 2 ? wc + 1 : wc + 5;
+    return adv[(uint64_t)col * total_rows + gs];
+  }
+  __device__ __forceinline__ uint32_t operator()(uint64_t gs, uint32_t col) const {
+    return at(gs, col < 3 ? col - 1 : col - 5);
+  }
+};
+
+__device__ __forceinline__ void copy_check(EvalAcc& A, uint32_t dv, uint32_t sv, uint64_t gd) {
+  if (dv != sv) A.fail(gd, B2F_CODE_COPY);
 }
 
-__device__ __forceinline__ void copies_of_quad(EvalAcc& A, const uint32_t* __restrict__ T,
-                                               const uint32_t* __restrict__ adv,
-                                               uint64_t total_rows, uint64_t tile0, uint64_t o,
-                                               const b2f_input* __restrict__ unused,
-                                               uint32_t rounds, uint32_t lq) {
-  (void)unused;
+// canonical cell of limb k of state word w as half-round hr starts (instance-local row)
+__device__ __forceinline__ uint32_t state_src(uint32_t w, uint32_t k, uint32_t spread, uint32_t hr,
+                                              uint32_t& col) {
+  if (hr == 0) {
+    col = spread ? A2 : A1;
+    if (w < 8) return 4 * w + k;
+    if (w >= 12 && w < 15) return 140 + 8 * (w - 12) + 2 * k;
+    return 108 + 4 * (w == 15 ? 7u : w - 8) + k;
+  }
+  uint32_t hp = hr - 1, role = w >> 2, pos = w & 3;
+  uint32_t g = (hp & 1) ? 4 + ((pos - role) & 3u) : pos;
+  uint32_t gb = INIT_ROWS + ROUND_ROWS * (hp >> 1) + G_ROWS * g;
+  col = role == 1 ? (spread ? A8 : A7) : (spread ? A2 : A1);
+  // a <- a2 (+28), b <- b2 (+44, stride 2), c <- c2 (+40), d <- d2 (+32, rot 16)
+  uint32_t off = role == 0 ? 28 + k : role == 1 ? 44 + 2 * k : role == 2 ? 40 + k
+                                                             : 32 + 2 * ((k + 1) & 3);
+  return gb + off;
+}
+
+// Copy constraints of the init XOR blocks and of the final XOR3 blocks (57 of the R/4 quads
+// of an instance): decoded directly.
+__device__ void copies_edge(EvalAcc& A, const uint4* dst, const Src& src, uint64_t o,
+                            uint32_t rounds, uint32_t lq) {
   QuadInfo d = decode_quad(lq, rounds);
-  const uint32_t r0 = 4 * lq;  // first row of the quad (instance-local)
-  switch (d.kind) {
-    case K_INW: case K_FMASK: case K_CONST: case K_PAD:
-      return;
-    case K_XOR3: {
-      Canon H = canon_h(d.a), V = canon_state(d.a, 2 * rounds), U = canon_state(d.a + 8, 2 * rounds);
+  const uint32_t r0 = 4 * lq;
+  if (d.kind == K_XOR && d.block < INIT_ROWS) {
+    // v12 = IV4 ^ t0, v13 = IV5 ^ t1, v14 = IV6 ^ fmask
 #pragma unroll
-      for (uint32_t h = 0; h < 2; h++) {
-        uint32_t k = 2 * d.q + h, row = r0 + 2 * h;
-        copy_check(A, T, adv, total_rows, tile0, o, A3, row, H.scol, H.row(k));
-        copy_check(A, T, adv, total_rows, tile0, o, A4, row, V.scol, V.row(k));
-        copy_check(A, T, adv, total_rows, tile0, o, A5, row, U.scol, U.row(k));
-      }
-      return;
+    for (uint32_t h = 0; h < 2; h++) {
+      uint32_t k = 2 * d.q + h;
+      uint32_t xs = 108 + 4 * (4 + d.a) + k;
+      uint32_t ys = (d.a < 2 ? 96 + 4 * d.a : 104) + k;
+      uint32_t dx = comp(dst[0], 2 * h), dy = comp(dst[1], 2 * h);
+      copy_check(A, dx, src(o + xs, A2), o + r0 + 2 * h);
+      copy_check(A, dy, src(o + ys, A2), o + r0 + 2 * h);
     }
-    default:
-      break;
+  } else if (d.kind == K_XOR3) {
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+      uint32_t k = 2 * d.q + h, cv, cu;
+      uint32_t vs = state_src(d.a, k, 1, 2 * rounds, cv);
+      uint32_t us = state_src(d.a + 8, k, 1, 2 * rounds, cu);
+      uint64_t gd = o + r0 + 2 * h;
+      copy_check(A, comp(dst[0], 2 * h), src(o + 4 * d.a + k, A2), gd);
+      copy_check(A, comp(dst[1], 2 * h), src(o + vs, cv), gd);
+      copy_check(A, comp(dst[2], 2 * h), src(o + us, cu), gd);
+    }
   }
-  // Operand words X, Y (and M for ADD3) of the block.
-  Canon X, Y, M;
-  M = canon_m(0);
-  if (d.block < INIT_ROWS) {  // init XORs
-    X = canon(108 + 4 * (4 + d.a), 1, 0, A1, A2);
-    Y = d.a < 2 ? canon(96 + 4 * d.a, 1, 0, A1, A2) : canon(104, 1, 0, A1, A2);
+}
+
+// MODE (diagnostics; the product uses EVAL_FULL): which checks run on a staged tile.
+enum { EVAL_LOOKUP = 1, EVAL_GATES = 2, EVAL_COPIES = 4, EVAL_FULL = 7, EVAL_TOUCH = 8 };
+
+// Issue the load behind extra slot `slot` of tile t (history / halo / init cache / info).
+// fo = {first, -, off[first]} of tile t (only the init slots use it).
+__device__ __forceinline__ uint4 extra_load(int slot, uint64_t t, const uint4& fo,
+                                            const uint32_t* __restrict__ adv,
+                                            uint64_t total_rows, uint64_t total_quads, uint32_t n,
+                                            const TileInfo* __restrict__ tinfo) {
+  const uint64_t tile0 = t * TILE_ROWS;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  if (slot < X_HIST) {
+    int ci = slot / (HIST / 4), hq = slot - ci * (HIST / 4);
+    int col = ci == 0 ? A1 : ci == 1 ? A2 : ci == 2 ? A7 : A8;
+    if (tile0 < (uint64_t)HIST) return z;
+    return *reinterpret_cast<const uint4*>(adv + (uint64_t)col * total_rows + tile0 - HIST + 4 * hq);
+  }
+  if (slot < X_HALO) {
+    int e = slot - X_HIST, gi = e >> 2, q = e & 3;
+    const int cols[9] = {A0, A1, A2, A3, A4, A5, A6, A7, A8};
+    uint64_t hq = (t + 1) * BLOCK + q;
+    if (hq >= total_quads) return z;
+    return *reinterpret_cast<const uint4*>(adv + (uint64_t)cols[gi] * total_rows + 4 * hq);
+  }
+  if (slot < X_INIT) {
+    int e = slot - X_HALO, ci = e / INIT_QUADS, q = e - ci * INIT_QUADS;
+    uint64_t of = ((uint64_t)fo.w << 32) | fo.z;
+    if (fo.x >= n || of + INIT_ROWS > total_rows) return z;
+    return *reinterpret_cast<const uint4*>(adv + (uint64_t)(A1 + ci) * total_rows + of + 4 * q);
+  }
+  if (slot < X_INFO) return reinterpret_cast<const uint4*>(tinfo + t)[slot - X_INIT];
+  return z;
+}
+
+__device__ __forceinline__ void extra_store(uint32_t* L, int slot, const uint4& v) {
+  int w;
+  if (slot < X_HIST) {
+    int ci = slot / (HIST / 4), hq = slot - ci * (HIST / 4);
+    w = L_W + ci * WSTRIDE + 4 * hq;
+  } else if (slot < X_HALO) {
+    int e = slot - X_HIST, gi = e >> 2, q = e & 3;
+    w = lds_cell(gi, TILE_ROWS + 4 * q);  // gate columns a_0..a_8 in order
+  } else if (slot < X_INIT) {
+    int e = slot - X_HALO, ci = e / INIT_QUADS, q = e - ci * INIT_QUADS;
+    w = L_IC + ci * INIT_ROWS + 4 * q;
+  } else if (slot < X_INFO) {
+    w = L_INFO + 4 * (slot - X_INIT);
   } else {
-    uint32_t r = d.a, g = d.g, hr = 2 * r + (g >= 4);
-    uint32_t gb = INIT_ROWS + ROUND_ROWS * r + G_ROWS * g;
-    Canon va = canon_state(c_gidx[g][0], hr), vb = canon_state(c_gidx[g][1], hr);
-    Canon vc = canon_state(c_gidx[g][2], hr), vd = canon_state(c_gidx[g][3], hr);
-    Canon a1 = canon(gb + 0, 1, 0, A1, A2), d1 = canon(gb + 4, 2, 2, A1, A2);
-    Canon c1 = canon(gb + 12, 1, 0, A1, A2), b1 = canon(gb + 16, 3, 0, A7, A8);
-    Canon a2 = canon(gb + 28, 1, 0, A1, A2), d2 = canon(gb + 32, 2, 1, A1, A2);
-    Canon c2 = canon(gb + 40, 1, 0, A1, A2);
-    const uint8_t* sg = c_sigma[r % 10];
-    switch (d.step) {
-      case 0: X = va; Y = vb; M = canon_m(sg[2 * g]); break;
-      case 1: X = vd; Y = a1; break;
-      case 2: X = vc; Y = d1; break;
-      case 3: X = vb; Y = c1; break;
-      case 4: X = a1; Y = b1; M = canon_m(sg[2 * g + 1]); break;
-      case 5: X = d1; Y = a2; break;
-      case 6: X = c1; Y = d2; break;
-      default: X = b1; Y = c2; break;
-    }
+    return;
   }
-  switch (d.kind) {
-    case K_ADD3:
-    case K_ADD2:
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++) {
-        uint32_t row = r0 + k;
-        copy_check(A, T, adv, total_rows, tile0, o, A3, row, X.dcol, X.row(k));
-        copy_check(A, T, adv, total_rows, tile0, o, A4, row, Y.dcol, Y.row(k));
-        if (d.kind == K_ADD3) copy_check(A, T, adv, total_rows, tile0, o, A5, row, M.dcol, M.row(k));
-      }
-      return;
-    case K_XOR:
-    case K_XOR63:
-#pragma unroll
-      for (uint32_t h = 0; h < 2; h++) {
-        uint32_t k = 2 * d.q + h, row = r0 + 2 * h;
-        copy_check(A, T, adv, total_rows, tile0, o, A3, row, X.scol, X.row(k));
-        copy_check(A, T, adv, total_rows, tile0, o, A4, row, Y.scol, Y.row(k));
-      }
-      return;
-    case K_XOR24:
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++) {
-        uint32_t R = 4 * d.q + j;
-        if (R % 3 == 0) {
-          uint32_t k = R / 3, row = r0 + j;
-          copy_check(A, T, adv, total_rows, tile0, o, A3, row, X.scol, X.row(k));
-          copy_check(A, T, adv, total_rows, tile0, o, A4, row, Y.scol, Y.row(k));
-        }
-      }
-      return;
-    default:
-      return;
-  }
+  *reinterpret_cast<uint4*>(&L[w]) = v;
 }
 
-__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ uint64_t wave_min(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t u = __shfl_xor(v, o, 64);
-    v = u < v ? u : v;
-  }
-  return v;
-}
-
-__global__ void __launch_bounds__(BLOCK) eval_kernel(const uint32_t* __restrict__ adv,
+template <int MODE>
+__global__ void __launch_bounds__(BLOCK, 3) eval_kernel(const uint32_t* __restrict__ adv,
                                                     const uint32_t* __restrict__ fixed,
                                                     const uint64_t* __restrict__ off, uint32_t n,
                                                     uint64_t total_rows,
+                                                    const TileInfo* __restrict__ tinfo,
+                                                    uint64_t n_tiles,
                                                     b2f_eval_report* __restrict__ rep,
-                                                    int* __restrict__ status,
-                                                    uint64_t tiles_per_wg) {
-  __shared__ __attribute__((aligned(16))) uint32_t T[NCOL_T * TSTRIDE];
-  EvalAcc A;
-#pragma unroll
-  for (int s = 0; s < B2F_NUM_GATES; s++) A.gate[s] = 0;
-  A.lookup = 0; A.copy = 0; A.first = ~0ull;
+                                                    int* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[LDS_WORDS];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < COPY_WORDS; i += BLOCK)
+    L[L_CT + i] = reinterpret_cast<const uint32_t*>(&c_copy)[i];
+  if (tid < 40) L[L_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
+  const Tile T{L};
+  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + L_SG);  // [10][16]
+
+  EvalAcc A{L + L_ACC};
+  if (tid < 20) L[L_ACC + tid] = 0;
+  if (tid == 20) *reinterpret_cast<uint64_t*>(L + L_ACC + 20) = ~0ull;
 
   const uint64_t total_quads = total_rows >> 2;
   const uint64_t used_rows = off[n];
-  if (used_rows > total_rows || off[0] != 0) {  // never read past the trace
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(status, 1 << B2F_ERR_LAYOUT);
-    return;
-  }
-  const uint64_t t0 = (uint64_t)blockIdx.x * tiles_per_wg;
-  const uint64_t t1 = t0 + tiles_per_wg;
-  uint32_t inst = 0;
-  bool have_inst = false;
-  for (uint64_t t = t0; t < t1; t++) {
-    const uint64_t tile0 = t * TILE_ROWS;
-    if (tile0 >= total_rows) break;
-    // ---- stage: every thread loads one quad (11 x 16 B); threads 0..3 also the halo
-    const uint64_t gq = t * BLOCK + threadIdx.x;
-    uint4 mine[NCOL_T];
-    if (gq < total_quads) {
-#pragma unroll
-      for (int c = 0; c < 10; c++)
-        mine[c] = *reinterpret_cast<const uint4*>(adv + (uint64_t)c * total_rows + 4 * gq);
-      mine[10] = *reinterpret_cast<const uint4*>(fixed + 4 * gq);
-    } else {
-#pragma unroll
-      for (int c = 0; c < NCOL_T; c++) mine[c] = make_uint4(0, 0, 0, 0);
-    }
+  const bool layout_ok = used_rows <= total_rows && off[0] == 0;  // never read past the trace
+  if (!layout_ok && blockIdx.x == 0 && tid == 0) atomicOr(status, 1 << B2F_ERR_LAYOUT);
+  const uint64_t G = gridDim.x;
+  const bool init_role = tid + BLOCK >= X_HALO && tid + BLOCK < X_INIT;  // slot tid+256
+
+  uint64_t t = blockIdx.x;
+  uint4 q[NCOL_T], x0 = make_uint4(0, 0, 0, 0), x1 = x0, fo = x0, fo_next = x0;
+  auto load_tile = [&](uint64_t tt, const uint4& f) {
+    const uint64_t gq = tt * BLOCK + tid;
 #pragma unroll
     for (int c = 0; c < NCOL_T; c++)
-      *reinterpret_cast<uint4*>(&T[c * TSTRIDE + 4 * threadIdx.x]) = mine[c];
-    if (threadIdx.x < HALO_ROWS / 4) {
-      uint64_t hq = (t + 1) * BLOCK + threadIdx.x;
+      q[c] = gq < total_quads
+                 ? *reinterpret_cast<const uint4*>((c < 10 ? adv + (uint64_t)c * total_rows : fixed) + 4 * gq)
+                 : make_uint4(0, 0, 0, 0);
+    x0 = extra_load(tid, tt, f, adv, total_rows, total_quads, n, tinfo);
+    x1 = extra_load(tid + BLOCK, tt, f, adv, total_rows, total_quads, n, tinfo);
+  };
+  if (layout_ok && t < n_tiles) {
+    if (init_role) fo = *reinterpret_cast<const uint4*>(tinfo + t);
+    load_tile(t, fo);
+    if (init_role && t + G < n_tiles) fo_next = *reinterpret_cast<const uint4*>(tinfo + t + G);
+  }
+  for (; layout_ok && t < n_tiles; t += G) {
+    // ---- stage tile t: registers -> LDS
 #pragma unroll
-      for (int c = 0; c < NCOL_T; c++) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (hq < total_quads)
-          v = *reinterpret_cast<const uint4*>((c < 10 ? adv + (uint64_t)c * total_rows : fixed) + 4 * hq);
-        *reinterpret_cast<uint4*>(&T[c * TSTRIDE + TILE_ROWS + 4 * threadIdx.x]) = v;
-      }
-    }
+    for (int c = 0; c < 9; c++) *reinterpret_cast<uint4*>(&L[lds_cell(c, 4 * tid)]) = q[c];
+    const uint4 cur9 = q[A9], curfx = q[10];
+    extra_store(L, tid, x0);
+    extra_store(L, tid + BLOCK, x1);
     __syncthreads();
+    // ---- prefetch tile t + G into registers while tile t is checked
+    const uint64_t tn = t + G;
+    if (tn < n_tiles) {
+      load_tile(tn, fo_next);
+      if (init_role && tn + G < n_tiles) fo_next = *reinterpret_cast<const uint4*>(tinfo + tn + G);
+    }
+    const uint64_t tile0 = t * TILE_ROWS;
+    const uint64_t gq = t * BLOCK + tid;
+    if ((MODE & EVAL_TOUCH) && gq < total_quads) {  // diagnostics: keep the staged words alive
+      uint4 a = T.quad(A0, 4 * tid), b = T.quad(A8, 4 * tid);
+      uint32_t x = a.x ^ b.w ^ cur9.x ^ curfx.y ^ L[L_W + 4 * tid] ^ L[L_IC + (tid & 255)] ^
+                   L[L_INFO + (tid & 15)] ^ T.at(A3, 4 * tid + 13);
+      if (x == 0x12345678u) A.fail(0, B2F_CODE_LOOKUP);
+    }
     if (gq < total_quads) {
       const uint64_t row0 = 4 * gq;
-      const uint32_t lr0 = 4 * threadIdx.x;
+      const uint32_t lr0 = 4 * tid;
       // ---- lookups and gates on the 4 rows
-#pragma unroll
+      const uint4 q0 = T.quad(A0, lr0), q1 = T.quad(A1, lr0), q2 = T.quad(A2, lr0);
+#pragma unroll 1
       for (int j = 0; j < 4; j++) {
-        uint32_t tg = (&mine[A0].x)[j], de = (&mine[A1].x)[j], sp = (&mine[A2].x)[j];
+        uint32_t tg = comp(q0, j), de = comp(q1, j), sp = comp(q2, j);
         bool ok = de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu);
-        if (!ok) { A.lookup++; note(A, row0 + j, B2F_CODE_LOOKUP); }
-        uint32_t sel = (&mine[10].x)[j] & 0xffffu;
+        if ((MODE & EVAL_LOOKUP) && !ok) A.fail(row0 + j, B2F_CODE_LOOKUP);
+        uint32_t k0 = comp(curfx, j);
+        uint32_t sel = (MODE & EVAL_GATES) ? k0 & 0xffffu : 0u;
+        const uint32_t a9 = comp(cur9, j);
+        uint32_t failed = 0;  // gates failing on this row (bit per selector)
         while (sel) {
           int s = __builtin_ctz(sel);
           sel &= sel - 1;
-          if (!gate_ok(T, s, lr0 + j)) { A.gate[s]++; note(A, row0 + j, (uint32_t)s); }
+          if (!gate_ok(T, s, lr0 + j, a9, k0)) failed |= 1u << s;
         }
+        if (failed) A.fail_gates(row0 + j, failed);
       }
       // ---- copy constraints whose operand cell lies in this quad
-      if (row0 < used_rows) {
-        if (!have_inst) { inst = find_instance(off, n, row0); have_inst = true; }
-        while (off[inst + 1] <= row0) inst++;
-        uint64_t o = off[inst], o1 = off[inst + 1], R = o1 - o;
+      const uint32_t first = L[L_INFO];
+      const uint64_t* Off = reinterpret_cast<const uint64_t*>(L + L_INFO + 2);
+      if ((MODE & EVAL_COPIES) && row0 < used_rows) {
+        // instance of this quad: scan the tile's offsets in LDS (global beyond 8 instances)
+        uint32_t inst = first, i = 0;
+        while (i + 1 < NOFF && Off[i + 1] <= row0) i++;
+        inst += i;
+        uint64_t o = Off[i], o1 = i + 1 < NOFF ? Off[i + 1] : off[inst + 1];
+        while (o1 <= row0) { inst++; o = o1; o1 = off[inst + 1]; }
+        uint64_t R = o1 - o;
+        const Src src{L + L_W, L + L_IC, adv, total_rows, tile0 - HIST, first < n ? Off[0] : ~0ull};
+        const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
         if (o1 > o && o1 <= total_rows && R >= FIXED_ROWS && (R - FIXED_ROWS) % ROUND_ROWS == 0 &&
             (R - FIXED_ROWS) / ROUND_ROWS <= B2F_MAX_ROUNDS) {
           uint32_t rounds = (uint32_t)((R - FIXED_ROWS) / ROUND_ROWS);
-          copies_of_quad(A, T, adv, total_rows, tile0, o, nullptr, rounds,
-                         (uint32_t)((row0 - o) >> 2));
+          uint32_t lq = (uint32_t)((row0 - o) >> 2);
+          uint32_t rq = lq - INIT_QUADS;
+          if (lq >= INIT_QUADS && rq < ROUND_QUADS * rounds) {
+            uint32_t r = rq / ROUND_QUADS, w = rq - r * ROUND_QUADS;
+            uint32_t g = w / G_QUADS, p = w - g * G_QUADS;
+            uint64_t gbase = o + INIT_ROWS + (uint64_t)ROUND_ROWS * r + G_ROWS * g;
+            const bool hr0 = (r == 0) && (g < 4);
+            const uint32_t* ct = L + L_CT + (g * G_QUADS + p) * 12;
+            const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
+#pragma unroll 1
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+              for (int c = 0; c < 3; c++) {
+                uint32_t e = ct[j * 3 + c];
+                uint32_t kind = e & 3u;
+                uint32_t k = (e >> 4) & 3u;
+                // rows relative to the instance (init region) or to the G's first row
+                uint32_t init_row = kind == 3 ? 32 + 4 * (uint32_t)sg[(e >> 6) & 1u] + k
+                                              : (e >> 17) & 255u;
+                bool from_init = kind == 3 || (kind == 2 && hr0);
+                uint64_t gs = from_init ? o + init_row
+                                        : gbase + (uint64_t)(int64_t)((int)((e >> 7) & 1023u) - 512);
+                uint32_t wc = (kind == 2 && hr0) ? (e >> 25) & 3u : (e >> 2) & 3u;
+                uint32_t sv = kind ? src.at(gs, wc) : 0u;
+                if (kind && comp(dq[c], j) != sv) A.fail(row0 + j, B2F_CODE_COPY);
+              }
+          } else {
+            copies_edge(A, dq, src, o, rounds, lq);
+          }
         } else {
           atomicOr(status, 1 << B2F_ERR_LAYOUT);
         }
@@ -711,17 +1014,18 @@ __global__ void __launch_bounds__(BLOCK) eval_kernel(const uint32_t* __restrict_
     }
     __syncthreads();
   }
-  // ---- reduce: wave, then one atomic per counter per wave
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int s = 0; s < B2F_NUM_GATES; s++) {
-    uint64_t v = wave_sum(A.gate[s]);
-    if (lane == 0 && v) atomicAdd((unsigned long long*)&rep->gate_failures[s], (unsigned long long)v);
-  }
-  uint64_t lk = wave_sum(A.lookup), cp = wave_sum(A.copy), fm = wave_min(A.first);
-  if (lane == 0) {
-    if (lk) atomicAdd((unsigned long long*)&rep->lookup_failures, (unsigned long long)lk);
-    if (cp) atomicAdd((unsigned long long*)&rep->copy_failures, (unsigned long long)cp);
+  // ---- flush the workgroup's counters: one global atomic per non-zero counter
+  __syncthreads();
+  if (tid < 18) {
+    uint32_t v = L[L_ACC + tid];
+    if (v) {
+      unsigned long long* dst = tid < 16 ? (unsigned long long*)&rep->gate_failures[tid]
+                                         : tid == 16 ? (unsigned long long*)&rep->lookup_failures
+                                                     : (unsigned long long*)&rep->copy_failures;
+      atomicAdd(dst, (unsigned long long)v);
+    }
+  } else if (tid == 18) {
+    uint64_t fm = *reinterpret_cast<const uint64_t*>(L + L_ACC + 20);
     if (fm != ~0ull) atomicMin((unsigned long long*)&rep->first_failure, (unsigned long long)fm);
   }
 }
@@ -744,6 +1048,8 @@ struct b2f_ctx {
   int* d_status;       // [0] fill, [1] eval
   uint64_t* d_rec;     // half-round states
   uint64_t rec_cap;    // in states (16 x u64 each)
+  TileInfo* d_tiles;   // per-tile instance context
+  uint64_t tiles_cap;
   int timing;
   std::vector<hipEvent_t> pool;  // event pairs, reused after every b2f_kernel_times
   std::vector<int> kinds;        // kernel kind of pair i
@@ -787,18 +1093,41 @@ void timed_end(b2f_ctx* ctx, int i, hipStream_t s) {
   if (i >= 0) (void)hipEventRecord(ctx->pool[2 * i + 1], s);
 }
 
+// Diagnostic kernel variants for ablation runs (B2F_DIAG_FILL / B2F_DIAG_EVAL); unset in
+// every product run, where the full kernels launch.
+int diag_mode(const char* var, int full) {
+  const char* v = getenv(var);
+  return v ? atoi(v) : full;
+}
+
 uint64_t layout_rows(uint32_t rounds) {
   if (rounds > B2F_MAX_ROUNDS) return 0;
   return (uint64_t)FIXED_ROWS + (uint64_t)ROUND_ROWS * rounds;
 }
 
-uint64_t grid_tiles(b2f_ctx* ctx, uint64_t total_rows, uint64_t* tiles_per_wg, int wgs_per_cu) {
-  uint64_t tiles = (total_rows + TILE_ROWS - 1) / TILE_ROWS;
-  uint64_t max_wg = (uint64_t)ctx->cu_count * wgs_per_cu;
-  uint64_t wgs = tiles < max_wg ? tiles : max_wg;
-  if (wgs == 0) wgs = 1;
-  *tiles_per_wg = (tiles + wgs - 1) / wgs;
-  return (tiles + *tiles_per_wg - 1) / *tiles_per_wg;
+uint64_t n_tiles_of(uint64_t total_rows) { return (total_rows + TILE_ROWS - 1) / TILE_ROWS; }
+
+uint32_t grid_for(const b2f_ctx* ctx, uint64_t n_tiles, int wgs_per_cu) {
+  uint64_t m = (uint64_t)ctx->cu_count * wgs_per_cu;
+  uint64_t g = n_tiles < m ? n_tiles : m;
+  return (uint32_t)(g ? g : 1);
+}
+
+// per-tile instance context for this call's offsets (scratch owned by the context)
+int launch_tile_index(b2f_ctx* ctx, const uint64_t* d_offsets, size_t n, uint64_t n_tiles,
+                      hipStream_t s) {
+  if (n_tiles > ctx->tiles_cap) {
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    if (ctx->d_tiles) HIPCHK(ctx, hipFree(ctx->d_tiles));
+    ctx->d_tiles = nullptr;
+    ctx->tiles_cap = 0;
+    HIPCHK(ctx, hipMalloc(&ctx->d_tiles, n_tiles * sizeof(TileInfo)));
+    ctx->tiles_cap = n_tiles;
+  }
+  hipLaunchKernelGGL(tile_info_kernel, dim3((uint32_t)((n_tiles + 255) / 256)), dim3(256), 0, s,
+                     d_offsets, (uint32_t)n, n_tiles, ctx->d_tiles);
+  HIPCHK(ctx, hipGetLastError());
+  return B2F_OK;
 }
 
 }  // namespace
@@ -866,6 +1195,7 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipFree(ctx->d_status);
   (void)hipFree(ctx->d_rec);
+  (void)hipFree(ctx->d_tiles);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   delete ctx;
 }
@@ -925,11 +1255,21 @@ B2F_API int b2f_fill_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const ui
                      d_offsets, total_rows, ctx->rec_cap, ctx->d_rec, d_h_out, ctx->d_status);
   HIPCHK(ctx, hipGetLastError());
   timed_end(ctx, tk, s);
-  uint64_t tpw;
-  uint64_t wgs = grid_tiles(ctx, total_rows, &tpw, 8);
+  uint64_t nt = n_tiles_of(total_rows);
+  int rc = launch_tile_index(ctx, d_offsets, n, nt, s);
+  if (rc) return rc;
+  uint32_t wgs = grid_for(ctx, nt, 8);
   tk = timed_begin(ctx, B2F_KERNEL_FILL, s);
-  hipLaunchKernelGGL(fill_kernel, dim3((uint32_t)wgs), dim3(BLOCK), 0, s, d_in, nn, d_offsets,
-                     total_rows, ctx->d_rec, d_advice, d_fixed, ctx->d_status, tpw);
+  switch (diag_mode("B2F_DIAG_FILL", FILL_FULL)) {
+#define B2F_FILL(M)                                                                            \
+  case M:                                                                                      \
+    hipLaunchKernelGGL(fill_kernel<M>, dim3(wgs), dim3(BLOCK), 0, s, d_in, nn, d_offsets,      \
+                       total_rows, ctx->d_rec, d_advice, d_fixed, ctx->d_status, ctx->d_tiles, \
+                       nt);                                                                    \
+    break;
+    B2F_FILL(0) B2F_FILL(1) B2F_FILL(2) default: B2F_FILL(3)
+#undef B2F_FILL
+  }
   HIPCHK(ctx, hipGetLastError());
   timed_end(ctx, tk, s);
   return B2F_OK;
@@ -950,11 +1290,21 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
   HIPCHK(ctx, hipMemsetAsync(ctx->d_status + 1, 0, sizeof(int), s));
   hipLaunchKernelGGL(report_init_kernel, dim3(1), dim3(1), 0, s, d_report, total_rows);
   HIPCHK(ctx, hipGetLastError());
-  uint64_t tpw;
-  uint64_t wgs = grid_tiles(ctx, total_rows, &tpw, 3);
+  uint64_t nt = n_tiles_of(total_rows);
+  int rc = launch_tile_index(ctx, d_offsets, n, nt, s);
+  if (rc) return rc;
+  uint32_t wgs = grid_for(ctx, nt, 3);
   int tk = timed_begin(ctx, B2F_KERNEL_EVAL, s);
-  hipLaunchKernelGGL(eval_kernel, dim3((uint32_t)wgs), dim3(BLOCK), 0, s, d_advice, d_fixed,
-                     d_offsets, (uint32_t)n, total_rows, d_report, ctx->d_status + 1, tpw);
+  switch (diag_mode("B2F_DIAG_EVAL", EVAL_FULL)) {
+#define B2F_EVAL(M)                                                                             \
+  case M:                                                                                       \
+    hipLaunchKernelGGL(eval_kernel<M>, dim3(wgs), dim3(BLOCK), 0, s, d_advice, d_fixed,         \
+                       d_offsets, (uint32_t)n, total_rows, ctx->d_tiles, nt, d_report,          \
+                       ctx->d_status + 1);                                                      \
+    break;
+    B2F_EVAL(1) B2F_EVAL(2) B2F_EVAL(4) B2F_EVAL(8) default: B2F_EVAL(7)
+#undef B2F_EVAL
+  }
   HIPCHK(ctx, hipGetLastError());
   timed_end(ctx, tk, s);
   return B2F_OK;
