@@ -8,7 +8,8 @@ import ctypes
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # zk-odst_amd/
-LIB_PATH = os.path.join(PKG_ROOT, "libb2f.so")
+# B2F_LIB overrides the library path (diagnostic A/B builds of the same ABI)
+LIB_PATH = os.environ.get("B2F_LIB") or os.path.join(PKG_ROOT, "libb2f.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "b2f.h")
 
 NUM_ADVICE = 10

@@ -57,6 +57,34 @@ __constant__ __attribute__((aligned(16))) uint8_t c_gidx[8][4] = {{0, 4, 8, 12},
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// c_gidx / c_sigma repacked for one scalar-friendly load per G
+constexpr uint32_t kGidxWord[8] = {0x0c080400u, 0x0d090501u, 0x0e0a0602u, 0x0f0b0703u,
+                                   0x0f0a0500u, 0x0c0b0601u, 0x0d080702u, 0x0e090403u};
+__constant__ uint32_t c_gidx_word[8] = {0x0c080400u, 0x0d090501u, 0x0e0a0602u, 0x0f0b0703u,
+                                        0x0f0a0500u, 0x0c0b0601u, 0x0d080702u, 0x0e090403u};
+struct SigmaPairs {
+  uint16_t v[10][8];  // SIGMA[r][2g] | SIGMA[r][2g+1] << 8
+};
+constexpr SigmaPairs make_sigma_pairs() {
+  const uint8_t S[10][16] = {
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+      {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+      {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+      {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+      {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+      {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+      {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+      {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+      {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
+  SigmaPairs P{};
+  for (int r = 0; r < 10; r++)
+    for (int g = 0; g < 8; g++) P.v[r][g] = (uint16_t)(S[r][2 * g] | (S[r][2 * g + 1] << 8));
+  return P;
+}
+__constant__ SigmaPairs c_sigma_pairs = make_sigma_pairs();
+#define c_sigma_pair c_sigma_pairs.v
+
 constexpr int BLOCK = 256;            // threads per workgroup = quads per tile
 constexpr int TILE_ROWS = 4 * BLOCK;  // 1024
 constexpr int HALO_ROWS = 16;         // blocks are at most 12 rows
@@ -377,6 +405,101 @@ __global__ void tile_info_kernel(const uint64_t* __restrict__ off, uint32_t n, u
   ti[t] = x;
 }
 
+// Round quads: one branch-free recipe for all eight G steps. The G is recomputed from its
+// half-round state, the step's operands (X, Y, M) are selected, and every row of the quad is
+// built from a per-(quad, row) recipe word, so all lanes of a wave run the same instructions
+// whatever block they are in (LAYOUT.md §4 blocks ADD3/ADD2/XOR/XOR24/XOR63).
+//   bits 0-1 limb k | 2-3 lookup source (0 S = X+Y+M, 1 Z = X^Y, 2 O = X&Y) | 4 lookup >> 8 |
+//   5-6 lookup mask (0 0xffff, 1 0xff, 2 0x7fff) | 7-8 a3/a4 (0 none, 1 dense, 2 spread) |
+//   9 a5 = M_k | 10 a7/a8 = W_k, spread(W_k) | 11 a6 = Z_k >> 15 | 12 a9 = carry |
+//   16-31 selector bits of the row
+struct RowTable {
+  uint32_t r[G_QUADS][4];
+};
+constexpr uint32_t row_recipe(uint32_t k, uint32_t src, uint32_t sh8, uint32_t mask, uint32_t ops,
+                              uint32_t m, uint32_t w, uint32_t zb, uint32_t cy, uint32_t sel) {
+  return k | (src << 2) | (sh8 << 4) | (mask << 5) | (ops << 7) | (m << 9) | (w << 10) |
+         (zb << 11) | (cy << 12) | (sel << 16);
+}
+constexpr uint32_t step_of_quad(uint32_t p) {  // a1 | d1 d1 | c1 | b1 b1 b1 | a2 | d2 d2 | c2 | b2 b2
+  return (p >= 1) + (p >= 3) + (p >= 4) + (p >= 7) + (p >= 8) + (p >= 10) + (p >= 11);
+}
+constexpr RowTable make_rows() {
+  RowTable T{};
+  const uint32_t first_quad[8] = {0, 1, 3, 4, 7, 8, 10, 11};
+  const uint32_t add_sel[8] = {1u << S_A1, 0, 1u << S_C1, 0, 1u << S_A2, 0, 1u << S_C2, 0};
+  for (uint32_t p = 0; p < G_QUADS; p++) {
+    uint32_t st = step_of_quad(p), q = p - first_quad[st];
+    for (uint32_t j = 0; j < 4; j++) {
+      uint32_t R = 4 * q + j, e = 0;
+      if (st % 2 == 0) {  // ADD3 (a1, a2) / ADD2 (c1, c2)
+        e = row_recipe(j, 0, 0, 0, 1, (st == 0 || st == 4) ? 1 : 0, 0, 0, j == 0, j == 0 ? add_sel[st] : 0);
+      } else if (st == 1 || st == 5) {  // XOR (d1, d2)
+        uint32_t sel = R == 0 ? (st == 1 ? 1u << S_D1 : 1u << S_D2) : 0;
+        e = (R % 2 == 0) ? row_recipe(R / 2, 1, 0, 0, 2, 0, 0, 0, 0, sel)
+                         : row_recipe(R / 2, 2, 0, 0, 0, 0, 0, 0, 0, 0);
+      } else if (st == 3) {  // XOR24 (b1)
+        uint32_t k = R / 3, t3 = R % 3, sel = R == 0 ? (1u << S_B1) | (1u << S_EFGH) : 0;
+        e = t3 == 0 ? row_recipe(k, 1, 0, 1, 2, 0, 1, 0, 0, sel)
+                    : t3 == 1 ? row_recipe(k, 1, 1, 1, 0, 0, 0, 0, 0, 0)
+                              : row_recipe(k, 2, 0, 0, 0, 0, 0, 0, 0, 0);
+      } else {  // XOR63 (b2)
+        uint32_t sel = R == 0 ? (1u << S_B2) | (1u << S_IJKL) : 0;
+        e = (R % 2 == 0) ? row_recipe(R / 2, 1, 0, 2, 2, 0, 1, 1, 0, sel)
+                         : row_recipe(R / 2, 2, 0, 0, 0, 0, 0, 0, 0, 0);
+      }
+      T.r[p][j] = e;
+    }
+  }
+  return T;
+}
+__constant__ __attribute__((aligned(16))) RowTable c_rows = make_rows();
+
+__device__ __forceinline__ void quad_round(Quad& Q, uint64_t a, uint64_t b, uint64_t c,
+                                           uint64_t d, uint64_t mx, uint64_t my, uint32_t p,
+                                           const uint32_t* __restrict__ rows) {
+  const uint64_t a1 = a + b + mx;
+  const uint64_t d1 = rotr64(d ^ a1, 32);
+  const uint64_t c1 = c + d1;
+  const uint64_t b1 = rotr64(b ^ c1, 24);
+  const uint64_t a2 = a1 + b1 + my;
+  const uint64_t d2 = rotr64(d1 ^ a2, 16);
+  const uint64_t c2 = c1 + d2;
+  const uint32_t st = (p >= 1) + (p >= 3) + (p >= 4) + (p >= 7) + (p >= 8) + (p >= 10) + (p >= 11);
+  const uint64_t X = st == 0 ? a : st == 1 ? d : st == 2 ? c : st == 3 ? b
+                   : st == 4 ? a1 : st == 5 ? d1 : st == 6 ? c1 : b1;
+  const uint64_t Y = st == 0 ? b : st == 1 ? a1 : st == 2 ? d1 : st == 3 ? c1
+                   : st == 4 ? b1 : st == 5 ? a2 : st == 6 ? d2 : c2;
+  const uint64_t M = st == 0 ? mx : st == 4 ? my : 0ull;
+  const uint64_t s1 = X + Y, S = s1 + M;
+  const uint32_t carry = (uint32_t)(s1 < X) + (uint32_t)(S < s1);
+  const uint64_t Z = X ^ Y, O = X & Y;
+  const uint64_t W = st == 3 ? rotr64(Z, 24) : rotr64(Z, 63);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t e = rows[4 * p + j];
+    const uint32_t sh = 16 * (e & 3u);
+    const uint32_t srcw = (e >> 2) & 3u;
+    const uint64_t V = srcw == 0 ? S : srcw == 1 ? Z : O;
+    const uint32_t mcode = (e >> 5) & 3u;
+    const uint32_t v = (uint32_t)(V >> (sh + 8 * ((e >> 4) & 1u))) &
+                       (mcode == 0 ? 0xffffu : mcode == 1 ? 0xffu : 0x7fffu);
+    lrow(Q, j, v);
+    const uint32_t xk = (uint32_t)(X >> sh) & 0xffffu, yk = (uint32_t)(Y >> sh) & 0xffffu;
+    const uint32_t ops = (e >> 7) & 3u;
+    Q.c[A3][j] = ops == 1 ? xk : ops == 2 ? spread16(xk) : 0u;
+    Q.c[A4][j] = ops == 1 ? yk : ops == 2 ? spread16(yk) : 0u;
+    Q.c[A5][j] = (e >> 9) & 1u ? (uint32_t)(M >> sh) & 0xffffu : 0u;
+    Q.c[A6][j] = (e >> 11) & 1u ? ((uint32_t)(Z >> sh) & 0xffffu) >> 15 : 0u;
+    const uint32_t wk = (uint32_t)(W >> sh) & 0xffffu;
+    const bool hw = (e >> 10) & 1u;
+    Q.c[A7][j] = hw ? wk : 0u;
+    Q.c[A8][j] = hw ? spread16(wk) : 0u;
+    Q.c[A9][j] = (e >> 12) & 1u ? carry : 0u;
+    Q.fx[j] = e >> 16;
+  }
+}
+
 // MODE (diagnostics; the product uses FILL_FULL): bit 0 = compute the cells (else zeros),
 // bit 1 = non-temporal stores (else plain stores).
 enum { FILL_COMPUTE = 1, FILL_NT = 2, FILL_FULL = 3 };
@@ -395,6 +518,9 @@ __global__ void __launch_bounds__(BLOCK) fill_kernel(const b2f_input* __restrict
                                                     const int* __restrict__ status,
                                                     const TileInfo* __restrict__ tinfo,
                                                     uint64_t n_tiles) {
+  __shared__ uint32_t rows[G_QUADS * 4];
+  if (threadIdx.x < G_QUADS * 4) rows[threadIdx.x] = (&c_rows.r[0][0])[threadIdx.x];
+  __syncthreads();
   if (*status) return;  // the record kernel rejected the layout: write nothing
   const uint64_t total_quads = total_rows >> 2;
   const uint64_t used_rows = off[n];
@@ -411,7 +537,18 @@ __global__ void __launch_bounds__(BLOCK) fill_kernel(const b2f_input* __restrict
       const b2f_input* x = in + inst;
       uint32_t rounds = x->rounds;
       const uint64_t* states = rec + 16ull * state_index(o, inst);
-      quad_cells(Q, x, states, rounds, (uint32_t)((row - o) >> 2));
+      const uint32_t lq = (uint32_t)((row - o) >> 2), rq = lq - INIT_QUADS;
+      if (lq >= INIT_QUADS && rq < ROUND_QUADS * rounds) {
+        const uint32_t r = rq / ROUND_QUADS, w = rq - r * ROUND_QUADS;
+        const uint32_t g = w / G_QUADS, p = w - g * G_QUADS;
+        const uint64_t* st = states + 16ull * (2ull * r + (g >= 4));
+        const uint32_t gi = c_gidx_word[g];  // a | b << 8 | c << 16 | d << 24
+        const uint32_t sg = c_sigma_pair[r % 10][g];
+        quad_round(Q, st[gi & 0xff], st[(gi >> 8) & 0xff], st[(gi >> 16) & 0xff], st[gi >> 24],
+                   x->m[sg & 0xff], x->m[sg >> 8], p, rows);
+      } else {
+        quad_cells(Q, x, states, rounds, lq);  // init and final regions
+      }
     }
 #pragma unroll
     for (int c = 0; c < 11; c++) {
@@ -744,6 +881,120 @@ __device__ __forceinline__ bool gate_ok(const Tile& T, int s, uint32_t r, uint32
   return true;
 }
 
+// Block gate evaluators: the gates of one block from 4-row LDS vectors (ds_read_b128), for
+// the selector patterns LAYOUT v1 writes. Each returns the mask of failing selector bits.
+// Any other selector combination (only a corrupted fixed column has one) is evaluated one
+// gate at a time by gate_ok. Both paths check the same identities.
+struct V3 {  // 12 consecutive rows of one column
+  uint4 a, b, c;
+  __device__ __forceinline__ uint32_t operator[](int i) const {
+    const uint4& v = i < 4 ? a : (i < 8 ? b : c);
+    return comp(v, i & 3);
+  }
+};
+__device__ __forceinline__ V3 rows12(const Tile& T, int col, uint32_t r) {
+  return V3{T.quad(col, r), T.quad(col, r + 4), T.quad(col, r + 8)};
+}
+__device__ __forceinline__ V3 rows8(const Tile& T, int col, uint32_t r) {
+  return V3{T.quad(col, r), T.quad(col, r + 4), make_uint4(0, 0, 0, 0)};
+}
+
+// XOR (s_spread_d1, s_spread_d2, s_xor) and XOR3 (s_xor3): operands on the even rows
+__device__ __forceinline__ bool g_xor(const Tile& T, uint32_t r, bool three) {
+  V3 s2 = rows8(T, A2, r);
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint64_t in = (uint64_t)T.at(A3, r + 2 * k) + T.at(A4, r + 2 * k) + (three ? T.at(A5, r + 2 * k) : 0u);
+    ok &= in == (uint64_t)s2[2 * k] + 2 * (uint64_t)s2[2 * k + 1];
+  }
+  return ok;
+}
+__device__ __forceinline__ bool g_digest(const Tile& T, uint32_t r) {
+  V3 d = rows8(T, A1, r);
+  return (uint64_t)T.at(A7, r) == (uint64_t)d[0] + ((uint64_t)d[2] << 16) &&
+         (uint64_t)T.at(A8, r) == (uint64_t)d[4] + ((uint64_t)d[6] << 16);
+}
+__device__ __forceinline__ bool g_add(const Tile& T, uint32_t r, uint32_t a9, bool three) {
+  typedef unsigned __int128 u128;
+  uint4 s = T.quad(A1, r), x = T.quad(A3, r), y = T.quad(A4, r);
+  uint4 z = three ? T.quad(A5, r) : make_uint4(0, 0, 0, 0);
+  u128 lhs = 0, rhs = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    lhs += (u128)((uint64_t)comp(x, k) + comp(y, k) + comp(z, k)) << (16 * k);
+    rhs += (u128)comp(s, k) << (16 * k);
+  }
+  rhs += (u128)a9 << 64;
+  return lhs == rhs && a9 <= (three ? 2u : 1u);
+}
+__device__ __forceinline__ uint32_t g_xor24(const Tile& T, uint32_t r, uint32_t sel) {
+  bool b1 = true, efgh = true;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t b = r + 3 * k, k1 = r + 3 * ((k + 1) & 3), k2 = r + 3 * ((k + 2) & 3);
+    b1 &= (uint64_t)T.at(A3, b) + T.at(A4, b) ==
+          (uint64_t)T.at(A2, b) + ((uint64_t)T.at(A2, b + 1) << 16) + 2 * (uint64_t)T.at(A2, b + 2);
+    b1 &= (T.at(A0, b) | T.at(A0, b + 1)) == 0u;
+    efgh &= (uint64_t)T.at(A7, b) == (uint64_t)T.at(A1, k1 + 1) + ((uint64_t)T.at(A1, k2) << 8);
+    efgh &= (uint64_t)T.at(A8, b) == (uint64_t)T.at(A2, k1 + 1) + ((uint64_t)T.at(A2, k2) << 16);
+  }
+  return ((b1 ? 0u : 1u << S_B1) | (efgh ? 0u : 1u << S_EFGH)) & sel;
+}
+__device__ __forceinline__ uint32_t g_xor63(const Tile& T, uint32_t r, uint32_t sel) {
+  V3 a2 = rows8(T, A2, r);
+  bool b2 = true, ijkl = true;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t b = 2 * k, k3 = 2 * ((k + 3) & 3);
+    uint32_t zb = T.at(A6, r + b), zp = T.at(A6, r + k3);
+    b2 &= (uint64_t)T.at(A3, r + b) + T.at(A4, r + b) ==
+          (uint64_t)a2[b] + ((uint64_t)zb << 30) + 2 * (uint64_t)a2[b + 1];
+    b2 &= T.at(A0, r + b) <= 1u && zb <= 1u;
+    ijkl &= (uint64_t)T.at(A7, r + b) == (uint64_t)zp + 2 * (uint64_t)T.at(A1, r + b);
+    ijkl &= (uint64_t)T.at(A8, r + b) == (uint64_t)zp + 4 * (uint64_t)a2[b];
+  }
+  return ((b2 ? 0u : 1u << S_B2) | (ijkl ? 0u : 1u << S_IJKL)) & sel;
+}
+
+// Any selector combination, one gate at a time (kept out of line: the hot path never takes it
+// for a trace this engine wrote).
+__device__ __noinline__ uint32_t gates_generic(const Tile& T, uint32_t sel, uint32_t r, uint32_t a9,
+                                               uint32_t k0) {
+  uint32_t failed = 0;
+  while (sel) {
+    int s = __builtin_ctz(sel);
+    sel &= sel - 1;
+    if (!gate_ok(T, s, r, a9, k0)) failed |= 1u << s;
+  }
+  return failed;
+}
+
+// Failing selector bits of selector row r (tile-local).
+__device__ __forceinline__ uint32_t row_gates(const Tile& T, uint32_t sel, uint32_t r, uint32_t a9,
+                                              uint32_t k0) {
+  switch (sel) {
+    case 1u << S_D1:
+    case 1u << S_D2:
+    case 1u << S_XOR:
+      return g_xor(T, r, false) ? 0u : sel;
+    case 1u << S_A1:
+    case 1u << S_A2:
+      return g_add(T, r, a9, true) ? 0u : sel;
+    case 1u << S_C1:
+    case 1u << S_C2:
+      return g_add(T, r, a9, false) ? 0u : sel;
+    case (1u << S_B1) | (1u << S_EFGH):
+      return g_xor24(T, r, sel);
+    case (1u << S_B2) | (1u << S_IJKL):
+      return g_xor63(T, r, sel);
+    case (1u << S_XOR3) | (1u << S_DIGEST):
+      return (g_xor(T, r, true) ? 0u : 1u << S_XOR3) | (g_digest(T, r) ? 0u : 1u << S_DIGEST);
+    default:
+      return gates_generic(T, sel, r, a9, k0);
+  }
+}
+
 // Copy-source lookup, all from LDS for a valid trace: rows inside the window come from W;
 // init-region words (h, m, t, fmask, IV, v12..v14) of the tile's first instance, which may
 // start before the window, from the init cache I (a_1 | a_2 of its rows 0..163). Anything
@@ -824,58 +1075,75 @@ __device__ void copies_edge(EvalAcc& A, const uint4* dst, const Src& src, uint64
 // MODE (diagnostics; the product uses EVAL_FULL): which checks run on a staged tile.
 enum { EVAL_LOOKUP = 1, EVAL_GATES = 2, EVAL_COPIES = 4, EVAL_FULL = 7, EVAL_TOUCH = 8 };
 
-// Issue the load behind extra slot `slot` of tile t (history / halo / init cache / info).
-// fo = {first, -, off[first]} of tile t (only the init slots use it).
-__device__ __forceinline__ uint4 extra_load(int slot, uint64_t t, const uint4& fo,
-                                            const uint32_t* __restrict__ adv,
-                                            uint64_t total_rows, uint64_t total_quads, uint32_t n,
-                                            const TileInfo* __restrict__ tinfo) {
-  const uint64_t tile0 = t * TILE_ROWS;
-  const uint4 z = make_uint4(0, 0, 0, 0);
+// The two extra (non-own-quad) loads a thread issues per tile, as a compact descriptor:
+// kind, LDS destination, and a base pointer the tile position is added to.
+enum { XK_NONE = 0, XK_HIST, XK_HALO, XK_INIT, XK_INFO };
+struct Extra {
+  const uint32_t* base;  // HIST/HALO: + tile0 rows; INIT: + off[first]; INFO: + 24 t words
+  uint32_t lds;          // LDS word offset of the 16-byte destination
+  uint32_t kind;
+  uint32_t q;            // HALO: quad index inside the halo
+};
+
+__device__ __forceinline__ Extra make_extra(int slot, const uint32_t* adv, uint64_t total_rows,
+                                            const TileInfo* tinfo) {
+  Extra x;
+  x.q = 0;
   if (slot < X_HIST) {
     int ci = slot / (HIST / 4), hq = slot - ci * (HIST / 4);
     int col = ci == 0 ? A1 : ci == 1 ? A2 : ci == 2 ? A7 : A8;
-    if (tile0 < (uint64_t)HIST) return z;
-    return *reinterpret_cast<const uint4*>(adv + (uint64_t)col * total_rows + tile0 - HIST + 4 * hq);
-  }
-  if (slot < X_HALO) {
-    int e = slot - X_HIST, gi = e >> 2, q = e & 3;
-    const int cols[9] = {A0, A1, A2, A3, A4, A5, A6, A7, A8};
-    uint64_t hq = (t + 1) * BLOCK + q;
-    if (hq >= total_quads) return z;
-    return *reinterpret_cast<const uint4*>(adv + (uint64_t)cols[gi] * total_rows + 4 * hq);
-  }
-  if (slot < X_INIT) {
-    int e = slot - X_HALO, ci = e / INIT_QUADS, q = e - ci * INIT_QUADS;
-    uint64_t of = ((uint64_t)fo.w << 32) | fo.z;
-    if (fo.x >= n || of + INIT_ROWS > total_rows) return z;
-    return *reinterpret_cast<const uint4*>(adv + (uint64_t)(A1 + ci) * total_rows + of + 4 * q);
-  }
-  if (slot < X_INFO) return reinterpret_cast<const uint4*>(tinfo + t)[slot - X_INIT];
-  return z;
-}
-
-__device__ __forceinline__ void extra_store(uint32_t* L, int slot, const uint4& v) {
-  int w;
-  if (slot < X_HIST) {
-    int ci = slot / (HIST / 4), hq = slot - ci * (HIST / 4);
-    w = L_W + ci * WSTRIDE + 4 * hq;
+    x.kind = XK_HIST;
+    x.base = adv + (uint64_t)col * total_rows - HIST + 4 * hq;
+    x.lds = L_W + ci * WSTRIDE + 4 * hq;
   } else if (slot < X_HALO) {
     int e = slot - X_HIST, gi = e >> 2, q = e & 3;
-    w = lds_cell(gi, TILE_ROWS + 4 * q);  // gate columns a_0..a_8 in order
+    x.kind = XK_HALO;
+    x.q = q;
+    x.base = adv + (uint64_t)gi * total_rows + TILE_ROWS + 4 * q;  // gate columns a_0..a_8
+    x.lds = lds_cell(gi, TILE_ROWS + 4 * q);
   } else if (slot < X_INIT) {
     int e = slot - X_HALO, ci = e / INIT_QUADS, q = e - ci * INIT_QUADS;
-    w = L_IC + ci * INIT_ROWS + 4 * q;
+    x.kind = XK_INIT;
+    x.base = adv + (uint64_t)(A1 + ci) * total_rows + 4 * q;
+    x.lds = L_IC + ci * INIT_ROWS + 4 * q;
   } else if (slot < X_INFO) {
-    w = L_INFO + 4 * (slot - X_INIT);
+    x.kind = XK_INFO;
+    x.base = reinterpret_cast<const uint32_t*>(tinfo) + 4 * (slot - X_INIT);
+    x.lds = L_INFO + 4 * (slot - X_INIT);
   } else {
-    return;
+    x.kind = XK_NONE;
+    x.base = adv;
+    x.lds = 0;
   }
-  *reinterpret_cast<uint4*>(&L[w]) = v;
+  return x;
+}
+
+// fo = {first, -, off[first] lo, hi} of tile t (only INIT slots read it)
+__device__ __forceinline__ uint4 extra_load(const Extra& x, uint64_t t, const uint4& fo, uint32_t n,
+                                            uint64_t total_rows, uint64_t total_quads) {
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  const uint64_t tile0 = t * TILE_ROWS;
+  switch (x.kind) {
+    case XK_HIST:
+      return tile0 >= (uint64_t)HIST ? *reinterpret_cast<const uint4*>(x.base + tile0) : z;
+    case XK_HALO:
+      return (t + 1) * BLOCK + x.q < total_quads ? *reinterpret_cast<const uint4*>(x.base + tile0) : z;
+    case XK_INIT: {
+      uint64_t of = ((uint64_t)fo.w << 32) | fo.z;
+      return (fo.x < n && of + INIT_ROWS <= total_rows) ? *reinterpret_cast<const uint4*>(x.base + of) : z;
+    }
+    case XK_INFO:
+      return *reinterpret_cast<const uint4*>(x.base + 24 * t);
+    default:
+      return z;
+  }
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(BLOCK, 3) eval_kernel(const uint32_t* __restrict__ adv,
+#ifndef B2F_EVAL_WAVES
+#define B2F_EVAL_WAVES 3  // waves per SIMD the eval kernel is compiled for (LDS allows 3 WGs/CU)
+#endif
+__global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint32_t* __restrict__ adv,
                                                     const uint32_t* __restrict__ fixed,
                                                     const uint64_t* __restrict__ off, uint32_t n,
                                                     uint64_t total_rows,
@@ -903,6 +1171,8 @@ __global__ void __launch_bounds__(BLOCK, 3) eval_kernel(const uint32_t* __restri
   const bool init_role = tid + BLOCK >= X_HALO && tid + BLOCK < X_INIT;  // slot tid+256
 
   uint64_t t = blockIdx.x;
+  const Extra e0 = make_extra(tid, adv, total_rows, tinfo);
+  const Extra e1 = make_extra(tid + BLOCK, adv, total_rows, tinfo);
   uint4 q[NCOL_T], x0 = make_uint4(0, 0, 0, 0), x1 = x0, fo = x0, fo_next = x0;
   auto load_tile = [&](uint64_t tt, const uint4& f) {
     const uint64_t gq = tt * BLOCK + tid;
@@ -911,8 +1181,8 @@ __global__ void __launch_bounds__(BLOCK, 3) eval_kernel(const uint32_t* __restri
       q[c] = gq < total_quads
                  ? *reinterpret_cast<const uint4*>((c < 10 ? adv + (uint64_t)c * total_rows : fixed) + 4 * gq)
                  : make_uint4(0, 0, 0, 0);
-    x0 = extra_load(tid, tt, f, adv, total_rows, total_quads, n, tinfo);
-    x1 = extra_load(tid + BLOCK, tt, f, adv, total_rows, total_quads, n, tinfo);
+    x0 = extra_load(e0, tt, f, n, total_rows, total_quads);
+    x1 = extra_load(e1, tt, f, n, total_rows, total_quads);
   };
   if (layout_ok && t < n_tiles) {
     if (init_role) fo = *reinterpret_cast<const uint4*>(tinfo + t);
@@ -924,15 +1194,20 @@ __global__ void __launch_bounds__(BLOCK, 3) eval_kernel(const uint32_t* __restri
 #pragma unroll
     for (int c = 0; c < 9; c++) *reinterpret_cast<uint4*>(&L[lds_cell(c, 4 * tid)]) = q[c];
     const uint4 cur9 = q[A9], curfx = q[10];
-    extra_store(L, tid, x0);
-    extra_store(L, tid + BLOCK, x1);
+    if (e0.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e0.lds]) = x0;
+    if (e1.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e1.lds]) = x1;
     __syncthreads();
     // ---- prefetch tile t + G into registers while tile t is checked
     const uint64_t tn = t + G;
-    if (tn < n_tiles) {
-      load_tile(tn, fo_next);
-      if (init_role && tn + G < n_tiles) fo_next = *reinterpret_cast<const uint4*>(tinfo + tn + G);
-    }
+    auto prefetch = [&]() {
+      if (tn < n_tiles) {
+        load_tile(tn, fo_next);
+        if (init_role && tn + G < n_tiles) fo_next = *reinterpret_cast<const uint4*>(tinfo + tn + G);
+      }
+    };
+#ifndef B2F_PREFETCH_LATE
+    prefetch();
+#endif
     const uint64_t tile0 = t * TILE_ROWS;
     const uint64_t gq = t * BLOCK + tid;
     if ((MODE & EVAL_TOUCH) && gq < total_quads) {  // diagnostics: keep the staged words alive
@@ -945,36 +1220,52 @@ __global__ void __launch_bounds__(BLOCK, 3) eval_kernel(const uint32_t* __restri
       const uint64_t row0 = 4 * gq;
       const uint32_t lr0 = 4 * tid;
       // ---- lookups and gates on the 4 rows
-      const uint4 q0 = T.quad(A0, lr0), q1 = T.quad(A1, lr0), q2 = T.quad(A2, lr0);
-#pragma unroll 1
-      for (int j = 0; j < 4; j++) {
-        uint32_t tg = comp(q0, j), de = comp(q1, j), sp = comp(q2, j);
-        bool ok = de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu);
-        if ((MODE & EVAL_LOOKUP) && !ok) A.fail(row0 + j, B2F_CODE_LOOKUP);
-        uint32_t k0 = comp(curfx, j);
-        uint32_t sel = (MODE & EVAL_GATES) ? k0 & 0xffffu : 0u;
-        const uint32_t a9 = comp(cur9, j);
-        uint32_t failed = 0;  // gates failing on this row (bit per selector)
-        while (sel) {
-          int s = __builtin_ctz(sel);
-          sel &= sel - 1;
-          if (!gate_ok(T, s, lr0 + j, a9, k0)) failed |= 1u << s;
+      if (MODE & EVAL_LOOKUP) {
+        const uint4 q0 = T.quad(A0, lr0), q1 = T.quad(A1, lr0), q2 = T.quad(A2, lr0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          uint32_t tg = comp(q0, j), de = comp(q1, j), sp = comp(q2, j);
+          bool ok = de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu);
+          if (!ok) A.fail(row0 + j, B2F_CODE_LOOKUP);
         }
-        if (failed) A.fail_gates(row0 + j, failed);
       }
+      if (MODE & EVAL_GATES) {
+        // rows of this quad that carry a selector (a block starts at j = 0; CONST has one
+        // on every row)
+        uint32_t rowmask = ((curfx.x & 0xffffu) ? 1u : 0u) | ((curfx.y & 0xffffu) ? 2u : 0u) |
+                           ((curfx.z & 0xffffu) ? 4u : 0u) | ((curfx.w & 0xffffu) ? 8u : 0u);
+        while (rowmask) {
+          int j = __builtin_ctz(rowmask);
+          rowmask &= rowmask - 1;
+          uint32_t k0 = comp(curfx, j);
+          uint32_t failed;
+          if ((k0 & 0xffffu) == (1u << S_CONST)) failed = T.at(A1, lr0 + j) == (k0 >> 16) ? 0u : 1u << S_CONST;
+          else failed = row_gates(T, k0 & 0xffffu, lr0 + j, comp(cur9, j), k0);
+          if (failed) A.fail_gates(row0 + j, failed);
+        }
+      }
+#ifdef B2F_PREFETCH_LATE
+    }
+    prefetch();  // after the gates: their registers are free again
+    if (gq < total_quads) {
+      const uint64_t row0 = 4 * gq;
+      const uint32_t lr0 = 4 * tid;
+#endif
       // ---- copy constraints whose operand cell lies in this quad
       const uint32_t first = L[L_INFO];
       const uint64_t* Off = reinterpret_cast<const uint64_t*>(L + L_INFO + 2);
       if ((MODE & EVAL_COPIES) && row0 < used_rows) {
         // instance of this quad: scan the tile's offsets in LDS (global beyond 8 instances)
         uint32_t inst = first, i = 0;
-        while (i + 1 < NOFF && Off[i + 1] <= row0) i++;
+        while (i + 2 < NOFF && Off[i + 1] <= row0) i++;
         inst += i;
-        uint64_t o = Off[i], o1 = i + 1 < NOFF ? Off[i + 1] : off[inst + 1];
-        while (o1 <= row0) { inst++; o = o1; o1 = off[inst + 1]; }
+        uint64_t o = Off[i], o1 = Off[i + 1];
+        if (o1 <= row0) {  // more than NOFF - 1 instances start in this tile (tiny rounds)
+          do { inst++; o = o1; o1 = off[inst + 1]; } while (o1 <= row0);
+        }
         uint64_t R = o1 - o;
         const Src src{L + L_W, L + L_IC, adv, total_rows, tile0 - HIST, first < n ? Off[0] : ~0ull};
-        const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
+
         if (o1 > o && o1 <= total_rows && R >= FIXED_ROWS && (R - FIXED_ROWS) % ROUND_ROWS == 0 &&
             (R - FIXED_ROWS) / ROUND_ROWS <= B2F_MAX_ROUNDS) {
           uint32_t rounds = (uint32_t)((R - FIXED_ROWS) / ROUND_ROWS);
@@ -987,7 +1278,9 @@ __global__ void __launch_bounds__(BLOCK, 3) eval_kernel(const uint32_t* __restri
             const bool hr0 = (r == 0) && (g < 4);
             const uint32_t* ct = L + L_CT + (g * G_QUADS + p) * 12;
             const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
-#pragma unroll 1
+            const uint64_t wlo = tile0 - HIST, ofirst = src.ofirst;
+            uint32_t bad = 0;  // failing operand cells, bit 3*j + c
+#pragma unroll
             for (int j = 0; j < 4; j++)
 #pragma unroll
               for (int c = 0; c < 3; c++) {
@@ -1001,10 +1294,22 @@ __global__ void __launch_bounds__(BLOCK, 3) eval_kernel(const uint32_t* __restri
                 uint64_t gs = from_init ? o + init_row
                                         : gbase + (uint64_t)(int64_t)((int)((e >> 7) & 1023u) - 512);
                 uint32_t wc = (kind == 2 && hr0) ? (e >> 25) & 3u : (e >> 2) & 3u;
-                uint32_t sv = kind ? src.at(gs, wc) : 0u;
-                if (kind && comp(dq[c], j) != sv) A.fail(row0 + j, B2F_CODE_COPY);
+                // the source is in the LDS window or the init cache for every valid layout
+                uint64_t dw = gs - wlo, di = gs - ofirst;
+                bool in_w = dw < (uint64_t)WSTRIDE, in_i = di < (uint64_t)INIT_ROWS && wc < 2;
+                uint32_t idx = in_w ? L_W + wc * WSTRIDE + (uint32_t)dw
+                                    : L_IC + (wc & 1u) * INIT_ROWS + (in_i ? (uint32_t)di : 0u);
+                uint32_t sv = L[idx];
+                if (kind && !in_w && !in_i) sv = src.at(gs, wc);  // corrupted layout only
+                bad |= (kind && T.at(A3 + c, lr0 + j) != sv) ? 1u << (3 * j + c) : 0u;
               }
+            while (bad) {
+              int b = __builtin_ctz(bad);
+              bad &= bad - 1;
+              A.fail(row0 + b / 3, B2F_CODE_COPY);
+            }
           } else {
+            const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
             copies_edge(A, dq, src, o, rounds, lq);
           }
         } else {
