@@ -73,6 +73,8 @@ def main():
     ap.add_argument("--mix", action="store_true", help="rounds uniform in {1,4,12} (config 5)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--export-rows", type=int, default=1 << 25,
+                    help="rows of the Fp export timed after the headline loop (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
     args = ap.parse_args()
@@ -174,6 +176,27 @@ def main():
     roof = {"bound": "hbm", "achieved": kern[dom]["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": kern[dom]["frac"], "traffic": traffic, "kernel": dom}
 
+    # Fp export, reported beside the headline, not part of it:
+    # Montgomery pallas limbs for a chunk of the resident trace (4 B read, 32 B written/cell)
+    fp_export = None
+    if args.export_rows > 0:
+        nr = min(args.export_rows, batch.total_rows)
+        out = torch.empty((10, nr, 4), dtype=torch.int64, device=batch.advice.device)
+        batch.export_fp(eng, nrows=nr, out=out, stream=stream)
+        eng.sync(stream)
+        eng.set_timing(True)
+        reps = 5
+        for _ in range(reps):
+            batch.export_fp(eng, nrows=nr, out=out, stream=stream)
+        tot, cnt = eng.kernel_times()["export"]
+        avg = tot / max(cnt, 1)
+        nbytes = nr * 10 * (4 + 32)
+        fp_export = {"rows": nr, "form": "montgomery", "avg_ms": round(avg, 4),
+                     "bytes_per_launch": nbytes,
+                     "achieved_GBs": round(nbytes / (avg * 1e-3) / 1e9, 1),
+                     "frac": round(nbytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        del out
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.rounds, mix, args.cpu_seconds)
@@ -191,7 +214,7 @@ def main():
                           "rounds": "mix{1,4,12}" if mix else args.rounds,
                           "rows_per_gpu": rows, "trace_bytes_per_gpu": rows * ROW_BYTES,
                           "parallelism": "dp%d (instance shards)" % world},
-               "roofline": roof, "cpu_baseline": cpu, "kernels": kern,
+               "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "fp_export": fp_export,
                "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None}
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -130,6 +130,22 @@ B2F_API int b2f_eval(b2f_ctx* ctx, const uint32_t* advice, const uint32_t* fixed
                      const uint64_t* offsets, size_t n, uint64_t total_rows,
                      b2f_eval_report* report);
 
+/* Fp export: advice cells as pallas::Base elements (pasta_curves
+ * 0.5.1 Fp, p = 0x40000000000000000000000000000000224698fc094cf91b992d30ed00000001), the
+ * form halo2's prover keeps its advice columns in. Rows [row_begin, row_begin + nrows) of
+ * the ten advice columns are written in halo2 column order (b2f_halo2_column_index):
+ * element of a_i at row row_begin + r goes to d_out[(h * out_rows + r) * 4 + limb],
+ * h = b2f_halo2_column_index(i), 4 little-endian u64 limbs. out_rows >= nrows is the
+ * column stride (rows past nrows are not written; a prover zero-fills to 2^k).
+ *   form B2F_FP_MONTGOMERY: x * 2^256 mod p (the in-memory Fp of pasta_curves)
+ *   form B2F_FP_CANONICAL:  x as a 32-byte little-endian integer (PrimeField::to_repr)
+ * d_out must be 16-byte aligned. Asynchronous on `stream`. */
+#define B2F_FP_CANONICAL 0
+#define B2F_FP_MONTGOMERY 1
+B2F_API int b2f_export_fp_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t total_rows,
+                              uint64_t row_begin, uint64_t nrows, uint32_t form,
+                              uint64_t* d_out, uint64_t out_rows, void* stream);
+
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel the
  * fill/eval calls launch (no host synchronization while recording). b2f_set_timing(ctx, 1)
  * clears the log and starts recording; b2f_kernel_times waits for the recorded events and
@@ -138,7 +154,8 @@ B2F_API int b2f_eval(b2f_ctx* ctx, const uint32_t* advice, const uint32_t* fixed
 #define B2F_KERNEL_RECORD 0 /* BLAKE2f compression + half-round states (fill, part 1) */
 #define B2F_KERNEL_FILL 1   /* trace expansion (fill, part 2) */
 #define B2F_KERNEL_EVAL 2   /* constraint evaluation */
-#define B2F_NUM_KERNELS 3
+#define B2F_KERNEL_EXPORT 3 /* Fp export */
+#define B2F_NUM_KERNELS 4
 B2F_API int b2f_set_timing(b2f_ctx* ctx, int enable);
 B2F_API int b2f_kernel_times(b2f_ctx* ctx, double* total_ms, uint32_t* count);
 

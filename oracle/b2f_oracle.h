@@ -67,6 +67,16 @@ int orc_fill(const orc_input* in, size_t n, const uint64_t* offsets, uint64_t to
 int orc_eval(const uint32_t* advice, const uint32_t* fixed, const uint64_t* offsets, size_t n,
              uint64_t total_rows, orc_report* rep, int nthreads);
 
+/* Fp export restatement: rows [row_begin, row_begin+nrows) of the
+ * advice columns as pasta_curves 0.5.1 pallas Fp elements (4 LE u64 limbs), halo2 column
+ * order h = {a_5,a_3,a_4,a_6,a_7,a_8,a_9,a_0,a_1,a_2} (table16.rs:281-294):
+ * out[(h*out_rows + r)*4 + limb]. form 0 = canonical (to_repr), 1 = Montgomery x*2^256 mod p,
+ * computed the textbook way (CIOS Montgomery product of x with R^2 mod p). */
+void orc_export_fp(const uint32_t* advice, uint64_t total_rows, uint64_t row_begin,
+                   uint64_t nrows, uint32_t form, uint64_t* out, uint64_t out_rows);
+/* One Montgomery conversion (the same routine), for pinning against big-integer math. */
+void orc_fp_mont(uint32_t x, uint64_t out[4]);
+
 int orc_max_threads(void);
 
 #ifdef __cplusplus

@@ -64,6 +64,9 @@ def lib():
         L.orc_eval.argtypes = [P, P, P, ctypes.c_size_t, ctypes.c_uint64, P, ctypes.c_int]
         L.orc_eval.restype = ctypes.c_int
         L.orc_max_threads.restype = ctypes.c_int
+        L.orc_export_fp.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                    ctypes.c_uint32, P, ctypes.c_uint64]
+        L.orc_fp_mont.argtypes = [ctypes.c_uint32, P]
         _lib = L
     return _lib
 
@@ -124,6 +127,27 @@ def evaluate(adv, fixed, off, nthreads=0):
     if rc != 0:
         raise ValueError("orc_eval: offsets are not a LAYOUT v1 row map")
     return rep.as_dict()
+
+
+FP_CANONICAL, FP_MONTGOMERY = 0, 1
+
+
+def export_fp(adv, row_begin=0, nrows=None, form=FP_MONTGOMERY, out_rows=None):
+    """Fp export restatement: returns u64 [10 (halo2 order), out_rows, 4] (rows past nrows
+    zero)."""
+    adv = np.ascontiguousarray(adv, dtype=np.uint32)
+    total = adv.shape[1]
+    nrows = total - row_begin if nrows is None else int(nrows)
+    out_rows = nrows if out_rows is None else int(out_rows)
+    out = np.zeros((NCOLS, out_rows, 4), dtype=np.uint64)
+    lib().orc_export_fp(_p(adv), total, int(row_begin), nrows, int(form), _p(out), out_rows)
+    return out
+
+
+def fp_mont(x):
+    out = np.zeros(4, dtype=np.uint64)
+    lib().orc_fp_mont(int(x), _p(out))
+    return out
 
 
 def max_threads():

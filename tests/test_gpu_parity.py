@@ -159,3 +159,47 @@ def test_padded_tail_rows_zero(engine, orc):
     used = batch.used_rows
     assert not adv[:, used:].any() and not fixed[used:].any()
     assert batch.report_dict() == orc.evaluate(adv, fixed, batch.offsets_host)
+
+
+def test_fp_export_matches_oracle(engine, orc):
+    """Fp export kernel == the oracle's textbook Montgomery
+    restatement, both forms, whole trace and an unaligned sub-range with a padded stride."""
+    import torch
+    import b2f
+
+    x = random_inputs(40, (0, 1, 4, 12), 24)
+    batch = b2f.DeviceBatch(x, device="cuda:0", total_rows=None)
+    batch.fill(engine)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    adv, _ = batch.host_trace()
+    for form in (b2f.FP_CANONICAL, b2f.FP_MONTGOMERY):
+        got = batch.export_fp(engine, form=form).cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, orc.export_fp(adv, form=form))
+    r0, nr = 1001, 12345
+    out = torch.full((10, nr + 7, 4), -1, dtype=torch.int64, device="cuda:0")
+    batch.export_fp(engine, row_begin=r0, nrows=nr, form=b2f.FP_MONTGOMERY, out=out)
+    got = out.cpu().numpy().view(np.uint64)
+    ref = orc.export_fp(adv, row_begin=r0, nrows=nr, form=orc.FP_MONTGOMERY)
+    assert np.array_equal(got[:, :nr], ref)
+    assert (got[:, nr:] == np.uint64(2**64 - 1)).all()  # stride padding untouched
+
+
+def test_fp_export_edge_values(engine, orc):
+    """Every cell value class: 0, 1, limb and spread extremes, all-ones."""
+    import torch
+    import b2f
+
+    rows = 4096
+    vals = np.array([0, 1, 2, 0xff, 0x100, 0x7fff, 0xffff, 0x55555555, 0xaaaaaaaa, 0xffffffff],
+                    dtype=np.uint32)
+    rng = np.random.default_rng(25)
+    adv = rng.integers(0, 2**32, (10, rows), dtype=np.uint64).astype(np.uint32)
+    adv[:, : len(vals)] = vals
+    batch = b2f.DeviceBatch(random_inputs(1, (0,), 1), device="cuda:0", total_rows=rows)
+    batch.advice.copy_(torch.from_numpy(adv.view(np.int32)))
+    got = batch.export_fp(engine, form=b2f.FP_MONTGOMERY).cpu().numpy().view(np.uint64)
+    assert np.array_equal(got, orc.export_fp(adv, form=orc.FP_MONTGOMERY))
+    with pytest.raises(b2f.B2FError):
+        batch.export_fp(engine, row_begin=rows - 4, nrows=8)
+    with pytest.raises(b2f.B2FError):
+        batch.export_fp(engine, form=7)

@@ -130,3 +130,40 @@ def test_bad_offsets_rejected(orc):
     off2[1] += 4
     with pytest.raises(ValueError):
         orc.evaluate(adv, fixed, off2)
+
+
+P_PALLAS = 0x40000000000000000000000000000000224698fc094cf91b992d30ed00000001  # pasta Fp modulus
+
+
+def _limbs_to_int(v):
+    return sum(int(v[i]) << (64 * i) for i in range(4))
+
+
+def test_fp_montgomery_vs_bigint(orc):
+    """Fp export restatement pinned to the definition
+    mont(x) = x * 2^256 mod p, with p the pallas base modulus."""
+    rng = np.random.default_rng(21)
+    xs = [0, 1, 2, 3, 255, 256, 0x7fff, 0xffff, 0x55555555, 0xaaaaaaaa, 0xfffffffe, 0xffffffff]
+    xs += [int(v) for v in rng.integers(0, 2**32, 2000, dtype=np.uint64)]
+    for x in xs:
+        assert _limbs_to_int(orc.fp_mont(x)) == (x << 256) % P_PALLAS, x
+    # mont(1) is pasta's R = 2^256 mod p
+    assert _limbs_to_int(orc.fp_mont(1)) == 0x3fffffffffffffffffffffffffffffff992c350be41914ad34786d38fffffffd
+
+
+def test_fp_export_layout(orc):
+    x = random_inputs(3, (1, 2), 22)
+    adv, fixed, h_out, off = orc.fill(_orc_inputs(x, orc))
+    order = [5, 3, 4, 6, 7, 8, 9, 0, 1, 2]  # halo2 column h -> a_i (table16.rs:281-294)
+    can = orc.export_fp(adv, form=orc.FP_CANONICAL)
+    for h, a in enumerate(order):
+        assert np.array_equal(can[h, :, 0], adv[a].astype(np.uint64))
+        assert not can[h, :, 1:].any()
+    r0, nr = 37, 501
+    mont = orc.export_fp(adv, row_begin=r0, nrows=nr, form=orc.FP_MONTGOMERY, out_rows=nr + 3)
+    assert not mont[:, nr:].any()
+    rng = np.random.default_rng(23)
+    for h, a in enumerate(order):
+        for r in rng.integers(0, nr, 40):
+            v = int(adv[a, r0 + r])
+            assert _limbs_to_int(mont[h, r]) == (v << 256) % P_PALLAS

@@ -76,6 +76,12 @@ class Engine:
         self._check(self.lib.b2f_eval_dev(self.ctx, _vp(d_adv), _vp(d_fixed), _vp(d_off), n,
                                           int(total_rows), _vp(d_report), _vp(stream)))
 
+    def export_fp_dev(self, d_adv, total_rows, row_begin, nrows, form, d_out, out_rows,
+                      stream=0):
+        self._check(self.lib.b2f_export_fp_dev(self.ctx, _vp(d_adv), int(total_rows),
+                                               int(row_begin), int(nrows), int(form),
+                                               _vp(d_out), int(out_rows), _vp(stream)))
+
     def sync(self, stream=0):
         self._check(self.lib.b2f_sync(self.ctx, _vp(stream)))
 
@@ -84,8 +90,9 @@ class Engine:
 
     def kernel_times(self):
         """{kernel: (total_ms, launches)} since set_timing(True) / the previous call."""
-        tot = (ctypes.c_double * 3)()
-        cnt = (ctypes.c_uint32 * 3)()
+        k = len(_lib.KERNEL_NAMES)
+        tot = (ctypes.c_double * k)()
+        cnt = (ctypes.c_uint32 * k)()
         self._check(self.lib.b2f_kernel_times(self.ctx, tot, cnt))
         return {name: (float(tot[i]), int(cnt[i])) for i, name in enumerate(_lib.KERNEL_NAMES)}
 
@@ -125,6 +132,24 @@ class DeviceBatch:
         s = stream if stream is not None else self.torch.cuda.current_stream().cuda_stream
         eng.eval_dev(self.advice.data_ptr(), self.fixed.data_ptr(), self.offsets.data_ptr(),
                      self.n, self.total_rows, self.report.data_ptr(), s)
+
+    def export_fp(self, eng, row_begin=0, nrows=None, form=_lib.FP_MONTGOMERY, out=None,
+                  stream=None):
+        """Advice rows [row_begin, row_begin + nrows) as pallas Fp elements: int64 tensor
+        [10 (halo2 column order), out_rows, 4] (u64 limb bit patterns). `out` may be a
+        preallocated tensor of that shape (out_rows >= nrows)."""
+        torch = self.torch
+        nrows = self.total_rows - row_begin if nrows is None else int(nrows)
+        if out is None:
+            out = torch.empty((_lib.NUM_ADVICE, nrows, 4), dtype=torch.int64,
+                              device=self.advice.device)
+        if out.dim() != 3 or out.shape[0] != _lib.NUM_ADVICE or out.shape[2] != 4 \
+                or out.dtype != torch.int64 or not out.is_contiguous():
+            raise _lib.B2FError(_lib.ERR_ARG, "export_fp: out must be contiguous int64 [10, rows, 4]")
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        eng.export_fp_dev(self.advice.data_ptr(), self.total_rows, row_begin, nrows, form,
+                          out.data_ptr(), out.shape[1], s)
+        return out
 
     def report_dict(self):
         raw = self.report.cpu().numpy().view(np.uint64)

@@ -1,0 +1,124 @@
+// b2f_export.hip -- Fp export of the trace: u32 advice cells ->
+// pallas::Base field elements as halo2's prover holds them, column by column in halo2's
+// advice-column order (table16.rs:281-294).
+//
+// Field: pasta_curves 0.5.1 Fp (Cargo.lock:1334-1337), p = 2^254 + d with
+//   d = 0x224698fc094cf91b992d30ed00000001 (126 bits).
+// In-memory form of Fp is Montgomery with R = 2^256: mont(x) = x * 2^256 mod p.
+// For a cell value x < 2^32 this needs no multiprecision reduction: 2^256 = 4 * 2^254 and
+// 2^254 = -d (mod p), so x * 2^256 = -4 x d (mod p), and since 4 x d < 2^160 < p,
+//   mont(x) = p - 4 x d = 2^254 - (4x - 1) d        (x != 0),   mont(0) = 0.
+// That is one 34 x 126-bit product and a 256-bit negation per cell (the oracle computes the
+// same values with a generic Montgomery multiply by R^2, oracle/b2f_oracle.c).
+// Canonical form (PrimeField::to_repr, 32-byte little endian) is simply (x, 0, 0, 0).
+//
+// HBM-bound: 4 B read, 32 B written per cell. A wave writes 64 x 16 B = 1 KiB contiguous per
+// store instruction (lane l stores 16-byte chunk l of a 1 KiB span, i.e. half l & 1 of cell
+// l >> 1 of the span's 32 cells), non-temporal.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/b2f.h"
+
+namespace b2f {
+
+hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
+                            uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
+                            int cu_count, hipStream_t s);
+
+namespace {
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+constexpr uint64_t kD0 = 0x992d30ed00000001ull;  // d, low limb
+constexpr uint64_t kD1 = 0x224698fc094cf91bull;  // d, high limb
+constexpr int EXPORT_BLOCK = 256;
+constexpr int CELLS_PER_ITER = EXPORT_BLOCK / 2;  // 128 cells = 4 KiB of output per WG pass
+
+// limbs (2*half, 2*half+1) of the field element for cell value x
+__device__ __forceinline__ u64x2 fp_half(uint32_t x, uint32_t half, uint32_t form) {
+  u64x2 r;
+  if (form == B2F_FP_CANONICAL) {
+    r.x = half ? 0 : x;
+    r.y = 0;
+    return r;
+  }
+  if (x == 0) {
+    r.x = 0;
+    r.y = 0;
+    return r;
+  }
+  // z = (4x - 1) * d  < 2^160: limbs z0, z1, z2
+  uint64_t y = 4ull * x - 1;
+  uint64_t z0 = y * kD0;
+  uint64_t h0 = __umul64hi(y, kD0);
+  uint64_t l1 = y * kD1;
+  uint64_t z2 = __umul64hi(y, kD1);
+  uint64_t z1 = h0 + l1;
+  z2 += (z1 < h0);
+  // v = 2^254 - z  (two's complement of z plus 2^254; z != 0 so the low borrow chain is
+  // that of a negation: v0 = -z0, then borrow 1 out of limb 0 iff z0 != 0)
+  uint64_t b0 = (z0 != 0);
+  uint64_t v0 = 0 - z0;
+  uint64_t v1 = 0 - z1 - b0;
+  uint64_t b1 = (z1 != 0) | b0;  // borrow out of limb 1
+  uint64_t v2 = 0 - z2 - b1;
+  uint64_t b2 = (z2 != 0) | b1;
+  uint64_t v3 = (1ull << 62) - b2;
+  r.x = half ? v2 : v0;
+  r.y = half ? v3 : v1;
+  return r;
+}
+
+// Persistent workgroups over XT-row tiles dealt round-robin (the fill kernel's pattern: the
+// whole chip writes one narrow band of each output column at a time). Per tile a workgroup
+// reads the ten 2 KiB column slices (all loads issued first) and writes the ten 16 KiB output
+// slices; every store instruction of a wave covers 1 KiB contiguous.
+constexpr int XT = 512;
+constexpr int XSUB = XT / CELLS_PER_ITER;  // 4 store passes per column per tile
+constexpr int kAofH[10] = {5, 3, 4, 6, 7, 8, 9, 0, 1, 2};
+
+__global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
+    const uint32_t* __restrict__ advice, uint64_t total_rows, uint64_t row_begin,
+    uint64_t nrows, uint32_t form, uint64_t* __restrict__ out, uint64_t out_rows) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t half = t & 1;
+  const uint64_t n_tiles = (nrows + XT - 1) / XT;
+  for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const uint64_t r0 = tile * XT;
+    uint32_t x[10][XSUB];
+#pragma unroll
+    for (int h = 0; h < 10; h++)
+#pragma unroll
+      for (int i = 0; i < XSUB; i++) {
+        uint64_t cell = r0 + i * CELLS_PER_ITER + (t >> 1);
+        x[h][i] = cell < nrows ? advice[(uint64_t)kAofH[h] * total_rows + row_begin + cell] : 0u;
+      }
+#pragma unroll
+    for (int h = 0; h < 10; h++) {
+      u64x2* dst = reinterpret_cast<u64x2*>(out + (uint64_t)h * out_rows * 4);
+#pragma unroll
+      for (int i = 0; i < XSUB; i++) {
+        uint64_t cell = r0 + i * CELLS_PER_ITER + (t >> 1);
+        if (cell < nrows) __builtin_nontemporal_store(fp_half(x[h][i], half, form), dst + 2 * cell + half);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
+                            uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
+                            int cu_count, hipStream_t s) {
+  // persistent grid: 4 workgroups per CU (halo2 column h -> a_i by kAofH)
+  uint64_t tiles = (nrows + XT - 1) / XT;
+  uint64_t want = (uint64_t)cu_count * 4;  // 122 VGPRs: 4 waves/SIMD
+  uint32_t gx = (uint32_t)(tiles < want ? tiles : want);
+  if (gx == 0) return hipSuccess;
+  hipLaunchKernelGGL(export_fp_kernel, dim3(gx), dim3(EXPORT_BLOCK), 0, s, d_advice,
+                     total_rows, row_begin, nrows, form, d_out, out_rows);
+  return hipGetLastError();
+}
+
+}  // namespace b2f

@@ -31,6 +31,12 @@
 
 using namespace b2f;
 
+namespace b2f {
+hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
+                            uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
+                            int cu_count, hipStream_t s);  // b2f_export.hip
+}
+
 namespace {
 
 __constant__ uint64_t c_iv[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL,
@@ -583,9 +589,31 @@ constexpr int L_CT = L_G + 5 * TSTRIDE;
 constexpr int L_SG = L_CT + 8 * G_QUADS * 12;
 constexpr int L_INFO = L_SG + 40;
 constexpr int L_IC = L_INFO + 24;
-constexpr int L_ACC = L_IC + 2 * INIT_ROWS;  // 16 gate + lookup + copy counters, first (u64)
+constexpr int L_XS = L_IC + 2 * INIT_ROWS;   // expected row-0 selector bits per G quad (16)
+constexpr int L_FLAG = L_XS + 16;            // per quad: 1 = canonical round quad (bytes)
+constexpr int L_A9 = L_FLAG + BLOCK / 4;     // per quad: a_9 of its first row
+constexpr int L_ACC = L_A9 + BLOCK;  // 16 gate + lookup + copy counters, first (u64)
 constexpr int LDS_WORDS = L_ACC + 20 + 2;
-static_assert(L_INFO % 4 == 0 && L_IC % 4 == 0 && L_G % 4 == 0, "16-byte aligned carve");
+static_assert(L_INFO % 4 == 0 && L_IC % 4 == 0 && L_G % 4 == 0 && L_CT % 4 == 0,
+              "16-byte aligned carve");
+static_assert(LDS_WORDS * 4 * 3 <= 160 * 1024, "three eval workgroups per CU");
+
+// Row-0 selector bits of each quad of a G when the fixed column is canonical (LAYOUT.md §5:
+// a1 | d1 d1 | c1 | b1 b1 b1 | a2 | d2 d2 | c2 | b2 b2, blocks start on a quad, rows 1-3 of
+// every round quad carry no selector).
+constexpr uint32_t expected_sel(uint32_t p) {
+  return p == 0 ? 1u << S_A1 : p == 1 ? 1u << S_D1 : p == 3 ? 1u << S_C1
+       : p == 4 ? (1u << S_B1) | (1u << S_EFGH) : p == 7 ? 1u << S_A2 : p == 8 ? 1u << S_D2
+       : p == 10 ? 1u << S_C2 : p == 11 ? (1u << S_B2) | (1u << S_IJKL) : 0u;
+}
+constexpr bool expected_sel_matches_fill() {
+  RowTable R = make_rows();
+  for (uint32_t p = 0; p < G_QUADS; p++)
+    for (uint32_t j = 0; j < 4; j++)
+      if ((R.r[p][j] >> 16) != (j == 0 ? expected_sel(p) : 0u)) return false;
+  return true;
+}
+static_assert(expected_sel_matches_fill(), "eval's canonical selectors = the fill's");
 
 // Extra (non-own-quad) loads of a tile: 2 slots per thread.
 constexpr int X_HIST = 4 * (HIST / 4);          // 384: 96 quads x 4 canonical columns
@@ -970,28 +998,79 @@ __device__ __noinline__ uint32_t gates_generic(const Tile& T, uint32_t sel, uint
   return failed;
 }
 
-// Failing selector bits of selector row r (tile-local).
+// Failing selector bits of selector row r (tile-local), for rows the per-G pass does not take:
+// the init and final blocks (XOR, XOR3 + digest inline; the rest out of line) and any
+// non-canonical selector row of a corrupted fixed column.
 __device__ __forceinline__ uint32_t row_gates(const Tile& T, uint32_t sel, uint32_t r, uint32_t a9,
                                               uint32_t k0) {
   switch (sel) {
-    case 1u << S_D1:
-    case 1u << S_D2:
     case 1u << S_XOR:
       return g_xor(T, r, false) ? 0u : sel;
-    case 1u << S_A1:
-    case 1u << S_A2:
-      return g_add(T, r, a9, true) ? 0u : sel;
-    case 1u << S_C1:
-    case 1u << S_C2:
-      return g_add(T, r, a9, false) ? 0u : sel;
-    case (1u << S_B1) | (1u << S_EFGH):
-      return g_xor24(T, r, sel);
-    case (1u << S_B2) | (1u << S_IJKL):
-      return g_xor63(T, r, sel);
     case (1u << S_XOR3) | (1u << S_DIGEST):
       return (g_xor(T, r, true) ? 0u : 1u << S_XOR3) | (g_digest(T, r) ? 0u : 1u << S_DIGEST);
     default:
       return gates_generic(T, sel, r, a9, k0);
+  }
+}
+
+// Gates of the canonical round blocks of a tile, one lane per (G, half): half 0 checks a1 (ADD3
+// +0), d1 (XOR +4), c1 (ADD2 +12), b1 (XOR24 +16); half 1 checks a2 (+28), d2 (+32), c2 (+40),
+// b2 (XOR63 +44). A tile holds at most 21 G starts in [tile0 - 44, tile0 + 1023], so one wave
+// covers them and every lane runs the same four evaluators (the per-quad assignment would make
+// each wave run all five block kinds, mostly masked). A block is checked here only if the quad
+// holding its selector row lies in this tile and is canonical (flag set by that quad's lane);
+// every other selector row is evaluated by its own quad's lane (row_gates).
+__device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const uint32_t* L,
+                                             uint64_t tile0, uint32_t n, uint32_t lane) {
+  const uint32_t first = L[L_INFO];
+  const uint64_t* Off = reinterpret_cast<const uint64_t*>(L + L_INFO + 2);
+  const int64_t lo = (int64_t)tile0 - 44, hi = (int64_t)tile0 + TILE_ROWS - 1;
+  uint32_t base = 0, h = 0;
+  int64_t gs = -1;
+  for (int i = 0; i + 1 < NOFF; i++) {
+    if (first + (uint32_t)i >= n) break;
+    const uint64_t o = Off[i], o1 = Off[i + 1];
+    if ((int64_t)o > hi) break;
+    const uint64_t R = o1 - o;
+    if (o1 <= o || R < FIXED_ROWS || (R - FIXED_ROWS) % ROUND_ROWS) continue;  // quads irregular
+    const uint64_t n_g = 8 * ((R - FIXED_ROWS) / ROUND_ROWS);
+    const int64_t g0 = (int64_t)o + INIT_ROWS;
+    const int64_t b = hi - g0;
+    if (n_g == 0 || b < 0) continue;
+    const int64_t a = lo - g0;
+    const uint64_t m_lo = a <= 0 ? 0 : ((uint64_t)a + G_ROWS - 1) / G_ROWS;
+    uint64_t m_hi = (uint64_t)b / G_ROWS;
+    if (m_hi >= n_g) m_hi = n_g - 1;
+    if (m_lo > m_hi) continue;
+    const uint32_t items = 2 * (uint32_t)(m_hi - m_lo + 1);
+    if (gs < 0 && lane >= base && lane < base + items) {
+      gs = g0 + (int64_t)G_ROWS * (int64_t)(m_lo + (lane - base) / 2);
+      h = (lane - base) & 1u;
+    }
+    base += items;
+  }
+  if (gs < 0) return;
+  const int sl = (int)(gs - (int64_t)tile0) + 28 * (int)h;  // tile-local row of the half's a-block
+  const uint8_t* F = reinterpret_cast<const uint8_t*>(L + L_FLAG);
+  auto mine = [&](int r) { return r >= 0 && r < TILE_ROWS && F[r >> 2]; };
+  uint32_t r;
+  if (mine(sl)) {  // a1 / a2
+    r = (uint32_t)sl;
+    if (!g_add(T, r, L[L_A9 + (r >> 2)], true)) A.fail_gates(tile0 + r, 1u << (h ? S_A2 : S_A1));
+  }
+  if (mine(sl + 4)) {  // d1 / d2
+    r = (uint32_t)(sl + 4);
+    if (!g_xor(T, r, false)) A.fail_gates(tile0 + r, 1u << (h ? S_D2 : S_D1));
+  }
+  if (mine(sl + 12)) {  // c1 / c2
+    r = (uint32_t)(sl + 12);
+    if (!g_add(T, r, L[L_A9 + (r >> 2)], false)) A.fail_gates(tile0 + r, 1u << (h ? S_C2 : S_C1));
+  }
+  if (mine(sl + 16)) {  // b1 (XOR24) / b2 (XOR63)
+    r = (uint32_t)(sl + 16);
+    uint32_t f = h ? g_xor63(T, r, (1u << S_B2) | (1u << S_IJKL))
+                   : g_xor24(T, r, (1u << S_B1) | (1u << S_EFGH));
+    if (f) A.fail_gates(tile0 + r, f);
   }
 }
 
@@ -1156,6 +1235,7 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
   for (int i = tid; i < COPY_WORDS; i += BLOCK)
     L[L_CT + i] = reinterpret_cast<const uint32_t*>(&c_copy)[i];
   if (tid < 40) L[L_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
+  if (tid < 16) L[L_XS + tid] = expected_sel((uint32_t)tid);
   const Tile T{L};
   const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + L_SG);  // [10][16]
 
@@ -1168,12 +1248,12 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
   const bool layout_ok = used_rows <= total_rows && off[0] == 0;  // never read past the trace
   if (!layout_ok && blockIdx.x == 0 && tid == 0) atomicOr(status, 1 << B2F_ERR_LAYOUT);
   const uint64_t G = gridDim.x;
-  const bool init_role = tid + BLOCK >= X_HALO && tid + BLOCK < X_INIT;  // slot tid+256
 
   uint64_t t = blockIdx.x;
+  // fo / fo_next (first instance and its offset, per tile) are workgroup-uniform: SGPRs
+  uint4 q[NCOL_T], x0 = make_uint4(0, 0, 0, 0), x1 = x0, fo = x0, fo_next = x0;
   const Extra e0 = make_extra(tid, adv, total_rows, tinfo);
   const Extra e1 = make_extra(tid + BLOCK, adv, total_rows, tinfo);
-  uint4 q[NCOL_T], x0 = make_uint4(0, 0, 0, 0), x1 = x0, fo = x0, fo_next = x0;
   auto load_tile = [&](uint64_t tt, const uint4& f) {
     const uint64_t gq = tt * BLOCK + tid;
 #pragma unroll
@@ -1185,9 +1265,9 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
     x1 = extra_load(e1, tt, f, n, total_rows, total_quads);
   };
   if (layout_ok && t < n_tiles) {
-    if (init_role) fo = *reinterpret_cast<const uint4*>(tinfo + t);
+    fo = *reinterpret_cast<const uint4*>(tinfo + t);
     load_tile(t, fo);
-    if (init_role && t + G < n_tiles) fo_next = *reinterpret_cast<const uint4*>(tinfo + t + G);
+    if (t + G < n_tiles) fo_next = *reinterpret_cast<const uint4*>(tinfo + t + G);
   }
   for (; layout_ok && t < n_tiles; t += G) {
     // ---- stage tile t: registers -> LDS
@@ -1199,15 +1279,10 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
     __syncthreads();
     // ---- prefetch tile t + G into registers while tile t is checked
     const uint64_t tn = t + G;
-    auto prefetch = [&]() {
-      if (tn < n_tiles) {
-        load_tile(tn, fo_next);
-        if (init_role && tn + G < n_tiles) fo_next = *reinterpret_cast<const uint4*>(tinfo + tn + G);
-      }
-    };
-#ifndef B2F_PREFETCH_LATE
-    prefetch();
-#endif
+    if (tn < n_tiles) {
+      load_tile(tn, fo_next);
+      if (tn + G < n_tiles) fo_next = *reinterpret_cast<const uint4*>(tinfo + tn + G);
+    }
     const uint64_t tile0 = t * TILE_ROWS;
     const uint64_t gq = t * BLOCK + tid;
     if ((MODE & EVAL_TOUCH) && gq < total_quads) {  // diagnostics: keep the staged words alive
@@ -1216,10 +1291,11 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
                    L[L_INFO + (tid & 15)] ^ T.at(A3, 4 * tid + 13);
       if (x == 0x12345678u) A.fail(0, B2F_CODE_LOOKUP);
     }
+    uint32_t regular = 0;
     if (gq < total_quads) {
       const uint64_t row0 = 4 * gq;
       const uint32_t lr0 = 4 * tid;
-      // ---- lookups and gates on the 4 rows
+      // ---- lookups on the 4 rows
       if (MODE & EVAL_LOOKUP) {
         const uint4 q0 = T.quad(A0, lr0), q1 = T.quad(A1, lr0), q2 = T.quad(A2, lr0);
 #pragma unroll
@@ -1229,93 +1305,135 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
           if (!ok) A.fail(row0 + j, B2F_CODE_LOOKUP);
         }
       }
-      if (MODE & EVAL_GATES) {
-        // rows of this quad that carry a selector (a block starts at j = 0; CONST has one
-        // on every row)
-        uint32_t rowmask = ((curfx.x & 0xffffu) ? 1u : 0u) | ((curfx.y & 0xffffu) ? 2u : 0u) |
-                           ((curfx.z & 0xffffu) ? 4u : 0u) | ((curfx.w & 0xffffu) ? 8u : 0u);
-        while (rowmask) {
-          int j = __builtin_ctz(rowmask);
-          rowmask &= rowmask - 1;
-          uint32_t k0 = comp(curfx, j);
-          uint32_t failed;
-          if ((k0 & 0xffffu) == (1u << S_CONST)) failed = T.at(A1, lr0 + j) == (k0 >> 16) ? 0u : 1u << S_CONST;
-          else failed = row_gates(T, k0 & 0xffffu, lr0 + j, comp(cur9, j), k0);
-          if (failed) A.fail_gates(row0 + j, failed);
-        }
-      }
-#ifdef B2F_PREFETCH_LATE
-    }
-    prefetch();  // after the gates: their registers are free again
-    if (gq < total_quads) {
-      const uint64_t row0 = 4 * gq;
-      const uint32_t lr0 = 4 * tid;
-#endif
-      // ---- copy constraints whose operand cell lies in this quad
+      // ---- the quad's instance: scan the tile's offsets in LDS (global beyond NOFF - 1)
       const uint32_t first = L[L_INFO];
       const uint64_t* Off = reinterpret_cast<const uint64_t*>(L + L_INFO + 2);
-      if ((MODE & EVAL_COPIES) && row0 < used_rows) {
-        // instance of this quad: scan the tile's offsets in LDS (global beyond 8 instances)
+      bool valid = false, cached = false, is_round = false;
+      uint64_t o = 0;
+      uint32_t rounds = 0, lq = 0, r = 0, g = 0, p = 0;
+      if (row0 < used_rows) {
         uint32_t inst = first, i = 0;
         while (i + 2 < NOFF && Off[i + 1] <= row0) i++;
         inst += i;
-        uint64_t o = Off[i], o1 = Off[i + 1];
-        if (o1 <= row0) {  // more than NOFF - 1 instances start in this tile (tiny rounds)
+        o = Off[i];
+        uint64_t o1 = Off[i + 1];
+        cached = o1 > row0;
+        if (!cached) {  // more than NOFF - 1 instances start in this tile (tiny rounds)
           do { inst++; o = o1; o1 = off[inst + 1]; } while (o1 <= row0);
         }
-        uint64_t R = o1 - o;
-        const Src src{L + L_W, L + L_IC, adv, total_rows, tile0 - HIST, first < n ? Off[0] : ~0ull};
-
-        if (o1 > o && o1 <= total_rows && R >= FIXED_ROWS && (R - FIXED_ROWS) % ROUND_ROWS == 0 &&
-            (R - FIXED_ROWS) / ROUND_ROWS <= B2F_MAX_ROUNDS) {
-          uint32_t rounds = (uint32_t)((R - FIXED_ROWS) / ROUND_ROWS);
-          uint32_t lq = (uint32_t)((row0 - o) >> 2);
-          uint32_t rq = lq - INIT_QUADS;
-          if (lq >= INIT_QUADS && rq < ROUND_QUADS * rounds) {
-            uint32_t r = rq / ROUND_QUADS, w = rq - r * ROUND_QUADS;
-            uint32_t g = w / G_QUADS, p = w - g * G_QUADS;
-            uint64_t gbase = o + INIT_ROWS + (uint64_t)ROUND_ROWS * r + G_ROWS * g;
-            const bool hr0 = (r == 0) && (g < 4);
-            const uint32_t* ct = L + L_CT + (g * G_QUADS + p) * 12;
-            const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
-            const uint64_t wlo = tile0 - HIST, ofirst = src.ofirst;
-            uint32_t bad = 0;  // failing operand cells, bit 3*j + c
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-#pragma unroll
-              for (int c = 0; c < 3; c++) {
-                uint32_t e = ct[j * 3 + c];
-                uint32_t kind = e & 3u;
-                uint32_t k = (e >> 4) & 3u;
-                // rows relative to the instance (init region) or to the G's first row
-                uint32_t init_row = kind == 3 ? 32 + 4 * (uint32_t)sg[(e >> 6) & 1u] + k
-                                              : (e >> 17) & 255u;
-                bool from_init = kind == 3 || (kind == 2 && hr0);
-                uint64_t gs = from_init ? o + init_row
-                                        : gbase + (uint64_t)(int64_t)((int)((e >> 7) & 1023u) - 512);
-                uint32_t wc = (kind == 2 && hr0) ? (e >> 25) & 3u : (e >> 2) & 3u;
-                // the source is in the LDS window or the init cache for every valid layout
-                uint64_t dw = gs - wlo, di = gs - ofirst;
-                bool in_w = dw < (uint64_t)WSTRIDE, in_i = di < (uint64_t)INIT_ROWS && wc < 2;
-                uint32_t idx = in_w ? L_W + wc * WSTRIDE + (uint32_t)dw
-                                    : L_IC + (wc & 1u) * INIT_ROWS + (in_i ? (uint32_t)di : 0u);
-                uint32_t sv = L[idx];
-                if (kind && !in_w && !in_i) sv = src.at(gs, wc);  // corrupted layout only
-                bad |= (kind && T.at(A3 + c, lr0 + j) != sv) ? 1u << (3 * j + c) : 0u;
-              }
-            while (bad) {
-              int b = __builtin_ctz(bad);
-              bad &= bad - 1;
-              A.fail(row0 + b / 3, B2F_CODE_COPY);
-            }
-          } else {
-            const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
-            copies_edge(A, dq, src, o, rounds, lq);
+        const uint64_t R = o1 - o;
+        valid = o1 > o && o1 <= total_rows && R >= FIXED_ROWS && (R - FIXED_ROWS) % ROUND_ROWS == 0 &&
+                (R - FIXED_ROWS) / ROUND_ROWS <= B2F_MAX_ROUNDS;
+        if (valid) {
+          rounds = (uint32_t)((R - FIXED_ROWS) / ROUND_ROWS);
+          lq = (uint32_t)((row0 - o) >> 2);
+          const uint32_t rq = lq - INIT_QUADS;
+          is_round = lq >= INIT_QUADS && rq < ROUND_QUADS * rounds;
+          if (is_round) {
+            r = rq / ROUND_QUADS;
+            const uint32_t w = rq - r * ROUND_QUADS;
+            g = w / G_QUADS;
+            p = w - g * G_QUADS;
           }
-        } else {
+        } else if (MODE & EVAL_COPIES) {
           atomicOr(status, 1 << B2F_ERR_LAYOUT);
         }
       }
+      // ---- gates: canonical round quads go to the per-G pass below; every other selector row
+      // (init / final blocks, a corrupted fixed column) is evaluated here, row by row
+      if (MODE & EVAL_GATES) {
+        const uint32_t rest = (curfx.y | curfx.z | curfx.w) & 0xffffu;
+        regular = (is_round && cached && rest == 0 && (curfx.x & 0xffffu) == L[L_XS + p]) ? 1u : 0u;
+        if (!regular) {
+          uint32_t rowmask = ((curfx.x & 0xffffu) ? 1u : 0u) | ((curfx.y & 0xffffu) ? 2u : 0u) |
+                             ((curfx.z & 0xffffu) ? 4u : 0u) | ((curfx.w & 0xffffu) ? 8u : 0u);
+          while (rowmask) {
+            int j = __builtin_ctz(rowmask);
+            rowmask &= rowmask - 1;
+            uint32_t k0 = comp(curfx, j);
+            uint32_t failed;
+            if ((k0 & 0xffffu) == (1u << S_CONST)) failed = T.at(A1, lr0 + j) == (k0 >> 16) ? 0u : 1u << S_CONST;
+            else failed = row_gates(T, k0 & 0xffffu, lr0 + j, comp(cur9, j), k0);
+            if (failed) A.fail_gates(row0 + j, failed);
+          }
+        }
+      }
+      // ---- copy constraints whose operand cell lies in this quad
+      if ((MODE & EVAL_COPIES) && valid) {
+        const uint64_t ofirst = L[L_INFO] < n ? *reinterpret_cast<const uint64_t*>(L + L_INFO + 2) : ~0ull;
+        if (is_round) {
+          // every source of a valid layout is in the window W (rows [tile0 - HIST, tile0 +
+          // TILE_ROWS + HALO)) or, for init-region words of the tile's first instance, in the
+          // init cache; offsets are 32-bit from here on
+          const int64_t wlo = (int64_t)tile0 - HIST;
+          const uint64_t gbase = o + INIT_ROWS + (uint64_t)ROUND_ROWS * r + G_ROWS * g;
+          const int gbw = (int)((int64_t)gbase - wlo);
+          const int64_t ib = (int64_t)o - wlo;
+          const int ibw = ib < -(1 << 30) ? -(1 << 30) : (int)ib;
+          const bool ofst = o == ofirst;
+          const bool hr0 = (r == 0) && (g < 4);
+          const uint4* ctq = reinterpret_cast<const uint4*>(L + L_CT + (g * G_QUADS + p) * 12);
+          const uint4 ce[3] = {ctq[0], ctq[1], ctq[2]};
+          const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
+          const uint32_t sgx = sg[0], sgy = sg[1];
+          const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
+          uint32_t bad = 0, needg = 0;  // bit 3*j + c
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+              const int sl = 3 * j + c;
+              const uint32_t e = comp(ce[sl >> 2], sl & 3);
+              const uint32_t kind = e & 3u;
+              const bool msg = kind == 3, st0 = kind == 2 && hr0, from_init = msg || st0;
+              const uint32_t init_row = msg ? 32 + 4 * (((e >> 6) & 1u) ? sgy : sgx) + ((e >> 4) & 3u)
+                                            : (e >> 17) & 255u;
+              const int d = from_init ? ibw + (int)init_row : gbw + (int)((e >> 7) & 1023u) - 512;
+              const uint32_t wc = st0 ? (e >> 25) & 3u : (e >> 2) & 3u;
+              const bool in_w = (uint32_t)d < (uint32_t)WSTRIDE;
+              const uint32_t idx = in_w ? L_W + wc * WSTRIDE + (uint32_t)d
+                                        : L_IC + (wc & 1u) * INIT_ROWS + init_row;
+              const uint32_t sv = L[idx];
+              const bool cache_ok = from_init && ofst && wc < 2;
+              needg |= (kind && !in_w && !cache_ok) ? 1u << sl : 0u;
+              bad |= (kind && comp(dq[c], j) != sv) ? 1u << sl : 0u;
+            }
+          if (needg) {  // a source outside W and the cache: only a corrupted layout gets here
+            const Src src{L + L_W, L + L_IC, adv, total_rows, tile0 - HIST, ofirst};
+            bad &= ~needg;
+            while (needg) {
+              const int sl = __builtin_ctz(needg);
+              needg &= needg - 1;
+              const uint32_t e = L[L_CT + (g * G_QUADS + p) * 12 + sl];
+              const uint32_t kind = e & 3u;
+              const bool msg = kind == 3, st0 = kind == 2 && hr0;
+              const uint32_t init_row = msg ? 32 + 4 * (((e >> 6) & 1u) ? sgy : sgx) + ((e >> 4) & 3u)
+                                            : (e >> 17) & 255u;
+              const uint64_t gs = (msg || st0) ? o + init_row
+                                               : gbase + (uint64_t)(int64_t)((int)((e >> 7) & 1023u) - 512);
+              const uint32_t wc = st0 ? (e >> 25) & 3u : (e >> 2) & 3u;
+              const uint32_t dv = T.at(A3 + sl % 3, lr0 + sl / 3);
+              if (dv != src.at(gs, wc)) bad |= 1u << sl;
+            }
+          }
+          while (bad) {
+            int b = __builtin_ctz(bad);
+            bad &= bad - 1;
+            A.fail(row0 + b / 3, B2F_CODE_COPY);
+          }
+        } else {
+          const Src src{L + L_W, L + L_IC, adv, total_rows, tile0 - HIST, ofirst};
+          const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
+          copies_edge(A, dq, src, o, rounds, lq);
+        }
+      }
+    }
+    if (MODE & EVAL_GATES) {
+      // ---- canonical round blocks: one lane per (G, half) in the first wave
+      reinterpret_cast<uint8_t*>(L + L_FLAG)[tid] = (uint8_t)regular;
+      L[L_A9 + tid] = cur9.x;
+      __syncthreads();
+      if (tid < 64) half_g_gates(T, A, L, tile0, n, (uint32_t)tid);
     }
     __syncthreads();
   }
@@ -1607,10 +1725,34 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
                        d_offsets, (uint32_t)n, total_rows, ctx->d_tiles, nt, d_report,          \
                        ctx->d_status + 1);                                                      \
     break;
-    B2F_EVAL(1) B2F_EVAL(2) B2F_EVAL(4) B2F_EVAL(8) default: B2F_EVAL(7)
+    B2F_EVAL(1) B2F_EVAL(2) B2F_EVAL(3) B2F_EVAL(4) B2F_EVAL(5) B2F_EVAL(6) B2F_EVAL(8)
+    default: B2F_EVAL(7)
 #undef B2F_EVAL
   }
   HIPCHK(ctx, hipGetLastError());
+  timed_end(ctx, tk, s);
+  return B2F_OK;
+}
+
+B2F_API int b2f_export_fp_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t total_rows,
+                              uint64_t row_begin, uint64_t nrows, uint32_t form,
+                              uint64_t* d_out, uint64_t out_rows, void* stream) {
+  if (!ctx) return B2F_ERR_ARG;
+  if (!d_advice || !d_out) return set_err(ctx, B2F_ERR_ARG, "export: null buffer");
+  if (form != B2F_FP_CANONICAL && form != B2F_FP_MONTGOMERY)
+    return set_err(ctx, B2F_ERR_ARG, "export: unknown form %u", form);
+  if ((uintptr_t)d_out & 15) return set_err(ctx, B2F_ERR_ARG, "export: d_out must be 16-byte aligned");
+  if (row_begin > total_rows || nrows > total_rows - row_begin)
+    return set_err(ctx, B2F_ERR_ROWS, "export: rows [%llu, +%llu) exceed total_rows %llu",
+                   (unsigned long long)row_begin, (unsigned long long)nrows,
+                   (unsigned long long)total_rows);
+  if (out_rows < nrows) return set_err(ctx, B2F_ERR_ROWS, "export: out_rows < nrows");
+  if (nrows == 0) return B2F_OK;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  int tk = timed_begin(ctx, B2F_KERNEL_EXPORT, s);
+  HIPCHK(ctx, launch_export_fp(d_advice, total_rows, row_begin, nrows, form, d_out, out_rows,
+                               ctx->cu_count, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
