@@ -379,6 +379,8 @@ __device__ __forceinline__ void quad_cells(Quad& Q, const b2f_input* __restrict_
   }
 }
 
+constexpr uint64_t MAX_INSTANCE_ROWS = FIXED_ROWS + (uint64_t)ROUND_ROWS * B2F_MAX_ROUNDS;
+static_assert(MAX_INSTANCE_ROWS < (1ull << 31), "instance-relative rows fit in int32");
 constexpr int HIST = 384;                // >= 361 + quad alignment
 constexpr int WSTRIDE = HIST + TSTRIDE;  // 1424
 constexpr int NOFF = 9;                  // offsets of the first 8 instances of a tile (+1)
@@ -1031,18 +1033,20 @@ __device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const ui
     if (first + (uint32_t)i >= n) break;
     const uint64_t o = Off[i], o1 = Off[i + 1];
     if ((int64_t)o > hi) break;
-    const uint64_t R = o1 - o;
-    if (o1 <= o || R < FIXED_ROWS || (R - FIXED_ROWS) % ROUND_ROWS) continue;  // quads irregular
-    const uint64_t n_g = 8 * ((R - FIXED_ROWS) / ROUND_ROWS);
+    if (o1 <= o || o1 - o > MAX_INSTANCE_ROWS) continue;  // its quads are irregular
+    const uint32_t R = (uint32_t)(o1 - o);
+    if (R < FIXED_ROWS || (R - FIXED_ROWS) % ROUND_ROWS) continue;
+    const uint32_t n_g = 8 * ((R - FIXED_ROWS) / ROUND_ROWS);
+    // G m starts at g0 + 52 m; o > tile0 - MAX_INSTANCE_ROWS, so these fit in 32 bits
     const int64_t g0 = (int64_t)o + INIT_ROWS;
-    const int64_t b = hi - g0;
+    const int b = (int)(hi - g0);
     if (n_g == 0 || b < 0) continue;
-    const int64_t a = lo - g0;
-    const uint64_t m_lo = a <= 0 ? 0 : ((uint64_t)a + G_ROWS - 1) / G_ROWS;
-    uint64_t m_hi = (uint64_t)b / G_ROWS;
+    const int a = (int)(lo - g0);
+    const uint32_t m_lo = a <= 0 ? 0u : ((uint32_t)a + G_ROWS - 1) / G_ROWS;
+    uint32_t m_hi = (uint32_t)b / G_ROWS;
     if (m_hi >= n_g) m_hi = n_g - 1;
     if (m_lo > m_hi) continue;
-    const uint32_t items = 2 * (uint32_t)(m_hi - m_lo + 1);
+    const uint32_t items = 2 * (m_hi - m_lo + 1);
     if (gs < 0 && lane >= base && lane < base + items) {
       gs = g0 + (int64_t)G_ROWS * (int64_t)(m_lo + (lane - base) / 2);
       h = (lane - base) & 1u;
@@ -1249,7 +1253,11 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
   if (!layout_ok && blockIdx.x == 0 && tid == 0) atomicOr(status, 1 << B2F_ERR_LAYOUT);
   const uint64_t G = gridDim.x;
 
-  uint64_t t = blockIdx.x;
+  // XCD-aware deal: workgroups are dispatched to the 8 XCDs round-robin (b % 8), so give each
+  // XCD a contiguous run of G / 8 tiles per band. A tile's history window and halo are then the
+  // rows its same-XCD neighbours just loaded, served from that XCD's L2 rather than refetched
+  // (placement is only a speed hint; any placement gives the same result).
+  uint64_t t = (G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
   // fo / fo_next (first instance and its offset, per tile) are workgroup-uniform: SGPRs
   uint4 q[NCOL_T], x0 = make_uint4(0, 0, 0, 0), x1 = x0, fo = x0, fo_next = x0;
   const Extra e0 = make_extra(tid, adv, total_rows, tinfo);
@@ -1321,11 +1329,11 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
         if (!cached) {  // more than NOFF - 1 instances start in this tile (tiny rounds)
           do { inst++; o = o1; o1 = off[inst + 1]; } while (o1 <= row0);
         }
-        const uint64_t R = o1 - o;
-        valid = o1 > o && o1 <= total_rows && R >= FIXED_ROWS && (R - FIXED_ROWS) % ROUND_ROWS == 0 &&
-                (R - FIXED_ROWS) / ROUND_ROWS <= B2F_MAX_ROUNDS;
+        const uint32_t R = (uint32_t)(o1 - o);
+        valid = o1 > o && o1 <= total_rows && o1 - o <= MAX_INSTANCE_ROWS && R >= FIXED_ROWS &&
+                (R - FIXED_ROWS) % ROUND_ROWS == 0;
         if (valid) {
-          rounds = (uint32_t)((R - FIXED_ROWS) / ROUND_ROWS);
+          rounds = (R - FIXED_ROWS) / ROUND_ROWS;
           lq = (uint32_t)((row0 - o) >> 2);
           const uint32_t rq = lq - INIT_QUADS;
           is_round = lq >= INIT_QUADS && rq < ROUND_QUADS * rounds;
