@@ -592,8 +592,9 @@ constexpr int L_SG = L_CT + 8 * G_QUADS * 12;
 constexpr int L_INFO = L_SG + 40;
 constexpr int L_IC = L_INFO + 24;
 constexpr int L_XS = L_IC + 2 * INIT_ROWS;   // expected row-0 selector bits per G quad (16)
-constexpr int L_FLAG = L_XS + 16;            // per quad: 1 = canonical round quad (bytes)
-constexpr int L_A9 = L_FLAG + BLOCK / 4;     // per quad: a_9 of its first row
+constexpr int L_QSEL = L_XS + 16;            // per quad: row-0 selector bits | 1 << 16 if rows
+                                             // 1-3 carry any selector
+constexpr int L_A9 = L_QSEL + BLOCK;         // per quad: a_9 of its first row
 constexpr int L_ACC = L_A9 + BLOCK;  // 16 gate + lookup + copy counters, first (u64)
 constexpr int LDS_WORDS = L_ACC + 20 + 2;
 static_assert(L_INFO % 4 == 0 && L_IC % 4 == 0 && L_G % 4 == 0 && L_CT % 4 == 0,
@@ -1015,15 +1016,18 @@ __device__ __forceinline__ uint32_t row_gates(const Tile& T, uint32_t sel, uint3
   }
 }
 
-// Gates of the canonical round blocks of a tile, one lane per (G, half): half 0 checks a1 (ADD3
-// +0), d1 (XOR +4), c1 (ADD2 +12), b1 (XOR24 +16); half 1 checks a2 (+28), d2 (+32), c2 (+40),
-// b2 (XOR63 +44). A tile holds at most 21 G starts in [tile0 - 44, tile0 + 1023], so one wave
-// covers them and every lane runs the same four evaluators (the per-quad assignment would make
-// each wave run all five block kinds, mostly masked). A block is checked here only if the quad
-// holding its selector row lies in this tile and is canonical (flag set by that quad's lane);
-// every other selector row is evaluated by its own quad's lane (row_gates).
+// Gates of the canonical round blocks of a tile. A tile holds at most 21 G starts in
+// [tile0 - 44, tile0 + 1023]; lane l of every wave takes item l = (G, half), and wave w checks
+// block kind w of it: 0 a1/a2 (ADD3, +0/+28), 1 d1/d2 (XOR, +4/+32), 2 c1/c2 (ADD2, +12/+40),
+// 3 b1 (XOR24, +16) / b2 (XOR63, +44). Each wave thus runs one evaluator (the b wave two)
+// instead of every wave running all five block kinds mostly masked, as a quad-per-lane
+// assignment would. A block is checked here only if the quad holding its selector row lies in
+// this tile and is canonical: row-0 selector bits exactly the block's and none on rows 1-3
+// (L_QSEL, written at staging). Every other selector row is evaluated by its own quad's lane
+// (row_gates), so each selector row is evaluated exactly once.
 __device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const uint32_t* L,
-                                             uint64_t tile0, uint32_t n, uint32_t lane) {
+                                             uint64_t tile0, uint32_t n, uint64_t total_rows,
+                                             uint32_t lane, uint32_t kind) {
   const uint32_t first = L[L_INFO];
   const uint64_t* Off = reinterpret_cast<const uint64_t*>(L + L_INFO + 2);
   const int64_t lo = (int64_t)tile0 - 44, hi = (int64_t)tile0 + TILE_ROWS - 1;
@@ -1033,7 +1037,7 @@ __device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const ui
     if (first + (uint32_t)i >= n) break;
     const uint64_t o = Off[i], o1 = Off[i + 1];
     if ((int64_t)o > hi) break;
-    if (o1 <= o || o1 - o > MAX_INSTANCE_ROWS) continue;  // its quads are irregular
+    if (o1 <= o || o1 > total_rows || o1 - o > MAX_INSTANCE_ROWS) continue;  // quads irregular
     const uint32_t R = (uint32_t)(o1 - o);
     if (R < FIXED_ROWS || (R - FIXED_ROWS) % ROUND_ROWS) continue;
     const uint32_t n_g = 8 * ((R - FIXED_ROWS) / ROUND_ROWS);
@@ -1054,28 +1058,23 @@ __device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const ui
     base += items;
   }
   if (gs < 0) return;
-  const int sl = (int)(gs - (int64_t)tile0) + 28 * (int)h;  // tile-local row of the half's a-block
-  const uint8_t* F = reinterpret_cast<const uint8_t*>(L + L_FLAG);
-  auto mine = [&](int r) { return r >= 0 && r < TILE_ROWS && F[r >> 2]; };
-  uint32_t r;
-  if (mine(sl)) {  // a1 / a2
-    r = (uint32_t)sl;
-    if (!g_add(T, r, L[L_A9 + (r >> 2)], true)) A.fail_gates(tile0 + r, 1u << (h ? S_A2 : S_A1));
+  const int off = (int)kind == 0 ? 0 : kind == 1 ? 4 : kind == 2 ? 12 : 16;
+  const int rl = (int)(gs - (int64_t)tile0) + 28 * (int)h + off;  // tile-local selector row
+  const uint32_t want = kind == 0 ? 1u << (h ? S_A2 : S_A1)
+                      : kind == 1 ? 1u << (h ? S_D2 : S_D1)
+                      : kind == 2 ? 1u << (h ? S_C2 : S_C1)
+                      : h ? (1u << S_B2) | (1u << S_IJKL) : (1u << S_B1) | (1u << S_EFGH);
+  if (rl < 0 || rl >= TILE_ROWS || L[L_QSEL + (rl >> 2)] != want) return;
+  const uint32_t r = (uint32_t)rl;
+  uint32_t f;
+  if (kind == 0 || kind == 2) {
+    f = g_add(T, r, L[L_A9 + (r >> 2)], kind == 0) ? 0u : want;
+  } else if (kind == 1) {
+    f = g_xor(T, r, false) ? 0u : want;
+  } else {
+    f = h ? g_xor63(T, r, want) : g_xor24(T, r, want);
   }
-  if (mine(sl + 4)) {  // d1 / d2
-    r = (uint32_t)(sl + 4);
-    if (!g_xor(T, r, false)) A.fail_gates(tile0 + r, 1u << (h ? S_D2 : S_D1));
-  }
-  if (mine(sl + 12)) {  // c1 / c2
-    r = (uint32_t)(sl + 12);
-    if (!g_add(T, r, L[L_A9 + (r >> 2)], false)) A.fail_gates(tile0 + r, 1u << (h ? S_C2 : S_C1));
-  }
-  if (mine(sl + 16)) {  // b1 (XOR24) / b2 (XOR63)
-    r = (uint32_t)(sl + 16);
-    uint32_t f = h ? g_xor63(T, r, (1u << S_B2) | (1u << S_IJKL))
-                   : g_xor24(T, r, (1u << S_B1) | (1u << S_EFGH));
-    if (f) A.fail_gates(tile0 + r, f);
-  }
+  if (f) A.fail_gates(tile0 + r, f);
 }
 
 // Copy-source lookup, all from LDS for a valid trace: rows inside the window come from W;
@@ -1282,6 +1281,10 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
 #pragma unroll
     for (int c = 0; c < 9; c++) *reinterpret_cast<uint4*>(&L[lds_cell(c, 4 * tid)]) = q[c];
     const uint4 cur9 = q[A9], curfx = q[10];
+    if (MODE & EVAL_GATES) {
+      L[L_QSEL + tid] = (curfx.x & 0xffffu) | (((curfx.y | curfx.z | curfx.w) & 0xffffu) ? 1u << 16 : 0u);
+      L[L_A9 + tid] = cur9.x;
+    }
     if (e0.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e0.lds]) = x0;
     if (e1.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e1.lds]) = x1;
     __syncthreads();
@@ -1293,13 +1296,15 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
     }
     const uint64_t tile0 = t * TILE_ROWS;
     const uint64_t gq = t * BLOCK + tid;
+    // ---- canonical round blocks: (G, half) items, one block kind per wave
+    if (MODE & EVAL_GATES) half_g_gates(T, A, L, tile0, n, total_rows, (uint32_t)tid & 63u,
+                                          (uint32_t)tid >> 6);
     if ((MODE & EVAL_TOUCH) && gq < total_quads) {  // diagnostics: keep the staged words alive
       uint4 a = T.quad(A0, 4 * tid), b = T.quad(A8, 4 * tid);
       uint32_t x = a.x ^ b.w ^ cur9.x ^ curfx.y ^ L[L_W + 4 * tid] ^ L[L_IC + (tid & 255)] ^
                    L[L_INFO + (tid & 15)] ^ T.at(A3, 4 * tid + 13);
       if (x == 0x12345678u) A.fail(0, B2F_CODE_LOOKUP);
     }
-    uint32_t regular = 0;
     if (gq < total_quads) {
       const uint64_t row0 = 4 * gq;
       const uint32_t lr0 = 4 * tid;
@@ -1351,7 +1356,7 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
       // (init / final blocks, a corrupted fixed column) is evaluated here, row by row
       if (MODE & EVAL_GATES) {
         const uint32_t rest = (curfx.y | curfx.z | curfx.w) & 0xffffu;
-        regular = (is_round && cached && rest == 0 && (curfx.x & 0xffffu) == L[L_XS + p]) ? 1u : 0u;
+        const bool regular = is_round && cached && rest == 0 && (curfx.x & 0xffffu) == L[L_XS + p];
         if (!regular) {
           uint32_t rowmask = ((curfx.x & 0xffffu) ? 1u : 0u) | ((curfx.y & 0xffffu) ? 2u : 0u) |
                              ((curfx.z & 0xffffu) ? 4u : 0u) | ((curfx.w & 0xffffu) ? 8u : 0u);
@@ -1435,13 +1440,6 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
           copies_edge(A, dq, src, o, rounds, lq);
         }
       }
-    }
-    if (MODE & EVAL_GATES) {
-      // ---- canonical round blocks: one lane per (G, half) in the first wave
-      reinterpret_cast<uint8_t*>(L + L_FLAG)[tid] = (uint8_t)regular;
-      L[L_A9 + tid] = cur9.x;
-      __syncthreads();
-      if (tid < 64) half_g_gates(T, A, L, tile0, n, (uint32_t)tid);
     }
     __syncthreads();
   }
