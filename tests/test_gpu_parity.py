@@ -115,6 +115,32 @@ def test_layout_errors(engine):
                         batch.advice.data_ptr(), batch.fixed.data_ptr(), 0)
 
 
+def test_eval_dev_flags_bad_offsets(engine):
+    """b2f_eval_dev validates the row map on the device (offsets_check_kernel): a shifted
+    offset and a zero-length instance are both B2F_ERR_LAYOUT, and a good map is clean."""
+    import b2f
+    import torch
+
+    stream = torch.cuda.current_stream().cuda_stream
+    x = random_inputs(6, (1, 2, 4), 10)
+    batch = b2f.DeviceBatch(x)
+    batch.fill(engine)
+    batch.evaluate(engine)
+    engine.sync(stream)
+    assert batch.report_dict()["first_failure"] == 2**64 - 1
+    good = batch.offsets.clone()
+    for i, new in ((3, int(good[3]) + 4), (2, int(good[1]))):
+        batch.offsets.copy_(good)
+        batch.offsets[i] = new
+        batch.evaluate(engine)
+        with pytest.raises(b2f.B2FError) as ei:
+            engine.sync(stream)
+        assert ei.value.code == 5
+    batch.offsets.copy_(good)
+    batch.evaluate(engine)
+    engine.sync(stream)
+
+
 def test_device_batch_2p16_bitexact(engine, orc):
     """BASELINE config 2: 2^16 x 12 rounds, full column diff against the oracle, streamed
     in chunks of instances so host memory stays bounded."""

@@ -575,30 +575,44 @@ __global__ void __launch_bounds__(BLOCK) fill_kernel(const b2f_input* __restrict
 // CU). While a workgroup checks tile t out of LDS, its loads for tile t + gridDim are already
 // in flight into registers; at the next iteration they are written to LDS behind one barrier.
 //
+// Per tile, one lane of the first wave per G whose rows meet the tile builds the G table (its
+// window/init-cache bases, message rows, G index) and marks which quads are round quads; the
+// gates of canonical round blocks and the 72 copy checks of every G then run from that table
+// spread evenly over the workgroup, whatever block each quad holds. Only init/final quads
+// (about 4% at 12 rounds) and non-canonical selector rows take per-quad paths.
+//
 // LDS per workgroup (one array, 16-byte aligned carve):
 //   W   the canonical columns a_1 a_2 a_7 a_8 (every copy source is one of them) for rows
 //       [tile0 - HIST, tile0 + TILE_ROWS + HALO): the tile plus a history window holding
-//       every state-word source (<= 361 rows back, see make_copy_table);
+//       every state-word source (<= 361 rows back, see max_copy_distance);
 //   G   the other gate columns a_0 a_3 a_4 a_5 a_6 for rows [tile0, tile0 + TILE_ROWS + HALO);
-//   CT  copy-source table (make_copy_table), SG SIGMA, INFO the tile's TileInfo,
+//   CT  copy-check table (make_check_table), SG SIGMA, INFO the tile's TileInfo,
 //   IC  init-region cache: a_1 | a_2 of rows 0..163 of the tile's first instance, the only
-//       instance whose init region (h, m, t, fmask, IV, v12..v14) can lie before the window.
-// a_9 and the fixed column are only read on their own row: kept in registers.
+//       instance whose init region (h, m, t, fmask, IV, v12..v14) can lie before the window;
+//   GT  the tile's G table, QM quad -> position in its G (0xff: not a round quad),
+//   QSEL / A9 per quad: row-0 selector bits (| 1 << 16 if rows 1-3 carry any) and row-0 a_9.
+// a_9 and the fixed column are otherwise only read on their own row: kept in registers.
+
+constexpr int G_CHECKS = 72;  // copy constraints per G (static_assert below)
+constexpr int MAX_TILE_G = 24;  // G starts in [tile0 - 51, tile0 + 1023]: at most 21
+constexpr int GT_WORDS = 8;
 
 constexpr int L_W = 0;
 constexpr int L_G = L_W + 4 * WSTRIDE;
 constexpr int L_CT = L_G + 5 * TSTRIDE;
-constexpr int L_SG = L_CT + 8 * G_QUADS * 12;
+constexpr int L_SG = L_CT + 12 * G_CHECKS;
 constexpr int L_INFO = L_SG + 40;
 constexpr int L_IC = L_INFO + 24;
 constexpr int L_XS = L_IC + 2 * INIT_ROWS;   // expected row-0 selector bits per G quad (16)
-constexpr int L_QSEL = L_XS + 16;            // per quad: row-0 selector bits | 1 << 16 if rows
-                                             // 1-3 carry any selector
-constexpr int L_A9 = L_QSEL + BLOCK;         // per quad: a_9 of its first row
-constexpr int L_ACC = L_A9 + BLOCK;  // 16 gate + lookup + copy counters, first (u64)
+constexpr int L_QSEL = L_XS + 16;
+constexpr int L_A9 = L_QSEL + BLOCK;
+constexpr int L_GT = L_A9 + BLOCK;           // MAX_TILE_G x GT_WORDS
+constexpr int L_QM = L_GT + MAX_TILE_G * GT_WORDS;  // BLOCK bytes
+constexpr int L_NG = L_QM + BLOCK / 4;       // number of G table entries
+constexpr int L_ACC = L_NG + 4;  // 16 gate + lookup + copy counters, first (u64)
 constexpr int LDS_WORDS = L_ACC + 20 + 2;
-static_assert(L_INFO % 4 == 0 && L_IC % 4 == 0 && L_G % 4 == 0 && L_CT % 4 == 0,
-              "16-byte aligned carve");
+static_assert(L_INFO % 4 == 0 && L_IC % 4 == 0 && L_G % 4 == 0 && L_CT % 4 == 0 && L_ACC % 2 == 0,
+              "aligned carve");
 static_assert(LDS_WORDS * 4 * 3 <= 160 * 1024, "three eval workgroups per CU");
 
 // Row-0 selector bits of each quad of a G when the fixed column is canonical (LAYOUT.md §5:
@@ -686,65 +700,104 @@ constexpr DescTable make_desc() {
 // consumer's G is a constant of (g, role, limb).
 constexpr uint8_t kGidx[8][4] = {{0, 4, 8, 12}, {1, 5, 9, 13}, {2, 6, 10, 14}, {3, 7, 11, 15},
                                  {0, 5, 10, 15}, {1, 6, 11, 12}, {2, 7, 8, 13}, {3, 4, 9, 14}};
-struct CopyTable {
-  uint32_t e[8][G_QUADS][4][3];
-};
 constexpr uint32_t wc_of(uint32_t col) { return col == A1 ? 0 : col == A2 ? 1 : col == A7 ? 2 : 3; }
-constexpr uint32_t pack_copy(uint32_t kind, uint32_t wc, uint32_t k, uint32_t y, int rel,
-                             uint32_t abs0, uint32_t wc0) {
-  return kind | (wc << 2) | (k << 4) | (y << 6) | ((uint32_t)(rel + 512) << 7) | (abs0 << 17) |
-         (wc0 << 25);
+
+// The copy checks of one G as a flat list (every operand cell of its eight blocks that is a
+// copy, LAYOUT.md §5 round table), with each source resolved at compile time per G index g:
+// entry [g] for half-rounds >= 1, [8 + g] for the first half-round (g < 4), whose state words
+// come from the instance's init region. Entry (u32):
+//   bits 0-13  C: LDS offset of the source relative to the per-G base chosen by bits 14-16
+//   bits 14-16 base: 0 window at the G start (- CBIAS), 1 init-region a_1, 2 init-region a_2,
+//              3 message x row, 4 message y row (GT words 0..4)
+//   bits 17-18 operand column a_3 / a_4 / a_5;  bits 19-24 operand row in the G (0..51)
+// In-G and state-word sources are `rel` rows from the G start: the state word of role a/b/c/d
+// of the half-round start was produced by the G of the previous half-round that owns it, in
+// its last step of that role (a <- a2 +28, b <- b2 +44 stride 2, c <- c2 +40, d <- d2 +32
+// rot 16), whose index is fixed by g, so rel is a constant of (g, role, limb).
+constexpr int CBIAS = 512;
+struct CheckTable {
+  uint32_t e[12][G_CHECKS];
+};
+constexpr uint32_t pack_check(uint32_t C, uint32_t base, uint32_t dcol, uint32_t drow) {
+  return C | (base << 14) | (dcol << 17) | (drow << 19);
 }
-constexpr CopyTable make_copy_table() {
-  CopyTable T{};
+constexpr int state_rel(uint32_t g, uint32_t role, uint32_t k) {
+  uint32_t w = kGidx[g][role], pos = w & 3u;
+  uint32_t prev_odd = g < 4 ? 1u : 0u;  // parity of the previous half-round
+  uint32_t gp = prev_odd ? ((pos - role) & 3u) : pos;
+  uint32_t off = role == 0 ? 28 + k : role == 1 ? 44 + 2 * k : role == 2 ? 40 + k
+                                                               : 32 + 2 * ((k + 1) & 3u);
+  return -(int)ROUND_ROWS / 2 + (int)G_ROWS * ((int)gp - (int)(g & 3u)) + (int)off;
+}
+constexpr uint32_t state_abs0(uint32_t g, uint32_t role, uint32_t k) {  // init-region row
+  uint32_t w = kGidx[g][role];
+  return w < 8 ? 4 * w + k : (w >= 12 && w < 15) ? 140 + 8 * (w - 12) + 2 * k
+                                                 : 108 + 4 * (w == 15 ? 7u : w - 8) + k;
+}
+constexpr CheckTable make_check_table() {
+  CheckTable T{};
   DescTable D = make_desc();
-  for (uint32_t g = 0; g < 8; g++)
+  for (uint32_t v = 0; v < 12; v++) {
+    uint32_t g = v < 8 ? v : v - 8;
+    bool hr0 = v >= 8;
+    int ci = 0;
     for (uint32_t p = 0; p < G_QUADS; p++)
       for (uint32_t j = 0; j < 4; j++)
         for (uint32_t c = 0; c < 3; c++) {
-          uint32_t d = D.d[p][j][c], kind = d & 3u, e = 0;
+          uint32_t d = D.d[p][j][c], kind = d & 3u, drow = 4 * p + j, e = 0;
+          if (kind == 0) continue;
           if (kind == 1) {
-            e = pack_copy(1, wc_of(d >> 8), 0, 0, (int)((d >> 2) & 63u), 0, 0);
+            uint32_t rel = (d >> 2) & 63u, wc = wc_of(d >> 8);
+            e = pack_check(L_W + wc * WSTRIDE + rel + CBIAS, 0, c, drow);
           } else if (kind == 2) {
             uint32_t role = (d >> 2) & 3u, k = (d >> 4) & 3u, sp = (d >> 6) & 1u;
-            uint32_t w = kGidx[g][role], pos = w & 3u;
-            uint32_t prev_odd = g < 4 ? 1u : 0u;  // parity of half-round hr - 1
-            uint32_t gp = prev_odd ? ((pos - role) & 3u) : pos;
-            uint32_t off = role == 0 ? 28 + k : role == 1 ? 44 + 2 * k : role == 2 ? 40 + k
-                                                                         : 32 + 2 * ((k + 1) & 3u);
-            int rel = -208 + 52 * ((int)gp - (int)(g & 3u)) + (int)off;
-            uint32_t col = role == 1 ? (sp ? A8 : A7) : (sp ? A2 : A1);
-            uint32_t abs0 = w < 8 ? 4 * w + k
-                            : (w >= 12 && w < 15) ? 140 + 8 * (w - 12) + 2 * k
-                                                  : 108 + 4 * (w == 15 ? 7u : w - 8) + k;
-            e = pack_copy(2, wc_of(col), k, 0, rel, abs0, sp ? 1u : 0u);
-          } else if (kind == 3) {
-            e = pack_copy(3, 0, (d >> 4) & 3u, (d >> 2) & 1u, 0, 0, 0);
+            if (hr0) {
+              e = pack_check(state_abs0(g, role, k), 1 + sp, c, drow);
+            } else {
+              uint32_t col = role == 1 ? (sp ? A8 : A7) : (sp ? A2 : A1);
+              e = pack_check((uint32_t)((int)(L_W + wc_of(col) * WSTRIDE) + state_rel(g, role, k) + CBIAS),
+                             0, c, drow);
+            }
+          } else {
+            e = pack_check((d >> 4) & 3u, 3 + ((d >> 2) & 1u), c, drow);
           }
-          T.e[g][p][j][c] = e;
+          if (ci < G_CHECKS) T.e[v][ci] = e;
+          ci++;
         }
+    if (ci != G_CHECKS) T.e[0][0] = 0xffffffffu;  // trips the static_assert below
+  }
   return T;
 }
-// The deepest state-word source (dst - src rows) must fit the history window.
+constexpr bool check_table_ok() {
+  CheckTable T = make_check_table();
+  if (T.e[0][0] == 0xffffffffu) return false;
+  for (int v = 0; v < 12; v++)
+    for (int i = 0; i < G_CHECKS; i++) {
+      uint32_t e = T.e[v][i];
+      if (((e >> 14) & 7u) > 4 || ((e >> 19) & 63u) >= G_ROWS || ((e >> 17) & 3u) > 2) return false;
+    }
+  return true;
+}
+static_assert(check_table_ok(), "72 copy checks per G, fields in range");
+// The deepest state-word source (consumer row - source row) must fit the history window.
 constexpr int max_copy_distance() {
-  CopyTable T = make_copy_table();
+  DescTable D = make_desc();
   int m = 0;
   for (uint32_t g = 0; g < 8; g++)
     for (uint32_t p = 0; p < G_QUADS; p++)
       for (uint32_t j = 0; j < 4; j++)
-        for (uint32_t c = 0; c < 3; c++)
-          if ((T.e[g][p][j][c] & 3u) == 2) {
-            int dst = 4 * (int)p + (int)j;  // the G's quads are contiguous from its first row
-            int rel = (int)((T.e[g][p][j][c] >> 7) & 1023u) - 512;
-            int dist = dst - rel;
-            m = dist > m ? dist : m;
-          }
+        for (uint32_t c = 0; c < 3; c++) {
+          uint32_t d = D.d[p][j][c];
+          if ((d & 3u) != 2) continue;
+          int dist = (int)(4 * p + j) - state_rel(g, (d >> 2) & 3u, (d >> 4) & 3u);
+          m = dist > m ? dist : m;
+        }
   return m;
 }
 static_assert(max_copy_distance() + 4 <= HIST, "history window too small for state sources");
 
-__constant__ __attribute__((aligned(16))) CopyTable c_copy = make_copy_table();
-constexpr int COPY_WORDS = (int)(sizeof(CopyTable) / 4);  // 1248
+__constant__ __attribute__((aligned(16))) CheckTable c_checks = make_check_table();
+constexpr int CHECK_WORDS = (int)(sizeof(CheckTable) / 4);  // 864
 
 // Failure accounting. Failures are rare, so they go straight to LDS atomics (per-workgroup
 // counters, flushed once at the end) instead of occupying registers on the hot path.
@@ -961,7 +1014,7 @@ __device__ __forceinline__ bool g_add(const Tile& T, uint32_t r, uint32_t a9, bo
 }
 __device__ __forceinline__ uint32_t g_xor24(const Tile& T, uint32_t r, uint32_t sel) {
   bool b1 = true, efgh = true;
-#pragma unroll
+#pragma unroll 1
   for (int k = 0; k < 4; k++) {
     uint32_t b = r + 3 * k, k1 = r + 3 * ((k + 1) & 3), k2 = r + 3 * ((k + 2) & 3);
     b1 &= (uint64_t)T.at(A3, b) + T.at(A4, b) ==
@@ -975,7 +1028,7 @@ __device__ __forceinline__ uint32_t g_xor24(const Tile& T, uint32_t r, uint32_t 
 __device__ __forceinline__ uint32_t g_xor63(const Tile& T, uint32_t r, uint32_t sel) {
   V3 a2 = rows8(T, A2, r);
   bool b2 = true, ijkl = true;
-#pragma unroll
+#pragma unroll 1
   for (int k = 0; k < 4; k++) {
     uint32_t b = 2 * k, k3 = 2 * ((k + 3) & 3);
     uint32_t zb = T.at(A6, r + b), zp = T.at(A6, r + k3);
@@ -1016,28 +1069,29 @@ __device__ __forceinline__ uint32_t row_gates(const Tile& T, uint32_t sel, uint3
   }
 }
 
-// Gates of the canonical round blocks of a tile. A tile holds at most 21 G starts in
-// [tile0 - 44, tile0 + 1023]; lane l of every wave takes item l = (G, half), and wave w checks
-// block kind w of it: 0 a1/a2 (ADD3, +0/+28), 1 d1/d2 (XOR, +4/+32), 2 c1/c2 (ADD2, +12/+40),
-// 3 b1 (XOR24, +16) / b2 (XOR63, +44). Each wave thus runs one evaluator (the b wave two)
-// instead of every wave running all five block kinds mostly masked, as a quad-per-lane
-// assignment would. A block is checked here only if the quad holding its selector row lies in
-// this tile and is canonical: row-0 selector bits exactly the block's and none on rows 1-3
-// (L_QSEL, written at staging). Every other selector row is evaluated by its own quad's lane
-// (row_gates), so each selector row is evaluated exactly once.
-__device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const uint32_t* L,
-                                             uint64_t tile0, uint32_t n, uint64_t total_rows,
-                                             uint32_t lane, uint32_t kind) {
+// G table of a tile (first wave, lane l = l-th G in row order whose start lies in
+// [tile0 - 51, tile0 + 1023], over the instances cached in INFO). GT words:
+//   0 window base of the G start - CBIAS     1, 2 init-region base of a_1, a_2
+//   3, 4 message x / y row bases             5 G start, tile-local      6 check-table row
+// Init-region bases point into the init cache for the tile's first instance (its init region
+// may lie before the window) and into the window for any later instance (which starts inside
+// the tile, so its init region is in the window). QM[q] = position of quad q in its G.
+// Instances past the cached eight cannot occur in a valid layout (each is >= 228 rows);
+// b2f_eval_dev flags invalid layouts separately (offsets_check_kernel).
+__device__ __forceinline__ void build_g_table(uint32_t* L, uint64_t tile0, uint32_t n,
+                                              uint64_t total_rows, uint32_t lane) {
   const uint32_t first = L[L_INFO];
   const uint64_t* Off = reinterpret_cast<const uint64_t*>(L + L_INFO + 2);
-  const int64_t lo = (int64_t)tile0 - 44, hi = (int64_t)tile0 + TILE_ROWS - 1;
-  uint32_t base = 0, h = 0;
-  int64_t gs = -1;
+  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + L_SG);
+  const int64_t lo = (int64_t)tile0 - (G_ROWS - 1), hi = (int64_t)tile0 + TILE_ROWS - 1;
+  uint32_t base = 0, m = 0;
+  int64_t o_mine = -1;
+  bool ofst = false;
   for (int i = 0; i + 1 < NOFF; i++) {
     if (first + (uint32_t)i >= n) break;
     const uint64_t o = Off[i], o1 = Off[i + 1];
     if ((int64_t)o > hi) break;
-    if (o1 <= o || o1 > total_rows || o1 - o > MAX_INSTANCE_ROWS) continue;  // quads irregular
+    if (o1 <= o || o1 > total_rows || o1 - o > MAX_INSTANCE_ROWS) continue;
     const uint32_t R = (uint32_t)(o1 - o);
     if (R < FIXED_ROWS || (R - FIXED_ROWS) % ROUND_ROWS) continue;
     const uint32_t n_g = 8 * ((R - FIXED_ROWS) / ROUND_ROWS);
@@ -1050,16 +1104,53 @@ __device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const ui
     uint32_t m_hi = (uint32_t)b / G_ROWS;
     if (m_hi >= n_g) m_hi = n_g - 1;
     if (m_lo > m_hi) continue;
-    const uint32_t items = 2 * (m_hi - m_lo + 1);
-    if (gs < 0 && lane >= base && lane < base + items) {
-      gs = g0 + (int64_t)G_ROWS * (int64_t)(m_lo + (lane - base) / 2);
-      h = (lane - base) & 1u;
+    const uint32_t cnt = m_hi - m_lo + 1;
+    if (o_mine < 0 && lane >= base && lane < base + cnt) {
+      o_mine = (int64_t)o;
+      m = m_lo + (lane - base);
+      ofst = i == 0;
     }
-    base += items;
+    base += cnt;
   }
-  if (gs < 0) return;
-  const int off = (int)kind == 0 ? 0 : kind == 1 ? 4 : kind == 2 ? 12 : 16;
-  const int rl = (int)(gs - (int64_t)tile0) + 28 * (int)h + off;  // tile-local selector row
+  if (lane == 0) L[L_NG] = base < (uint32_t)MAX_TILE_G ? base : (uint32_t)MAX_TILE_G;
+  if (o_mine < 0 || lane >= (uint32_t)MAX_TILE_G) return;
+  const uint32_t r = m >> 3, g = m & 7u;
+  const int gl = (int)(o_mine + INIT_ROWS + (int64_t)G_ROWS * m - (int64_t)tile0);
+  const int64_t ob64 = o_mine - (int64_t)tile0 + HIST;  // instance start, window index
+  const int ob = ofst ? 0 : (int)ob64;                    // (later instances: in the window)
+  const int ib0 = ofst ? L_IC : L_W + ob;
+  const int ib1 = ofst ? L_IC + (int)INIT_ROWS : L_W + WSTRIDE + ob;
+  const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
+  uint32_t* gt = L + L_GT + GT_WORDS * lane;
+  gt[0] = (uint32_t)(gl + HIST - CBIAS);
+  gt[1] = (uint32_t)ib0;
+  gt[2] = (uint32_t)ib1;
+  gt[3] = (uint32_t)(ib0 + 32 + 4 * sg[0]);
+  gt[4] = (uint32_t)(ib0 + 32 + 4 * sg[1]);
+  gt[5] = (uint32_t)gl;
+  gt[6] = (m < 4 ? 8 + g : g) * G_CHECKS;
+  uint8_t* qm = reinterpret_cast<uint8_t*>(L + L_QM);
+#pragma unroll
+  for (int p = 0; p < (int)G_QUADS; p++) {
+    int q = (gl >> 2) + p;
+    if (q >= 0 && q < BLOCK) qm[q] = (uint8_t)p;
+  }
+}
+
+// Gates of the canonical round blocks of a tile. Lane l of every wave takes item l =
+// (G table entry l >> 1, half l & 1), and wave w checks block kind w of it: 0 a1/a2 (ADD3,
+// +0/+28), 1 d1/d2 (XOR, +4/+32), 2 c1/c2 (ADD2, +12/+40), 3 b1 (XOR24, +16) / b2 (XOR63,
+// +44). Each wave thus runs one evaluator (the b wave two) instead of every wave running all
+// five block kinds mostly masked, as a quad-per-lane assignment would. A block is checked here
+// only if its selector row lies in this tile and its quad is canonical: row-0 selector bits
+// exactly the block's and none on rows 1-3 (QSEL, staged). Every other selector row is
+// evaluated by its own quad's lane (row_gates), so each selector row is evaluated once.
+__device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const uint32_t* L,
+                                             uint64_t tile0, uint32_t lane, uint32_t kind) {
+  if (lane >= 2 * L[L_NG]) return;
+  const uint32_t h = lane & 1u;
+  const int off = kind == 0 ? 0 : kind == 1 ? 4 : kind == 2 ? 12 : 16;
+  const int rl = (int)L[L_GT + GT_WORDS * (lane >> 1) + 5] + 28 * (int)h + off;  // selector row
   const uint32_t want = kind == 0 ? 1u << (h ? S_A2 : S_A1)
                       : kind == 1 ? 1u << (h ? S_D2 : S_D1)
                       : kind == 2 ? 1u << (h ? S_C2 : S_C1)
@@ -1075,6 +1166,28 @@ __device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const ui
     f = h ? g_xor63(T, r, want) : g_xor24(T, r, want);
   }
   if (f) A.fail_gates(tile0 + r, f);
+}
+
+// The copy checks of the tile's G's: item it = (G table entry it / 72, check it % 72), spread
+// over all threads. A check belongs to this tile if its operand row does; its source is one
+// LDS read at (per-G base) + C for every valid layout.
+__device__ __forceinline__ void round_copies(EvalAcc& A, const uint32_t* L, uint64_t tile0,
+                                             uint32_t tid) {
+  const uint32_t nchk = L[L_NG] * G_CHECKS;
+#pragma unroll 2
+  for (uint32_t k = 0; k < (MAX_TILE_G * G_CHECKS + BLOCK - 1) / BLOCK; k++) {
+    const uint32_t it = tid + k * BLOCK;
+    if (it >= nchk) break;
+    const uint32_t gi = it / G_CHECKS, ci = it - gi * G_CHECKS;
+    const uint32_t* gt = L + L_GT + GT_WORDS * gi;
+    const uint32_t e = L[L_CT + gt[6] + ci];
+    const int dl = (int)gt[5] + (int)((e >> 19) & 63u);
+    const int src = (int)gt[(e >> 14) & 7u] + (int)(e & 16383u);
+    const uint32_t sv = L[src < 0 ? 0 : src];  // < 0 only for checks outside the tile
+    const int dlc = dl < 0 ? 0 : (dl >= TILE_ROWS ? TILE_ROWS - 1 : dl);
+    const uint32_t dv = L[L_G + (1 + ((e >> 17) & 3u)) * TSTRIDE + dlc];
+    if (dl >= 0 && dl < TILE_ROWS && dv != sv) A.fail(tile0 + (uint64_t)dl, B2F_CODE_COPY);
+  }
 }
 
 // Copy-source lookup, all from LDS for a valid trace: rows inside the window come from W;
@@ -1235,8 +1348,8 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
                                                     int* __restrict__ status) {
   __shared__ __attribute__((aligned(16))) uint32_t L[LDS_WORDS];
   const int tid = threadIdx.x;
-  for (int i = tid; i < COPY_WORDS; i += BLOCK)
-    L[L_CT + i] = reinterpret_cast<const uint32_t*>(&c_copy)[i];
+  for (int i = tid; i < CHECK_WORDS; i += BLOCK)
+    L[L_CT + i] = reinterpret_cast<const uint32_t*>(&c_checks)[i];
   if (tid < 40) L[L_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
   if (tid < 16) L[L_XS + tid] = expected_sel((uint32_t)tid);
   const Tile T{L};
@@ -1281,9 +1394,10 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
 #pragma unroll
     for (int c = 0; c < 9; c++) *reinterpret_cast<uint4*>(&L[lds_cell(c, 4 * tid)]) = q[c];
     const uint4 cur9 = q[A9], curfx = q[10];
-    if (MODE & EVAL_GATES) {
+    if (MODE & (EVAL_GATES | EVAL_COPIES)) {
       L[L_QSEL + tid] = (curfx.x & 0xffffu) | (((curfx.y | curfx.z | curfx.w) & 0xffffu) ? 1u << 16 : 0u);
       L[L_A9 + tid] = cur9.x;
+      if (tid < BLOCK / 4) L[L_QM + tid] = 0xffffffffu;
     }
     if (e0.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e0.lds]) = x0;
     if (e1.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e1.lds]) = x1;
@@ -1296,148 +1410,68 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
     }
     const uint64_t tile0 = t * TILE_ROWS;
     const uint64_t gq = t * BLOCK + tid;
-    // ---- canonical round blocks: (G, half) items, one block kind per wave
-    if (MODE & EVAL_GATES) half_g_gates(T, A, L, tile0, n, total_rows, (uint32_t)tid & 63u,
-                                          (uint32_t)tid >> 6);
+    const uint64_t row0 = 4 * gq;
+    const uint32_t lr0 = 4 * tid;
     if ((MODE & EVAL_TOUCH) && gq < total_quads) {  // diagnostics: keep the staged words alive
       uint4 a = T.quad(A0, 4 * tid), b = T.quad(A8, 4 * tid);
       uint32_t x = a.x ^ b.w ^ cur9.x ^ curfx.y ^ L[L_W + 4 * tid] ^ L[L_IC + (tid & 255)] ^
                    L[L_INFO + (tid & 15)] ^ T.at(A3, 4 * tid + 13);
       if (x == 0x12345678u) A.fail(0, B2F_CODE_LOOKUP);
     }
-    if (gq < total_quads) {
-      const uint64_t row0 = 4 * gq;
-      const uint32_t lr0 = 4 * tid;
-      // ---- lookups on the 4 rows
-      if (MODE & EVAL_LOOKUP) {
-        const uint4 q0 = T.quad(A0, lr0), q1 = T.quad(A1, lr0), q2 = T.quad(A2, lr0);
+    // ---- lookups on the 4 rows (before the G table barrier: they need only the staged tile)
+    if ((MODE & EVAL_LOOKUP) && gq < total_quads) {
+      const uint4 q0 = T.quad(A0, lr0), q1 = T.quad(A1, lr0), q2 = T.quad(A2, lr0);
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          uint32_t tg = comp(q0, j), de = comp(q1, j), sp = comp(q2, j);
-          bool ok = de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu);
-          if (!ok) A.fail(row0 + j, B2F_CODE_LOOKUP);
-        }
+      for (int j = 0; j < 4; j++) {
+        uint32_t tg = comp(q0, j), de = comp(q1, j), sp = comp(q2, j);
+        bool ok = de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu);
+        if (!ok) A.fail(row0 + j, B2F_CODE_LOOKUP);
       }
-      // ---- the quad's instance: scan the tile's offsets in LDS (global beyond NOFF - 1)
-      const uint32_t first = L[L_INFO];
-      const uint64_t* Off = reinterpret_cast<const uint64_t*>(L + L_INFO + 2);
-      bool valid = false, cached = false, is_round = false;
-      uint64_t o = 0;
-      uint32_t rounds = 0, lq = 0, r = 0, g = 0, p = 0;
-      if (row0 < used_rows) {
-        uint32_t inst = first, i = 0;
-        while (i + 2 < NOFF && Off[i + 1] <= row0) i++;
-        inst += i;
-        o = Off[i];
-        uint64_t o1 = Off[i + 1];
-        cached = o1 > row0;
-        if (!cached) {  // more than NOFF - 1 instances start in this tile (tiny rounds)
-          do { inst++; o = o1; o1 = off[inst + 1]; } while (o1 <= row0);
-        }
-        const uint32_t R = (uint32_t)(o1 - o);
-        valid = o1 > o && o1 <= total_rows && o1 - o <= MAX_INSTANCE_ROWS && R >= FIXED_ROWS &&
-                (R - FIXED_ROWS) % ROUND_ROWS == 0;
-        if (valid) {
-          rounds = (R - FIXED_ROWS) / ROUND_ROWS;
-          lq = (uint32_t)((row0 - o) >> 2);
-          const uint32_t rq = lq - INIT_QUADS;
-          is_round = lq >= INIT_QUADS && rq < ROUND_QUADS * rounds;
-          if (is_round) {
-            r = rq / ROUND_QUADS;
-            const uint32_t w = rq - r * ROUND_QUADS;
-            g = w / G_QUADS;
-            p = w - g * G_QUADS;
-          }
-        } else if (MODE & EVAL_COPIES) {
-          atomicOr(status, 1 << B2F_ERR_LAYOUT);
-        }
-      }
-      // ---- gates: canonical round quads go to the per-G pass below; every other selector row
-      // (init / final blocks, a corrupted fixed column) is evaluated here, row by row
-      if (MODE & EVAL_GATES) {
-        const uint32_t rest = (curfx.y | curfx.z | curfx.w) & 0xffffu;
-        const bool regular = is_round && cached && rest == 0 && (curfx.x & 0xffffu) == L[L_XS + p];
-        if (!regular) {
-          uint32_t rowmask = ((curfx.x & 0xffffu) ? 1u : 0u) | ((curfx.y & 0xffffu) ? 2u : 0u) |
-                             ((curfx.z & 0xffffu) ? 4u : 0u) | ((curfx.w & 0xffffu) ? 8u : 0u);
-          while (rowmask) {
-            int j = __builtin_ctz(rowmask);
-            rowmask &= rowmask - 1;
-            uint32_t k0 = comp(curfx, j);
-            uint32_t failed;
-            if ((k0 & 0xffffu) == (1u << S_CONST)) failed = T.at(A1, lr0 + j) == (k0 >> 16) ? 0u : 1u << S_CONST;
-            else failed = row_gates(T, k0 & 0xffffu, lr0 + j, comp(cur9, j), k0);
-            if (failed) A.fail_gates(row0 + j, failed);
-          }
-        }
-      }
-      // ---- copy constraints whose operand cell lies in this quad
-      if ((MODE & EVAL_COPIES) && valid) {
-        const uint64_t ofirst = L[L_INFO] < n ? *reinterpret_cast<const uint64_t*>(L + L_INFO + 2) : ~0ull;
-        if (is_round) {
-          // every source of a valid layout is in the window W (rows [tile0 - HIST, tile0 +
-          // TILE_ROWS + HALO)) or, for init-region words of the tile's first instance, in the
-          // init cache; offsets are 32-bit from here on
-          const int64_t wlo = (int64_t)tile0 - HIST;
-          const uint64_t gbase = o + INIT_ROWS + (uint64_t)ROUND_ROWS * r + G_ROWS * g;
-          const int gbw = (int)((int64_t)gbase - wlo);
-          const int64_t ib = (int64_t)o - wlo;
-          const int ibw = ib < -(1 << 30) ? -(1 << 30) : (int)ib;
-          const bool ofst = o == ofirst;
-          const bool hr0 = (r == 0) && (g < 4);
-          const uint4* ctq = reinterpret_cast<const uint4*>(L + L_CT + (g * G_QUADS + p) * 12);
-          const uint4 ce[3] = {ctq[0], ctq[1], ctq[2]};
-          const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
-          const uint32_t sgx = sg[0], sgy = sg[1];
-          const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
-          uint32_t bad = 0, needg = 0;  // bit 3*j + c
-#pragma unroll
-          for (int j = 0; j < 4; j++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-              const int sl = 3 * j + c;
-              const uint32_t e = comp(ce[sl >> 2], sl & 3);
-              const uint32_t kind = e & 3u;
-              const bool msg = kind == 3, st0 = kind == 2 && hr0, from_init = msg || st0;
-              const uint32_t init_row = msg ? 32 + 4 * (((e >> 6) & 1u) ? sgy : sgx) + ((e >> 4) & 3u)
-                                            : (e >> 17) & 255u;
-              const int d = from_init ? ibw + (int)init_row : gbw + (int)((e >> 7) & 1023u) - 512;
-              const uint32_t wc = st0 ? (e >> 25) & 3u : (e >> 2) & 3u;
-              const bool in_w = (uint32_t)d < (uint32_t)WSTRIDE;
-              const uint32_t idx = in_w ? L_W + wc * WSTRIDE + (uint32_t)d
-                                        : L_IC + (wc & 1u) * INIT_ROWS + init_row;
-              const uint32_t sv = L[idx];
-              const bool cache_ok = from_init && ofst && wc < 2;
-              needg |= (kind && !in_w && !cache_ok) ? 1u << sl : 0u;
-              bad |= (kind && comp(dq[c], j) != sv) ? 1u << sl : 0u;
+    }
+    if (MODE & (EVAL_GATES | EVAL_COPIES)) {
+      // ---- the tile's G table (first wave), then gates and copies from it
+      if (tid < 64) build_g_table(L, tile0, n, total_rows, (uint32_t)tid);
+      __syncthreads();
+      if (MODE & EVAL_GATES) half_g_gates(T, A, L, tile0, (uint32_t)tid & 63u, (uint32_t)tid >> 6);
+      if (MODE & EVAL_COPIES) round_copies(A, L, tile0, (uint32_t)tid);
+      // ---- per quad: selector rows the G pass does not take, and init/final-block copies
+      if (gq < total_quads) {
+        const uint32_t pq = reinterpret_cast<const uint8_t*>(L + L_QM)[tid];
+        const bool in_g = pq != 0xffu;
+        if (MODE & EVAL_GATES) {
+          const uint32_t rest = (curfx.y | curfx.z | curfx.w) & 0xffffu;
+          const bool regular = in_g && rest == 0 && (curfx.x & 0xffffu) == L[L_XS + (pq & 15u)];
+          if (!regular) {
+            uint32_t rowmask = ((curfx.x & 0xffffu) ? 1u : 0u) | ((curfx.y & 0xffffu) ? 2u : 0u) |
+                               ((curfx.z & 0xffffu) ? 4u : 0u) | ((curfx.w & 0xffffu) ? 8u : 0u);
+            while (rowmask) {
+              int j = __builtin_ctz(rowmask);
+              rowmask &= rowmask - 1;
+              uint32_t k0 = comp(curfx, j);
+              uint32_t failed;
+              if ((k0 & 0xffffu) == (1u << S_CONST)) failed = T.at(A1, lr0 + j) == (k0 >> 16) ? 0u : 1u << S_CONST;
+              else failed = row_gates(T, k0 & 0xffffu, lr0 + j, comp(cur9, j), k0);
+              if (failed) A.fail_gates(row0 + j, failed);
             }
-          if (needg) {  // a source outside W and the cache: only a corrupted layout gets here
+          }
+        }
+        if ((MODE & EVAL_COPIES) && !in_g && row0 < used_rows) {
+          // the quad's instance: scan the tile's cached offsets (a valid layout never needs
+          // more; offsets_check_kernel flags any other)
+          const uint32_t first = L[L_INFO];
+          const uint64_t* Off = reinterpret_cast<const uint64_t*>(L + L_INFO + 2);
+          uint32_t i = 0;
+          while (i + 2 < NOFF && Off[i + 1] <= row0) i++;
+          const uint64_t o = Off[i], o1 = Off[i + 1];
+          const uint64_t R = o1 - o;
+          if (first + i < n && o1 > row0 && o1 <= total_rows && R >= FIXED_ROWS &&
+              R <= MAX_INSTANCE_ROWS && ((uint32_t)R - FIXED_ROWS) % ROUND_ROWS == 0) {
+            const uint32_t rounds = ((uint32_t)R - FIXED_ROWS) / ROUND_ROWS;
+            const uint64_t ofirst = first < n ? Off[0] : ~0ull;
             const Src src{L + L_W, L + L_IC, adv, total_rows, tile0 - HIST, ofirst};
-            bad &= ~needg;
-            while (needg) {
-              const int sl = __builtin_ctz(needg);
-              needg &= needg - 1;
-              const uint32_t e = L[L_CT + (g * G_QUADS + p) * 12 + sl];
-              const uint32_t kind = e & 3u;
-              const bool msg = kind == 3, st0 = kind == 2 && hr0;
-              const uint32_t init_row = msg ? 32 + 4 * (((e >> 6) & 1u) ? sgy : sgx) + ((e >> 4) & 3u)
-                                            : (e >> 17) & 255u;
-              const uint64_t gs = (msg || st0) ? o + init_row
-                                               : gbase + (uint64_t)(int64_t)((int)((e >> 7) & 1023u) - 512);
-              const uint32_t wc = st0 ? (e >> 25) & 3u : (e >> 2) & 3u;
-              const uint32_t dv = T.at(A3 + sl % 3, lr0 + sl / 3);
-              if (dv != src.at(gs, wc)) bad |= 1u << sl;
-            }
+            const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
+            copies_edge(A, dq, src, o, rounds, (uint32_t)((row0 - o) >> 2));
           }
-          while (bad) {
-            int b = __builtin_ctz(bad);
-            bad &= bad - 1;
-            A.fail(row0 + b / 3, B2F_CODE_COPY);
-          }
-        } else {
-          const Src src{L + L_W, L + L_IC, adv, total_rows, tile0 - HIST, ofirst};
-          const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
-          copies_edge(A, dq, src, o, rounds, lq);
         }
       }
     }
@@ -1457,6 +1491,19 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
     uint64_t fm = *reinterpret_cast<const uint64_t*>(L + L_ACC + 20);
     if (fm != ~0ull) atomicMin((unsigned long long*)&rep->first_failure, (unsigned long long)fm);
   }
+}
+
+// Device-side layout validation for b2f_eval_dev: every instance's rows must be R(rounds) for
+// some rounds and lie inside the trace. The eval kernel relies on it (an invalid layout is an
+// error whatever the counters say; it only has to stay in bounds).
+__global__ void offsets_check_kernel(const uint64_t* __restrict__ off, uint32_t n,
+                                     uint64_t total_rows, int* __restrict__ status) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t o = off[i], o1 = off[i + 1], R = o1 - o;
+  const bool bad = o1 < o || o1 > total_rows || (i == 0 && o != 0) || R < FIXED_ROWS ||
+                   R > MAX_INSTANCE_ROWS || ((uint32_t)R - FIXED_ROWS) % ROUND_ROWS != 0;
+  if (bad) atomicOr(status, 1 << B2F_ERR_LAYOUT);
 }
 
 __global__ void report_init_kernel(b2f_eval_report* rep, uint64_t total_rows) {
@@ -1718,6 +1765,9 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
   HIPCHK(ctx, hipSetDevice(ctx->device));
   HIPCHK(ctx, hipMemsetAsync(ctx->d_status + 1, 0, sizeof(int), s));
   hipLaunchKernelGGL(report_init_kernel, dim3(1), dim3(1), 0, s, d_report, total_rows);
+  HIPCHK(ctx, hipGetLastError());
+  hipLaunchKernelGGL(offsets_check_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                     d_offsets, (uint32_t)n, total_rows, ctx->d_status + 1);
   HIPCHK(ctx, hipGetLastError());
   uint64_t nt = n_tiles_of(total_rows);
   int rc = launch_tile_index(ctx, d_offsets, n, nt, s);
