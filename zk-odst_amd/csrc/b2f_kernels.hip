@@ -606,10 +606,13 @@ constexpr int L_IC = L_INFO + 24;
 constexpr int L_XS = L_IC + 2 * INIT_ROWS;   // expected row-0 selector bits per G quad (16)
 constexpr int L_QSEL = L_XS + 16;
 constexpr int L_A9 = L_QSEL + BLOCK;
-constexpr int L_GT = L_A9 + BLOCK;           // MAX_TILE_G x GT_WORDS
-constexpr int L_QM = L_GT + MAX_TILE_G * GT_WORDS;  // BLOCK bytes
-constexpr int L_NG = L_QM + BLOCK / 4;       // number of G table entries
-constexpr int L_ACC = L_NG + 4;  // 16 gate + lookup + copy counters, first (u64)
+constexpr int L_INFO2 = L_A9 + BLOCK;        // the TileInfo two tiles ahead (t + gridDim)
+// G set: G table (MAX_TILE_G x GT_WORDS), QM (BLOCK bytes), NG (entries); two sets, the one of
+// the current tile and the one being built for the next
+constexpr int GS_GT = 0, GS_QM = MAX_TILE_G * GT_WORDS, GS_NG = GS_QM + BLOCK / 4;
+constexpr int GSET = GS_NG + 4;
+constexpr int L_GS = L_INFO2 + 24;
+constexpr int L_ACC = L_GS + 2 * GSET;  // 16 gate + lookup + copy counters, first (u64)
 constexpr int LDS_WORDS = L_ACC + 20 + 2;
 static_assert(L_INFO % 4 == 0 && L_IC % 4 == 0 && L_G % 4 == 0 && L_CT % 4 == 0 && L_ACC % 2 == 0,
               "aligned carve");
@@ -636,8 +639,9 @@ static_assert(expected_sel_matches_fill(), "eval's canonical selectors = the fil
 constexpr int X_HIST = 4 * (HIST / 4);          // 384: 96 quads x 4 canonical columns
 constexpr int X_HALO = X_HIST + 9 * (HALO_ROWS / 4);  // +36: 4 quads x 9 gate columns
 constexpr int X_INIT = X_HALO + 2 * INIT_QUADS;  // +82: 41 quads x (a_1, a_2)
-constexpr int X_INFO = X_INIT + 6;               // +6: TileInfo
-static_assert(X_INFO <= 2 * BLOCK, "two extra slots per thread");
+constexpr int X_INFO = X_INIT + 5;               // +5: TileInfo words 0..19 (first, off[9])
+constexpr int X_INFO2 = X_INFO + 5;              // +5: the same for tile t + gridDim
+static_assert(X_INFO2 <= 2 * BLOCK, "two extra slots per thread");
 
 // copy-source descriptor (u16): bits 0-1 kind: 0 none, 1 in-G (bits 2-7 row from the G's first
 // row, bits 8-11 column), 2 state word at the half-round start (bits 2-3 role a/b/c/d, bits 4-5
@@ -1078,11 +1082,13 @@ __device__ __forceinline__ uint32_t row_gates(const Tile& T, uint32_t sel, uint3
 // the tile, so its init region is in the window). QM[q] = position of quad q in its G.
 // Instances past the cached eight cannot occur in a valid layout (each is >= 228 rows);
 // b2f_eval_dev flags invalid layouts separately (offsets_check_kernel).
-__device__ __forceinline__ void build_g_table(uint32_t* L, uint64_t tile0, uint32_t n,
-                                              uint64_t total_rows, uint32_t lane) {
-  const uint32_t first = L[L_INFO];
-  const uint64_t* Off = reinterpret_cast<const uint64_t*>(L + L_INFO + 2);
-  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + L_SG);
+__device__ __forceinline__ void build_g_table(uint32_t* S, const uint32_t* info, const uint8_t* Sg,
+                                              uint64_t tile0, uint32_t n, uint64_t total_rows,
+                                              uint32_t lane) {
+  // one wave: its lanes reset QM, then mark their G's quads (LDS order within a wave)
+  S[GS_QM + lane] = 0xffffffffu;
+  const uint32_t first = info[0];
+  const uint64_t* Off = reinterpret_cast<const uint64_t*>(info + 2);
   const int64_t lo = (int64_t)tile0 - (G_ROWS - 1), hi = (int64_t)tile0 + TILE_ROWS - 1;
   uint32_t base = 0, m = 0;
   int64_t o_mine = -1;
@@ -1112,7 +1118,7 @@ __device__ __forceinline__ void build_g_table(uint32_t* L, uint64_t tile0, uint3
     }
     base += cnt;
   }
-  if (lane == 0) L[L_NG] = base < (uint32_t)MAX_TILE_G ? base : (uint32_t)MAX_TILE_G;
+  if (lane == 0) S[GS_NG] = base < (uint32_t)MAX_TILE_G ? base : (uint32_t)MAX_TILE_G;
   if (o_mine < 0 || lane >= (uint32_t)MAX_TILE_G) return;
   const uint32_t r = m >> 3, g = m & 7u;
   const int gl = (int)(o_mine + INIT_ROWS + (int64_t)G_ROWS * m - (int64_t)tile0);
@@ -1121,7 +1127,7 @@ __device__ __forceinline__ void build_g_table(uint32_t* L, uint64_t tile0, uint3
   const int ib0 = ofst ? L_IC : L_W + ob;
   const int ib1 = ofst ? L_IC + (int)INIT_ROWS : L_W + WSTRIDE + ob;
   const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
-  uint32_t* gt = L + L_GT + GT_WORDS * lane;
+  uint32_t* gt = S + GS_GT + GT_WORDS * lane;
   gt[0] = (uint32_t)(gl + HIST - CBIAS);
   gt[1] = (uint32_t)ib0;
   gt[2] = (uint32_t)ib1;
@@ -1129,7 +1135,7 @@ __device__ __forceinline__ void build_g_table(uint32_t* L, uint64_t tile0, uint3
   gt[4] = (uint32_t)(ib0 + 32 + 4 * sg[1]);
   gt[5] = (uint32_t)gl;
   gt[6] = (m < 4 ? 8 + g : g) * G_CHECKS;
-  uint8_t* qm = reinterpret_cast<uint8_t*>(L + L_QM);
+  uint8_t* qm = reinterpret_cast<uint8_t*>(S + GS_QM);
 #pragma unroll
   for (int p = 0; p < (int)G_QUADS; p++) {
     int q = (gl >> 2) + p;
@@ -1146,11 +1152,12 @@ __device__ __forceinline__ void build_g_table(uint32_t* L, uint64_t tile0, uint3
 // exactly the block's and none on rows 1-3 (QSEL, staged). Every other selector row is
 // evaluated by its own quad's lane (row_gates), so each selector row is evaluated once.
 __device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const uint32_t* L,
-                                             uint64_t tile0, uint32_t lane, uint32_t kind) {
-  if (lane >= 2 * L[L_NG]) return;
+                                             const uint32_t* S, uint64_t tile0, uint32_t lane,
+                                             uint32_t kind) {
+  if (lane >= 2 * S[GS_NG]) return;
   const uint32_t h = lane & 1u;
   const int off = kind == 0 ? 0 : kind == 1 ? 4 : kind == 2 ? 12 : 16;
-  const int rl = (int)L[L_GT + GT_WORDS * (lane >> 1) + 5] + 28 * (int)h + off;  // selector row
+  const int rl = (int)S[GS_GT + GT_WORDS * (lane >> 1) + 5] + 28 * (int)h + off;  // selector row
   const uint32_t want = kind == 0 ? 1u << (h ? S_A2 : S_A1)
                       : kind == 1 ? 1u << (h ? S_D2 : S_D1)
                       : kind == 2 ? 1u << (h ? S_C2 : S_C1)
@@ -1171,15 +1178,15 @@ __device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const ui
 // The copy checks of the tile's G's: item it = (G table entry it / 72, check it % 72), spread
 // over all threads. A check belongs to this tile if its operand row does; its source is one
 // LDS read at (per-G base) + C for every valid layout.
-__device__ __forceinline__ void round_copies(EvalAcc& A, const uint32_t* L, uint64_t tile0,
-                                             uint32_t tid) {
-  const uint32_t nchk = L[L_NG] * G_CHECKS;
+__device__ __forceinline__ void round_copies(EvalAcc& A, const uint32_t* L, const uint32_t* S,
+                                             uint64_t tile0, uint32_t tid) {
+  const uint32_t nchk = S[GS_NG] * G_CHECKS;
 #pragma unroll 2
   for (uint32_t k = 0; k < (MAX_TILE_G * G_CHECKS + BLOCK - 1) / BLOCK; k++) {
     const uint32_t it = tid + k * BLOCK;
     if (it >= nchk) break;
     const uint32_t gi = it / G_CHECKS, ci = it - gi * G_CHECKS;
-    const uint32_t* gt = L + L_GT + GT_WORDS * gi;
+    const uint32_t* gt = S + GS_GT + GT_WORDS * gi;
     const uint32_t e = L[L_CT + gt[6] + ci];
     const int dl = (int)gt[5] + (int)((e >> 19) & 63u);
     const int src = (int)gt[(e >> 14) & 7u] + (int)(e & 16383u);
@@ -1272,7 +1279,7 @@ enum { EVAL_LOOKUP = 1, EVAL_GATES = 2, EVAL_COPIES = 4, EVAL_FULL = 7, EVAL_TOU
 
 // The two extra (non-own-quad) loads a thread issues per tile, as a compact descriptor:
 // kind, LDS destination, and a base pointer the tile position is added to.
-enum { XK_NONE = 0, XK_HIST, XK_HALO, XK_INIT, XK_INFO };
+enum { XK_NONE = 0, XK_HIST, XK_HALO, XK_INIT, XK_INFO, XK_INFO2 };
 struct Extra {
   const uint32_t* base;  // HIST/HALO: + tile0 rows; INIT: + off[first]; INFO: + 24 t words
   uint32_t lds;          // LDS word offset of the 16-byte destination
@@ -1305,6 +1312,10 @@ __device__ __forceinline__ Extra make_extra(int slot, const uint32_t* adv, uint6
     x.kind = XK_INFO;
     x.base = reinterpret_cast<const uint32_t*>(tinfo) + 4 * (slot - X_INIT);
     x.lds = L_INFO + 4 * (slot - X_INIT);
+  } else if (slot < X_INFO2) {
+    x.kind = XK_INFO2;
+    x.base = reinterpret_cast<const uint32_t*>(tinfo) + 4 * (slot - X_INFO);
+    x.lds = L_INFO2 + 4 * (slot - X_INFO);
   } else {
     x.kind = XK_NONE;
     x.base = adv;
@@ -1313,25 +1324,22 @@ __device__ __forceinline__ Extra make_extra(int slot, const uint32_t* adv, uint6
   return x;
 }
 
-// fo = {first, -, off[first] lo, hi} of tile t (only INIT slots read it)
+// fo = {first, -, off[first] lo, hi} of tile t (only INIT slots read it). One predicated
+// 16-byte load whatever the slot kind (a switch around the loads serialises their issue).
 __device__ __forceinline__ uint4 extra_load(const Extra& x, uint64_t t, const uint4& fo, uint32_t n,
-                                            uint64_t total_rows, uint64_t total_quads) {
-  const uint4 z = make_uint4(0, 0, 0, 0);
+                                            uint64_t total_rows, uint64_t total_quads,
+                                            uint64_t G, uint64_t n_tiles) {
   const uint64_t tile0 = t * TILE_ROWS;
-  switch (x.kind) {
-    case XK_HIST:
-      return tile0 >= (uint64_t)HIST ? *reinterpret_cast<const uint4*>(x.base + tile0) : z;
-    case XK_HALO:
-      return (t + 1) * BLOCK + x.q < total_quads ? *reinterpret_cast<const uint4*>(x.base + tile0) : z;
-    case XK_INIT: {
-      uint64_t of = ((uint64_t)fo.w << 32) | fo.z;
-      return (fo.x < n && of + INIT_ROWS <= total_rows) ? *reinterpret_cast<const uint4*>(x.base + of) : z;
-    }
-    case XK_INFO:
-      return *reinterpret_cast<const uint4*>(x.base + 24 * t);
-    default:
-      return z;
-  }
+  const uint64_t of = ((uint64_t)fo.w << 32) | fo.z;
+  const uint32_t k = x.kind;
+  const uint64_t w = k == XK_INIT ? of : k == XK_INFO ? 24 * t : k == XK_INFO2 ? 24 * (t + G) : tile0;
+  const bool ok = k == XK_HIST    ? tile0 >= (uint64_t)HIST
+                : k == XK_HALO    ? (t + 1) * BLOCK + x.q < total_quads
+                : k == XK_INIT    ? fo.x < n && of + INIT_ROWS <= total_rows
+                : k == XK_INFO    ? true
+                : k == XK_INFO2   ? t + G < n_tiles
+                                  : false;
+  return ok ? *reinterpret_cast<const uint4*>(x.base + w) : make_uint4(0, 0, 0, 0);
 }
 
 template <int MODE>
@@ -1381,15 +1389,15 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
       q[c] = gq < total_quads
                  ? *reinterpret_cast<const uint4*>((c < 10 ? adv + (uint64_t)c * total_rows : fixed) + 4 * gq)
                  : make_uint4(0, 0, 0, 0);
-    x0 = extra_load(e0, tt, f, n, total_rows, total_quads);
-    x1 = extra_load(e1, tt, f, n, total_rows, total_quads);
+    x0 = extra_load(e0, tt, f, n, total_rows, total_quads, G, n_tiles);
+    x1 = extra_load(e1, tt, f, n, total_rows, total_quads, G, n_tiles);
   };
   if (layout_ok && t < n_tiles) {
     fo = *reinterpret_cast<const uint4*>(tinfo + t);
     load_tile(t, fo);
     if (t + G < n_tiles) fo_next = *reinterpret_cast<const uint4*>(tinfo + t + G);
   }
-  for (; layout_ok && t < n_tiles; t += G) {
+  for (uint32_t iter = 0; layout_ok && t < n_tiles; t += G, iter++) {
     // ---- stage tile t: registers -> LDS
 #pragma unroll
     for (int c = 0; c < 9; c++) *reinterpret_cast<uint4*>(&L[lds_cell(c, 4 * tid)]) = q[c];
@@ -1397,7 +1405,6 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
     if (MODE & (EVAL_GATES | EVAL_COPIES)) {
       L[L_QSEL + tid] = (curfx.x & 0xffffu) | (((curfx.y | curfx.z | curfx.w) & 0xffffu) ? 1u << 16 : 0u);
       L[L_A9 + tid] = cur9.x;
-      if (tid < BLOCK / 4) L[L_QM + tid] = 0xffffffffu;
     }
     if (e0.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e0.lds]) = x0;
     if (e1.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e1.lds]) = x1;
@@ -1429,14 +1436,21 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
       }
     }
     if (MODE & (EVAL_GATES | EVAL_COPIES)) {
-      // ---- the tile's G table (first wave), then gates and copies from it
-      if (tid < 64) build_g_table(L, tile0, n, total_rows, (uint32_t)tid);
-      __syncthreads();
-      if (MODE & EVAL_GATES) half_g_gates(T, A, L, tile0, (uint32_t)tid & 63u, (uint32_t)tid >> 6);
-      if (MODE & EVAL_COPIES) round_copies(A, L, tile0, (uint32_t)tid);
+      // ---- G tables: the first wave builds the next tile's (from INFO2) while this tile is
+      // checked with the one built during the previous iteration
+      const uint32_t* S = L + L_GS + (iter & 1) * GSET;
+      uint32_t* Sn = L + L_GS + ((iter + 1) & 1) * GSET;
+      if (iter == 0) {  // nothing was built ahead for the first tile
+        if (tid < 64) build_g_table(L + L_GS, L + L_INFO, Sg, tile0, n, total_rows, (uint32_t)tid);
+        __syncthreads();
+      }
+      if (tid < 64) build_g_table(Sn, L + L_INFO2, Sg, (t + G) * TILE_ROWS, t + G < n_tiles ? n : 0,
+                                  total_rows, (uint32_t)tid);
+      if (MODE & EVAL_GATES) half_g_gates(T, A, L, S, tile0, (uint32_t)tid & 63u, (uint32_t)tid >> 6);
+      if (MODE & EVAL_COPIES) round_copies(A, L, S, tile0, (uint32_t)tid);
       // ---- per quad: selector rows the G pass does not take, and init/final-block copies
       if (gq < total_quads) {
-        const uint32_t pq = reinterpret_cast<const uint8_t*>(L + L_QM)[tid];
+        const uint32_t pq = reinterpret_cast<const uint8_t*>(S + GS_QM)[tid];
         const bool in_g = pq != 0xffu;
         if (MODE & EVAL_GATES) {
           const uint32_t rest = (curfx.y | curfx.z | curfx.w) & 0xffffu;
