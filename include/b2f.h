@@ -118,6 +118,22 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
                          const uint64_t* d_offsets, size_t n, uint64_t total_rows,
                          b2f_eval_report* d_report, void* stream);
 
+/* Fused witness fill + constraint evaluation, device pointers: the same trace, h' and
+ * verdict as b2f_fill_dev followed by b2f_eval_dev on that trace (MockProver::run then
+ * ::verify, blake2f.rs:301-302), in one pass: every cell is checked while it is still on the
+ * CU, so the trace is written once and never read back. Arguments as b2f_fill_dev plus the
+ * report (overwritten). Asynchronous on `stream`. */
+B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
+                              const uint64_t* d_offsets, uint64_t total_rows, uint32_t* d_advice,
+                              uint32_t* d_fixed, uint64_t* d_h_out, b2f_eval_report* d_report,
+                              void* stream);
+
+/* Test hook for the fused path: XOR `mask` into cell (row, col) as b2f_fill_eval_dev assigns
+ * it (col 0..9 = a_col, 10 = the fixed column), so both the trace it writes and the trace it
+ * checks carry the fault; row = UINT64_MAX turns it off (the default). Lets tests prove the
+ * fused verdict equals b2f_eval_dev's / the oracle's on the trace actually written. */
+B2F_API int b2f_debug_inject(b2f_ctx* ctx, uint64_t row, uint32_t col, uint32_t mask);
+
 /* Wait for `stream` and return the first device-side error of the fill/eval calls issued
  * since the previous b2f_sync (B2F_ERR_LAYOUT / B2F_ERR_ROUNDS), then clear it. */
 B2F_API int b2f_sync(b2f_ctx* ctx, void* stream);
@@ -155,7 +171,8 @@ B2F_API int b2f_export_fp_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t t
 #define B2F_KERNEL_FILL 1   /* trace expansion (fill, part 2) */
 #define B2F_KERNEL_EVAL 2   /* constraint evaluation */
 #define B2F_KERNEL_EXPORT 3 /* Fp export */
-#define B2F_NUM_KERNELS 4
+#define B2F_KERNEL_FILL_EVAL 4 /* fused trace expansion + constraint evaluation */
+#define B2F_NUM_KERNELS 5
 B2F_API int b2f_set_timing(b2f_ctx* ctx, int enable);
 B2F_API int b2f_kernel_times(b2f_ctx* ctx, double* total_ms, uint32_t* count);
 

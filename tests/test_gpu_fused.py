@@ -1,0 +1,197 @@
+"""GPU parity of the fused fill + eval path (b2f_fill_eval_dev, csrc/b2f_fused.hip).
+
+The fused kernel must produce exactly what b2f_fill_dev followed by b2f_eval_dev produce --
+the trace, h' and the MockProver verdict -- and therefore what the CPU oracle produces. Fault
+injection (b2f_debug_inject) flips one cell as the fused kernel assigns it; the trace it writes
+then differs from the clean one in exactly that cell, and its verdict must equal the verdict
+of b2f_eval_dev and of the oracle on that written trace. Faults are placed on the places the
+fused kernel's tiling makes special: the 16 rows either side of every tile boundary (carried
+quads, deferred gates), band starts (recomputed history) and the last rows of the trace (zero
+halo). Every test here needs an MI355X (`-m gpu`)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import random_inputs
+
+pytestmark = pytest.mark.gpu
+
+NONE = 2**64 - 1
+
+
+def _as_oracle(x, orc):
+    return np.frombuffer(x.tobytes(), dtype=orc.INPUT_DTYPE).copy()
+
+
+def _stream():
+    import torch
+
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _fused(engine, x, band, total_rows=None, inject=None):
+    """One b2f_fill_eval_dev call on a fresh DeviceBatch (buffers poisoned first)."""
+    import b2f
+
+    os.environ["B2F_BAND"] = str(band)
+    try:
+        batch = b2f.DeviceBatch(x, total_rows=total_rows)
+        batch.advice.fill_(-1)
+        batch.fixed.fill_(-1)
+        if inject is not None:
+            engine.debug_inject(*inject)
+        batch.fill_evaluate(engine)
+        engine.sync(_stream())
+    finally:
+        engine.debug_inject(None)
+        os.environ.pop("B2F_BAND", None)
+    return batch
+
+
+@pytest.mark.parametrize("band", [1, 2, 3, 16])
+@pytest.mark.parametrize("rounds_choices,n,seed", [((12,), 23, 31), ((0, 1, 4, 12, 13), 71, 32),
+                                                   ((1,), 200, 33)])
+def test_fused_equals_oracle(engine, orc, band, rounds_choices, n, seed):
+    x = random_inputs(n, rounds_choices, seed)
+    batch = _fused(engine, x, band)
+    adv, fixed = batch.host_trace()
+    oadv, ofixed, oh, ooff = orc.fill(_as_oracle(x, orc))
+    for c in range(10):
+        bad = np.nonzero(adv[c] != oadv[c])[0]
+        assert bad.size == 0, "a_%d differs at rows %s" % (c, bad[:10])
+    assert np.array_equal(fixed, ofixed)
+    assert np.array_equal(batch.host_h_out(), oh)
+    rep = batch.report_dict()
+    assert rep == orc.evaluate(adv, fixed, ooff)
+    assert rep["first_failure"] == NONE and rep["rows_checked"] == int(ooff[-1])
+
+
+def test_fused_padded_tail(engine, orc):
+    """total_rows past the batch (not a multiple of the 1024-row tile): zero rows, clean."""
+    import b2f
+
+    x = random_inputs(9, (1, 4), 34)
+    total = int(b2f.offsets(x)[-1]) + 1028
+    batch = _fused(engine, x, 2, total_rows=total)
+    adv, fixed = batch.host_trace()
+    used = batch.used_rows
+    assert not adv[:, used:].any() and not fixed[used:].any()
+    rep = batch.report_dict()
+    assert rep == orc.evaluate(adv, fixed, batch.offsets_host) and rep["first_failure"] == NONE
+
+
+def _boundary_rows(total, rng, k):
+    """Rows on both sides of tile boundaries, the first/last rows, and random rows."""
+    rows = set()
+    for t in range(1, (total + 1023) // 1024):
+        for d in (-16, -13, -12, -9, -5, -4, -1, 0, 1, 3, 4, 11, 15):
+            r = 1024 * t + d
+            if 0 <= r < total:
+                rows.add(r)
+    rows.update([0, 1, 2, 3, total - 1, total - 2, total - 4, total - 8, total - 12])
+    rows = sorted(rows)
+    pick = list(rng.choice(rows, size=min(k, len(rows)), replace=False))
+    pick += list(rng.integers(0, total, k // 4))
+    return [int(r) for r in pick]
+
+
+@pytest.mark.parametrize("band", [1, 3, 16])
+def test_fused_injection_matches_eval(engine, orc, band):
+    """Fused verdict == b2f_eval_dev verdict on the trace the fused kernel wrote, for single
+    cell faults in every column (advice and fixed) at tile/band boundaries; the written trace
+    differs from the clean one in exactly the injected cell; a subset is checked against the
+    oracle too."""
+    import torch
+
+    rng = np.random.default_rng(40 + band)
+    x = random_inputs(24, (0, 1, 4, 12), 41)
+    clean = _fused(engine, x, band)
+    cadv, cfix = clean.advice.clone(), clean.fixed.clone()
+    total = clean.total_rows
+    flagged = 0
+    cases = 0
+    for r in _boundary_rows(total, rng, 96):
+        for col in rng.choice(11, size=2, replace=False):
+            col = int(col)
+            bit = int(rng.integers(0, 16 if col == 10 and rng.random() < 0.7 else 32))
+            batch = _fused(engine, x, band, inject=(r, col, 1 << bit))
+            dadv = (batch.advice != cadv).nonzero().cpu().numpy()
+            dfix = (batch.fixed != cfix).nonzero().cpu().numpy()
+            if col < 10:
+                assert dadv.tolist() == [[col, r]] and dfix.size == 0, (r, col, bit)
+            else:
+                assert dadv.size == 0 and dfix.reshape(-1).tolist() == [r], (r, col, bit)
+            got = batch.report_dict()
+            batch.evaluate(engine)  # the standalone eval on the written trace
+            engine.sync(_stream())
+            ref = batch.report_dict()
+            assert got == ref, (r, col, bit, got, ref)
+            if cases % 8 == 0:
+                adv, fixed = batch.host_trace()
+                assert got == orc.evaluate(adv, fixed, batch.offsets_host), (r, col, bit)
+            flagged += got["first_failure"] != NONE
+            cases += 1
+            del batch
+            torch.cuda.empty_cache()
+    assert flagged > cases // 3
+
+
+def test_fused_injection_last_rows(engine, orc):
+    """Selector bits injected into the last rows of the trace: gates that run past the end
+    read zero rows (the eval's out-of-trace rule) -- through the fused kernel's zero halo."""
+    import b2f
+
+    x = random_inputs(5, (1,), 42)
+    total = int(b2f.offsets(x)[-1])
+    total_p = ((total + 1023) // 1024) * 1024  # trace ends exactly on a tile boundary
+    for total_rows in (total, total_p):
+        for r in (total_rows - 1, total_rows - 3, total_rows - 7, total_rows - 12):
+            for bit in (0, 1, 4, 6, 8, 11, 13, 15):
+                batch = _fused(engine, x, 2, total_rows=total_rows, inject=(r, 10, 1 << bit))
+                got = batch.report_dict()
+                adv, fixed = batch.host_trace()
+                assert got == orc.evaluate(adv, fixed, batch.offsets_host), (total_rows, r, bit)
+
+
+def test_fused_2p16_equals_fill_eval(engine):
+    """BASELINE config 2 size: the fused trace, h' and verdict equal fill_dev + eval_dev's
+    (compared on the device; fill_dev itself is diffed against the oracle at this size in
+    test_gpu_parity.test_device_batch_2p16_bitexact)."""
+    import b2f
+    import torch
+
+    from b2f import synth
+
+    x = synth.batch(1 << 16, rounds=12)
+    a = b2f.DeviceBatch(x)
+    a.fill(engine)
+    a.evaluate(engine)
+    engine.sync(_stream())
+    ra = a.report_dict()
+    b = _fused(engine, x, 16)
+    assert torch.equal(a.advice, b.advice) and torch.equal(a.fixed, b.fixed)
+    assert torch.equal(a.h_out, b.h_out)
+    assert b.report_dict() == ra and ra["first_failure"] == NONE
+
+
+def test_fused_mixed_rounds_2p14(engine, orc):
+    """BASELINE config 5 shape (rounds in {1, 4, 12}) at 2^14, oracle-checked in chunks."""
+    import b2f
+    from b2f import synth
+
+    n = 1 << 14
+    x = synth.batch(n, rounds_mix=[1, 4, 12])
+    batch = _fused(engine, x, 16)
+    rep = batch.report_dict()
+    assert rep["first_failure"] == NONE and sum(rep["gate_failures"]) == 0
+    off = batch.offsets_host
+    h_out = batch.host_h_out()
+    for s in range(0, n, 4096):
+        e = min(n, s + 4096)
+        oadv, ofixed, oh, _ = orc.fill(_as_oracle(x[s:e], orc))
+        r0, r1 = int(off[s]), int(off[e])
+        assert np.array_equal(batch.advice[:, r0:r1].cpu().numpy().view(np.uint32), oadv)
+        assert np.array_equal(batch.fixed[r0:r1].cpu().numpy().view(np.uint32), ofixed)
+        assert np.array_equal(h_out[s:e], oh)
+    del b2f

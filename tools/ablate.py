@@ -15,6 +15,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--fill-modes", default="3,2,1,0")
     ap.add_argument("--eval-modes", default="7,8,2,4")
+    ap.add_argument("--bands", default="", help="fused fill+eval band sizes to time (B2F_BAND)")
+    ap.add_argument("--fused-modes", default="", help="fused kernel variants (B2F_DIAG_FUSED)")
     args = ap.parse_args()
     import torch
 
@@ -46,6 +48,20 @@ def main():
             t = eng.kernel_times()["eval"][0]
             res.setdefault("eval%s" % m, []).append(t)
         os.environ.pop("B2F_DIAG_EVAL")
+        for b in [v for v in args.bands.split(",") if v]:
+            os.environ["B2F_BAND"] = b
+            eng.set_timing(True)
+            batch.fill_evaluate(eng, s)
+            t = eng.kernel_times()["fill_eval"][0]
+            res.setdefault("fused%s" % b, []).append(t)
+        os.environ.pop("B2F_BAND", None)
+        for m in [v for v in args.fused_modes.split(",") if v]:
+            os.environ["B2F_DIAG_FUSED"] = m
+            eng.set_timing(True)
+            batch.fill_evaluate(eng, s)
+            t = eng.kernel_times()["fill_eval"][0]
+            res.setdefault("fmode%s" % m, []).append(t)
+        os.environ.pop("B2F_DIAG_FUSED", None)
     for k, v in res.items():
         best = min(v)
         print("%-6s min %8.3f ms  (%6.0f GB/s)  all %s" % (k, best, nbytes / best / 1e6,

@@ -9,7 +9,7 @@ agg = collections.OrderedDict()
 for f in sorted(glob.glob(root + "/*/p_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "fill_kernel" not in k and "eval_kernel" not in k:
+        if "fill_kernel" not in k and "eval_kernel" not in k and "fused_kernel" not in k:
             continue
         name = k.split("(")[0].split("::")[-1]
         mode = k.split("<")[1].split(">")[0] if "<" in k else ""

@@ -76,6 +76,19 @@ class Engine:
         self._check(self.lib.b2f_eval_dev(self.ctx, _vp(d_adv), _vp(d_fixed), _vp(d_off), n,
                                           int(total_rows), _vp(d_report), _vp(stream)))
 
+    def fill_eval_dev(self, d_in, n, d_off, total_rows, d_adv, d_fixed, d_h_out, d_report,
+                      stream=0):
+        self._check(self.lib.b2f_fill_eval_dev(self.ctx, _vp(d_in), n, _vp(d_off),
+                                               int(total_rows), _vp(d_adv), _vp(d_fixed),
+                                               _vp(d_h_out) if d_h_out else None,
+                                               _vp(d_report), _vp(stream)))
+
+    def debug_inject(self, row=None, col=0, mask=0):
+        """Test hook: XOR `mask` into cell (row, col) (col 10 = fixed) as the fused path assigns
+        it; row=None turns it off."""
+        r = 2**64 - 1 if row is None else int(row)
+        self._check(self.lib.b2f_debug_inject(self.ctx, r, int(col), int(mask) & 0xffffffff))
+
     def export_fp_dev(self, d_adv, total_rows, row_begin, nrows, form, d_out, out_rows,
                       stream=0):
         self._check(self.lib.b2f_export_fp_dev(self.ctx, _vp(d_adv), int(total_rows),
@@ -132,6 +145,13 @@ class DeviceBatch:
         s = stream if stream is not None else self.torch.cuda.current_stream().cuda_stream
         eng.eval_dev(self.advice.data_ptr(), self.fixed.data_ptr(), self.offsets.data_ptr(),
                      self.n, self.total_rows, self.report.data_ptr(), s)
+
+    def fill_evaluate(self, eng, stream=None):
+        """Fused fill + eval (b2f_fill_eval_dev): trace, h' and report in one pass."""
+        s = stream if stream is not None else self.torch.cuda.current_stream().cuda_stream
+        eng.fill_eval_dev(self.inputs.data_ptr(), self.n, self.offsets.data_ptr(),
+                          self.total_rows, self.advice.data_ptr(), self.fixed.data_ptr(),
+                          self.h_out.data_ptr(), self.report.data_ptr(), s)
 
     def export_fp(self, eng, row_begin=0, nrows=None, form=_lib.FP_MONTGOMERY, out=None,
                   stream=None):
