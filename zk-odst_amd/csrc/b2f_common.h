@@ -486,6 +486,7 @@ constexpr uint32_t wc_of(uint32_t col) { return col == A1 ? 0 : col == A2 ? 1 : 
 // rot 16), whose index is fixed by g, so rel is a constant of (g, role, limb).
 constexpr int CBIAS = 512;
 constexpr int G_CHECKS = 72;  // copy constraints per G (check_table_ok)
+constexpr int GT_WORDS_ = 8;  // words per G table entry
 struct CheckTable {
   uint32_t e[12][G_CHECKS];
 };
@@ -802,6 +803,126 @@ __device__ __forceinline__ uint32_t g_xor63(const Tile& T, uint32_t r, uint32_t 
     ijkl &= (uint64_t)T.at(A8, r + b) == (uint64_t)zp + 4 * (uint64_t)a2[b];
   }
   return ((b2 ? 0u : 1u << S_B2) | (ijkl ? 0u : 1u << S_IJKL)) & sel;
+}
+
+// ---------------------------------------------------------------- per-tile G pass and copies
+// Shared by eval_kernel (check rows = selector rows / operand rows in [0, 1024) of the tile)
+// and fused_kernel (u coordinates: a block is checked where its last row lands, u in
+// [16, 1040); operand rows in [16, 1040)). A G table entry is GT_WORDS words: 0 window base -
+// CBIAS, 1/2 init-region a_1/a_2 bases, 3/4 message x/y row bases, 5 G start (tile-local),
+// 6 check-table row.
+struct GCarve {
+  int qsel, a9;     // LDS: per-quad row-0 selector word | rest flag, row-0 a_9
+  int ct;           // LDS: copy-check table
+  int g, ts;        // LDS: gate columns a_0 a_3 a_4 a_5 a_6, stride
+  int lo, hi;       // check-row range (tile-local)
+  bool last_rule;   // fused: a block belongs to the tile holding its last row
+};
+
+// One limb k of an XOR24 (b1 + efgh) or XOR63 (b2 + ijkl) block: bit 0 = the spread-XOR
+// identity of limb k fails, bit 1 = the re-split identity of limb k fails. The block's gate
+// fails iff some limb's bit is set (the polynomials of LAYOUT.md §4 are per-limb conjunctions).
+template <class Tile>
+__device__ __forceinline__ uint32_t g_xor24_limb(const Tile& T, uint32_t r, uint32_t k) {
+  const uint32_t b = r + 3 * k, k1 = r + 3 * ((k + 1) & 3u), k2 = r + 3 * ((k + 2) & 3u);
+  const bool b1 = (uint64_t)T.at(A3, b) + T.at(A4, b) ==
+                      (uint64_t)T.at(A2, b) + ((uint64_t)T.at(A2, b + 1) << 16) + 2 * (uint64_t)T.at(A2, b + 2) &&
+                  (T.at(A0, b) | T.at(A0, b + 1)) == 0u;
+  const bool efgh = (uint64_t)T.at(A7, b) == (uint64_t)T.at(A1, k1 + 1) + ((uint64_t)T.at(A1, k2) << 8) &&
+                    (uint64_t)T.at(A8, b) == (uint64_t)T.at(A2, k1 + 1) + ((uint64_t)T.at(A2, k2) << 16);
+  return (b1 ? 0u : 1u) | (efgh ? 0u : 2u);
+}
+template <class Tile>
+__device__ __forceinline__ uint32_t g_xor63_limb(const Tile& T, uint32_t r, uint32_t k) {
+  const uint32_t b = r + 2 * k, p = r + 2 * ((k + 3) & 3u);
+  const uint32_t zb = T.at(A6, b), zp = T.at(A6, p), s0 = T.at(A2, b);
+  const bool b2 = (uint64_t)T.at(A3, b) + T.at(A4, b) ==
+                      (uint64_t)s0 + ((uint64_t)zb << 30) + 2 * (uint64_t)T.at(A2, b + 1) &&
+                  T.at(A0, b) <= 1u && zb <= 1u;
+  const bool ijkl = (uint64_t)T.at(A7, b) == (uint64_t)zp + 2 * (uint64_t)T.at(A1, b) &&
+                    (uint64_t)T.at(A8, b) == (uint64_t)zp + 4 * (uint64_t)s0;
+  return (b2 ? 0u : 1u) | (ijkl ? 0u : 2u);
+}
+
+// OR of v over the four lanes of a DPP quad (lanes 4i .. 4i + 3); every lane must be active.
+__device__ __forceinline__ uint32_t quad_or(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+  return v;
+}
+
+// Canonical round blocks of the tile's G's, one block kind per wave so that every wave runs a
+// single evaluator: wave 0 the four adds (a1 c1 a2 c2, a lane per block), wave 1 the two XORs
+// (d1 d2, a lane per block), wave 2 XOR24 (b1) and wave 3 XOR63 (b2) with the four limbs of a
+// block on the four lanes of a DPP quad, combined before the block is reported. A block is
+// taken only if its quad carries exactly the canonical selectors (QSEL); every other selector
+// row goes through the per-quad path.
+template <class Tile>
+__device__ __forceinline__ void g_pass(const Tile& T, EvalAcc& A, const uint32_t* L,
+                                       const uint32_t* gt_base, uint32_t ng, int64_t row_base,
+                                       uint32_t lane, uint32_t wave, const GCarve& C) {
+  const uint32_t per_g = wave == 1 ? 2u : 4u;
+  const uint32_t items = per_g * ng;
+#pragma unroll 1
+  for (uint32_t it0 = 0; it0 < items; it0 += 64) {  // uniform trip count (DPP below)
+    const uint32_t it = it0 + lane;
+    const uint32_t g = wave == 1 ? it >> 1 : it >> 2;
+    const uint32_t w = wave == 1 ? it & 1u : it & 3u;  // waves 2, 3: w = limb
+    // wave 0: a1 +0, c1 +12, a2 +28, c2 +40; wave 1: d1 +4, d2 +32; b1 +16; b2 +44
+    const int off = wave == 0 ? (w == 0 ? 0 : w == 1 ? 12 : w == 2 ? 28 : 40)
+                  : wave == 1 ? (w ? 32 : 4) : wave == 2 ? 16 : 44;
+    const int len = wave == 0 ? 4 : wave == 2 ? 12 : 8;
+    const uint32_t want = wave == 0 ? 1u << (w == 0 ? S_A1 : w == 1 ? S_C1 : w == 2 ? S_A2 : S_C2)
+                        : wave == 1 ? 1u << (w ? S_D2 : S_D1)
+                        : wave == 2 ? (1u << S_B1) | (1u << S_EFGH) : (1u << S_B2) | (1u << S_IJKL);
+    const int rl = it < items ? (int)gt_base[GT_WORDS_ * g + 5] + off : -1;
+    const int key = C.last_rule ? rl + len - 1 : rl;
+    const bool take = rl >= 0 && key >= C.lo && key < C.hi && L[C.qsel + (rl >> 2)] == want;
+    const uint32_t r = (uint32_t)rl;
+    uint32_t f = 0;
+    if (wave >= 2) {
+      uint32_t bits = 0;
+      if (take) bits = wave == 2 ? g_xor24_limb(T, r, w) : g_xor63_limb(T, r, w);
+      bits = quad_or(bits);
+      if (take && w == 0 && bits)
+        f = ((bits & 1u) ? 1u << (wave == 2 ? S_B1 : S_B2) : 0u) |
+            ((bits & 2u) ? 1u << (wave == 2 ? S_EFGH : S_IJKL) : 0u);
+    } else if (take) {
+      f = (wave == 0 ? g_add(T, r, L[C.a9 + (r >> 2)], (w & 1u) == 0) : g_xor(T, r, false)) ? 0u : want;
+    }
+    if (f) A.fail_gates((uint64_t)(row_base + rl), f);
+  }
+}
+
+// The 72 copy checks of every G of the tile: LPG lanes per G table entry, each reading the
+// entry once and then issuing its checks' LDS reads independently (source cell at per-G base
+// + table offset, operand cell at its row). A check belongs to the tile holding its operand row.
+constexpr int LPG = 10;
+#ifndef B2F_GT_WAVE
+#define B2F_GT_WAVE 1
+#endif
+constexpr int GT_WAVE = B2F_GT_WAVE;  // wave that builds the next tile's G table (g_pass: XOR)
+__device__ __forceinline__ void g_copies(EvalAcc& A, const uint32_t* L, const uint32_t* gt_base,
+                                         uint32_t ng, int64_t row_base, uint32_t tid,
+                                         const GCarve& C) {
+  const uint32_t gi = tid / LPG, c0 = tid - gi * LPG;
+  if (gi >= ng) return;
+  const uint4 g0 = *reinterpret_cast<const uint4*>(gt_base + GT_WORDS_ * gi);
+  const uint4 g1 = *reinterpret_cast<const uint4*>(gt_base + GT_WORDS_ * gi + 4);
+#pragma unroll 4
+  for (int j = 0; j < (G_CHECKS + LPG - 1) / LPG; j++) {
+    const uint32_t ci = c0 + LPG * j;
+    if (ci >= (uint32_t)G_CHECKS) break;
+    const uint32_t e = L[C.ct + g1.z + ci];
+    const uint32_t sel = (e >> 14) & 7u;
+    const uint32_t base = sel == 0 ? g0.x : sel == 1 ? g0.y : sel == 2 ? g0.z : sel == 3 ? g0.w : g1.x;
+    const int src = (int)base + (int)(e & 16383u);
+    const int dl = (int)g1.y + (int)((e >> 19) & 63u);
+    const uint32_t sv = L[src < 0 ? 0 : src];  // < 0 only for checks outside the tile
+    const int dlc = dl < C.lo ? C.lo : (dl >= C.hi ? C.hi - 1 : dl);
+    const uint32_t dv = L[C.g + (1 + ((e >> 17) & 3u)) * C.ts + dlc];
+    if (dl >= C.lo && dl < C.hi && dv != sv) A.fail((uint64_t)(row_base + dl), B2F_CODE_COPY);
+  }
 }
 
 // Any selector combination, one gate at a time (kept out of line: the hot path never takes it

@@ -71,6 +71,7 @@ static_assert(F_INFO % 4 == 0 && F_IV % 2 == 0 && F_IC % 4 == 0 && (F_IC + INIT_
               "aligned carve");
 static_assert((F_WORDS + G_QUADS * 4) * 4 * 3 <= 160 * 1024, "three fused workgroups per CU");
 static_assert(check_table_ok<F_W, F_WS>(), "72 copy checks per G, fields in range");
+static_assert(F_GT_WORDS == GT_WORDS_ && F_MAX_G * LPG <= BLOCK, "G table layout / copy lanes");
 
 __constant__ __attribute__((aligned(16))) CheckTable c_fchecks = make_check_table<F_W, F_WS>();
 using FTile = TileT<F_W, F_WS, F_G, F_TS>;
@@ -322,55 +323,6 @@ __device__ __forceinline__ void build_g_table_f(uint32_t* S, const uint32_t* inf
   }
 }
 
-// Canonical round blocks whose last row is a check row (u in [16, 1040)); wave w checks block
-// kind w of item (G, half) = lane (the eval's half_g_gates).
-__device__ __forceinline__ void half_g_gates_f(const FTile& T, EvalAcc& A, const uint32_t* L,
-                                               const uint32_t* S, int64_t base0, uint32_t lane,
-                                               uint32_t kind) {
-  if (lane >= 2 * S[FS_NG]) return;
-  const uint32_t h = lane & 1u;
-  const int off = kind == 0 ? 0 : kind == 1 ? 4 : kind == 2 ? 12 : 16;
-  const int rl = (int)S[FS_GT + F_GT_WORDS * (lane >> 1) + 5] + 28 * (int)h + off;
-  const int len = (kind == 0 || kind == 2) ? 4 : (kind == 1 || h) ? 8 : 12;
-  const int last = rl + len - 1;
-  if (last < SHIFT || last >= U_END) return;
-  const uint32_t want = kind == 0 ? 1u << (h ? S_A2 : S_A1)
-                      : kind == 1 ? 1u << (h ? S_D2 : S_D1)
-                      : kind == 2 ? 1u << (h ? S_C2 : S_C1)
-                      : h ? (1u << S_B2) | (1u << S_IJKL) : (1u << S_B1) | (1u << S_EFGH);
-  if (L[F_QSEL + (rl >> 2)] != want) return;
-  const uint32_t r = (uint32_t)rl;
-  uint32_t f;
-  if (kind == 0 || kind == 2) {
-    f = g_add(T, r, L[F_A9 + (r >> 2)], kind == 0) ? 0u : want;
-  } else if (kind == 1) {
-    f = g_xor(T, r, false) ? 0u : want;
-  } else {
-    f = h ? g_xor63(T, r, want) : g_xor24(T, r, want);
-  }
-  if (f) A.fail_gates((uint64_t)(base0 + rl), f);
-}
-
-// The copy checks of the tile's G's whose operand row is a check row.
-__device__ __forceinline__ void round_copies_f(EvalAcc& A, const uint32_t* L, const uint32_t* S,
-                                               int64_t base0, uint32_t tid) {
-  const uint32_t nchk = S[FS_NG] * G_CHECKS;
-#pragma unroll 2
-  for (uint32_t k = 0; k < (F_MAX_G * G_CHECKS + BLOCK - 1) / BLOCK; k++) {
-    const uint32_t it = tid + k * BLOCK;
-    if (it >= nchk) break;
-    const uint32_t gi = it / G_CHECKS, ci = it - gi * G_CHECKS;
-    const uint32_t* gt = S + FS_GT + F_GT_WORDS * gi;
-    const uint32_t e = L[F_CT + gt[6] + ci];
-    const int dl = (int)gt[5] + (int)((e >> 19) & 63u);
-    const int src = (int)gt[(e >> 14) & 7u] + (int)(e & 16383u);
-    const uint32_t sv = L[src < 0 ? 0 : src];  // < 0 only for checks outside the check rows
-    const int dlc = dl < SHIFT ? SHIFT : (dl >= U_END ? U_END - 1 : dl);
-    const uint32_t dv = L[F_G + (1 + ((e >> 17) & 3u)) * F_TS + dlc];
-    if (dl >= SHIFT && dl < U_END && dv != sv) A.fail((uint64_t)(base0 + dl), B2F_CODE_COPY);
-  }
-}
-
 // Per-quad gates of a selector quad the G pass does not take (init/final blocks, any
 // non-canonical selector row): the gates of rows r0..r0+3 whose last row is in [lo, hi).
 __device__ __forceinline__ void quad_gates_f(const FTile& T, EvalAcc& A, const uint4& fx,
@@ -407,10 +359,10 @@ __device__ __forceinline__ void sts4(uint32_t* L, int w, const uint4& v) {
 #define B2F_FUSED_WAVES 3  // waves per SIMD (LDS allows 3 workgroups per CU)
 #endif
 
-// MODE: FZ_CHECK evaluate the tile (else assign only), FZ_STORE write the trace to HBM,
-// FZ_INJECT the test-only fault injection. Product launches: FZ_CHECK | FZ_STORE (diagnostic
+// MODE: FZ_LOOKUP / FZ_GATES / FZ_COPIES which checks run, FZ_STORE write the trace to HBM,
+// FZ_INJECT the test-only fault injection. Product launches: FZ_FULL (diagnostic
 // variants via B2F_DIAG_FUSED).
-enum { FZ_CHECK = 1, FZ_STORE = 2, FZ_FULL = 3, FZ_INJECT = 4 };
+enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16, FZ_FULL = 27 };
 
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK, B2F_FUSED_WAVES)
@@ -559,14 +511,6 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     const uint32_t own_lq = P.lq, own_rounds = P.rounds;
     const uint4 fx = make_uint4(Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]);
     const uint4 a9 = make_uint4(Q.c[A9][0], Q.c[A9][1], Q.c[A9][2], Q.c[A9][3]);
-    if ((MODE & FZ_CHECK) && gq < total_quads) {
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t tg = Q.c[A0][j], de = Q.c[A1][j], sp = Q.c[A2][j];
-        if (!(de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu)))
-          A.fail(row0 + j, B2F_CODE_LOOKUP);
-      }
-    }
     if (!band_start && tid >= (TILE_ROWS - HIST) / 4 - SHIFT / 4) {
       // the rows this thread is about to overwrite become the history window (u - 1024)
 #pragma unroll
@@ -610,18 +554,29 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     __syncthreads();
 
     // ---- C. build the next tile's G table, check this tile
-    if (has_next && tid < 64)
+    if (has_next && (tid >> 6) == GT_WAVE)
       build_g_table_f(L + F_GS + nxt * FSET, ninfo, Sg, (int64_t)(tn * TILE_ROWS) - SHIFT, n,
-                      total_rows, tid);
+                      total_rows, (uint32_t)tid & 63u);
     const uint32_t* S = L + F_GS + cur * FSET;
-    if (MODE & FZ_CHECK) {
-    half_g_gates_f(T, A, L, S, base0, (uint32_t)tid & 63u, (uint32_t)tid >> 6);
-    round_copies_f(A, L, S, base0, (uint32_t)tid);
+    if ((MODE & FZ_LOOKUP) && gq < total_quads) {
+      // the staged cells of this thread's rows (LDS, as every other check reads them)
+      const uint4 q0 = T.quad(A0, (uint32_t)u0), q1 = T.quad(A1, (uint32_t)u0), q2 = T.quad(A2, (uint32_t)u0);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t tg = comp(q0, j), de = comp(q1, j), sp = comp(q2, j);
+        if (!(de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu)))
+          A.fail(row0 + j, B2F_CODE_LOOKUP);
+      }
+    }
+    const GCarve C{F_QSEL, F_A9, F_CT, F_G, F_TS, SHIFT, U_END, true};
+    const uint32_t ng = S[FS_NG];
+    if (MODE & FZ_GATES) g_pass(T, A, L, S + FS_GT, ng, base0, (uint32_t)tid & 63u, (uint32_t)tid >> 6, C);
+    if (MODE & FZ_COPIES) g_copies(A, L, S + FS_GT, ng, base0, (uint32_t)tid, C);
     const int hi = last_tile ? U_END + F_HALO : U_END;
-    if (!canonical_quad(L, S, SHIFT / 4 + tid, fx)) {
-      quad_gates_f(T, A, fx, a9, u0, SHIFT, hi, base0);
+    if ((MODE & (FZ_GATES | FZ_COPIES)) && !canonical_quad(L, S, SHIFT / 4 + tid, fx)) {
+      if (MODE & FZ_GATES) quad_gates_f(T, A, fx, a9, u0, SHIFT, hi, base0);
       const uint32_t pq = reinterpret_cast<const uint8_t*>(S + FS_QM)[SHIFT / 4 + tid];
-      if (pq == 0xffu && own_rounds != ~0u) {  // init/final-block copies
+      if ((MODE & FZ_COPIES) && pq == 0xffu && own_rounds != ~0u) {  // init/final-block copies
         const uint64_t o = row0 - 4ull * own_lq;
         const uint64_t ofirst = first < n ? reinterpret_cast<const uint64_t*>(info + 2)[0] : ~0ull;
         const Src<F_WS> src{L + F_W, L + F_IC, adv, total_rows, (uint64_t)(base0 - HIST), ofirst};
@@ -633,10 +588,10 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
       // the carried quad u 0..15 this thread assigned last tile: its gates that end here
       const int qc = tid - (BLOCK - SHIFT / 4);
       const uint4 cfx = lds4(L, F_CAR + 4 * qc), ca9 = lds4(L, F_CAR + 16 + 4 * qc);
-      if (!canonical_quad(L, S, qc, cfx)) quad_gates_f(T, A, cfx, ca9, 4 * qc, SHIFT, hi, base0);
+      if ((MODE & FZ_GATES) && !canonical_quad(L, S, qc, cfx))
+        quad_gates_f(T, A, cfx, ca9, 4 * qc, SHIFT, hi, base0);
       sts4(L, F_CAR + 4 * qc, fx);
       sts4(L, F_CAR + 16 + 4 * qc, a9);
-    }
     }
     __syncthreads();
     P = Pn;
@@ -687,7 +642,8 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                        total_rows, rec, d_adv, d_fixed, reinterpret_cast<const TileInfo*>(tinfo), \
                        n_tiles, band, d_rep, d_status, inj);                                  \
     break;
-    B2F_FUSED(0) B2F_FUSED(1) B2F_FUSED(2) B2F_FUSED(FZ_FULL | FZ_INJECT)
+    B2F_FUSED(0) B2F_FUSED(2) B2F_FUSED(3) B2F_FUSED(10) B2F_FUSED(18) B2F_FUSED(8) B2F_FUSED(16)
+    B2F_FUSED(FZ_FULL | FZ_INJECT)
     default: B2F_FUSED(FZ_FULL)
 #undef B2F_FUSED
   }

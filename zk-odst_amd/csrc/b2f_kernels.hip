@@ -247,6 +247,8 @@ constexpr int LDS_WORDS = L_ACC + 20 + 2;
 static_assert(L_INFO % 4 == 0 && L_IC % 4 == 0 && L_G % 4 == 0 && L_CT % 4 == 0 && L_ACC % 2 == 0,
               "aligned carve");
 static_assert(LDS_WORDS * 4 * 3 <= 160 * 1024, "three eval workgroups per CU");
+static_assert(GT_WORDS == GT_WORDS_ && L_GS % 4 == 0 && GSET % 4 == 0, "G table entries are two aligned uint4");
+static_assert(MAX_TILE_G * LPG <= BLOCK, "copy lanes");
 
 
 // Extra (non-own-quad) loads of a tile: 2 slots per thread.
@@ -346,61 +348,6 @@ __device__ __forceinline__ void build_g_table(uint32_t* S, const uint32_t* info,
     if (q >= 0 && q < BLOCK) qm[q] = (uint8_t)p;
   }
 }
-
-// Gates of the canonical round blocks of a tile. Lane l of every wave takes item l =
-// (G table entry l >> 1, half l & 1), and wave w checks block kind w of it: 0 a1/a2 (ADD3,
-// +0/+28), 1 d1/d2 (XOR, +4/+32), 2 c1/c2 (ADD2, +12/+40), 3 b1 (XOR24, +16) / b2 (XOR63,
-// +44). Each wave thus runs one evaluator (the b wave two) instead of every wave running all
-// five block kinds mostly masked, as a quad-per-lane assignment would. A block is checked here
-// only if its selector row lies in this tile and its quad is canonical: row-0 selector bits
-// exactly the block's and none on rows 1-3 (QSEL, staged). Every other selector row is
-// evaluated by its own quad's lane (row_gates), so each selector row is evaluated once.
-__device__ __forceinline__ void half_g_gates(const Tile& T, EvalAcc& A, const uint32_t* L,
-                                             const uint32_t* S, uint64_t tile0, uint32_t lane,
-                                             uint32_t kind) {
-  if (lane >= 2 * S[GS_NG]) return;
-  const uint32_t h = lane & 1u;
-  const int off = kind == 0 ? 0 : kind == 1 ? 4 : kind == 2 ? 12 : 16;
-  const int rl = (int)S[GS_GT + GT_WORDS * (lane >> 1) + 5] + 28 * (int)h + off;  // selector row
-  const uint32_t want = kind == 0 ? 1u << (h ? S_A2 : S_A1)
-                      : kind == 1 ? 1u << (h ? S_D2 : S_D1)
-                      : kind == 2 ? 1u << (h ? S_C2 : S_C1)
-                      : h ? (1u << S_B2) | (1u << S_IJKL) : (1u << S_B1) | (1u << S_EFGH);
-  if (rl < 0 || rl >= TILE_ROWS || L[L_QSEL + (rl >> 2)] != want) return;
-  const uint32_t r = (uint32_t)rl;
-  uint32_t f;
-  if (kind == 0 || kind == 2) {
-    f = g_add(T, r, L[L_A9 + (r >> 2)], kind == 0) ? 0u : want;
-  } else if (kind == 1) {
-    f = g_xor(T, r, false) ? 0u : want;
-  } else {
-    f = h ? g_xor63(T, r, want) : g_xor24(T, r, want);
-  }
-  if (f) A.fail_gates(tile0 + r, f);
-}
-
-// The copy checks of the tile's G's: item it = (G table entry it / 72, check it % 72), spread
-// over all threads. A check belongs to this tile if its operand row does; its source is one
-// LDS read at (per-G base) + C for every valid layout.
-__device__ __forceinline__ void round_copies(EvalAcc& A, const uint32_t* L, const uint32_t* S,
-                                             uint64_t tile0, uint32_t tid) {
-  const uint32_t nchk = S[GS_NG] * G_CHECKS;
-#pragma unroll 2
-  for (uint32_t k = 0; k < (MAX_TILE_G * G_CHECKS + BLOCK - 1) / BLOCK; k++) {
-    const uint32_t it = tid + k * BLOCK;
-    if (it >= nchk) break;
-    const uint32_t gi = it / G_CHECKS, ci = it - gi * G_CHECKS;
-    const uint32_t* gt = S + GS_GT + GT_WORDS * gi;
-    const uint32_t e = L[L_CT + gt[6] + ci];
-    const int dl = (int)gt[5] + (int)((e >> 19) & 63u);
-    const int src = (int)gt[(e >> 14) & 7u] + (int)(e & 16383u);
-    const uint32_t sv = L[src < 0 ? 0 : src];  // < 0 only for checks outside the tile
-    const int dlc = dl < 0 ? 0 : (dl >= TILE_ROWS ? TILE_ROWS - 1 : dl);
-    const uint32_t dv = L[L_G + (1 + ((e >> 17) & 3u)) * TSTRIDE + dlc];
-    if (dl >= 0 && dl < TILE_ROWS && dv != sv) A.fail(tile0 + (uint64_t)dl, B2F_CODE_COPY);
-  }
-}
-
 
 // MODE (diagnostics; the product uses EVAL_FULL): which checks run on a staged tile.
 enum { EVAL_LOOKUP = 1, EVAL_GATES = 2, EVAL_COPIES = 4, EVAL_FULL = 7, EVAL_TOUCH = 8 };
@@ -572,10 +519,14 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
         if (tid < 64) build_g_table(L + L_GS, L + L_INFO, Sg, tile0, n, total_rows, (uint32_t)tid);
         __syncthreads();
       }
-      if (tid < 64) build_g_table(Sn, L + L_INFO2, Sg, (t + G) * TILE_ROWS, t + G < n_tiles ? n : 0,
-                                  total_rows, (uint32_t)tid);
-      if (MODE & EVAL_GATES) half_g_gates(T, A, L, S, tile0, (uint32_t)tid & 63u, (uint32_t)tid >> 6);
-      if (MODE & EVAL_COPIES) round_copies(A, L, S, tile0, (uint32_t)tid);
+      if ((tid >> 6) == GT_WAVE)  // the wave with the lightest G pass (XOR) builds ahead
+        build_g_table(Sn, L + L_INFO2, Sg, (t + G) * TILE_ROWS, t + G < n_tiles ? n : 0,
+                      total_rows, (uint32_t)tid & 63u);
+      const GCarve C{L_QSEL, L_A9, L_CT, L_G, TSTRIDE, 0, TILE_ROWS, false};
+      const uint32_t ng = S[GS_NG];
+      if (MODE & EVAL_GATES)
+        g_pass(T, A, L, S + GS_GT, ng, (int64_t)tile0, (uint32_t)tid & 63u, (uint32_t)tid >> 6, C);
+      if (MODE & EVAL_COPIES) g_copies(A, L, S + GS_GT, ng, (int64_t)tile0, (uint32_t)tid, C);
       // ---- per quad: selector rows the G pass does not take, and init/final-block copies
       if (gq < total_quads) {
         const uint32_t pq = reinterpret_cast<const uint8_t*>(S + GS_QM)[tid];
@@ -932,7 +883,7 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
   HIPCHK(ctx, launch_fill_eval(d_in, (uint32_t)n, d_offsets, total_rows, ctx->d_rec, d_advice,
                                d_fixed, ctx->d_tiles, nt, band, d_report, ctx->d_status,
                                ctx->inj_row, ctx->inj_col, ctx->inj_mask,
-                               diag_mode("B2F_DIAG_FUSED", 3), ctx->cu_count, s));
+                               diag_mode("B2F_DIAG_FUSED", 27), ctx->cu_count, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
