@@ -307,7 +307,9 @@ static_assert(sizeof(TileInfo) == 96, "TileInfo is six 16-byte loads");
 //   16-31 selector bits of the row
 struct RowTable {
   uint32_t r[G_QUADS][4];
+  uint32_t slot[G_QUADS];  // per-quad operand slots (make_slots)
 };
+constexpr int ROW_TABLE_WORDS = G_QUADS * 5;
 constexpr uint32_t row_recipe(uint32_t k, uint32_t src, uint32_t sh8, uint32_t mask, uint32_t ops,
                               uint32_t m, uint32_t w, uint32_t zb, uint32_t cy, uint32_t sel) {
   return k | (src << 2) | (sh8 << 4) | (mask << 5) | (ops << 7) | (m << 9) | (w << 10) |
@@ -343,10 +345,32 @@ constexpr RowTable make_rows() {
       T.r[p][j] = e;
     }
   }
+  // Operand slots: the (at most two) rows of a quad whose a_3/a_4 hold spread operand limbs
+  // (XOR, XOR24, XOR63 blocks), with their limb, so a quad needs six operand spreads instead of
+  // three per row. bits 0-1 row A, 2-3 limb A, 4 A used, 5-6 row B, 7-8 limb B, 9 B used,
+  // 10 a7/a8 = W limb / spread at the slot rows, 11 a6 = Z limb >> 15 at the slot rows,
+  // 12 dense a3/a4 (ADD: limb j on row j), 13 a5 = M limb (ADD3).
+  for (uint32_t p = 0; p < G_QUADS; p++) {
+    const uint32_t st = step_of_quad(p), q = p - first_quad[st];
+    uint32_t d = 0;
+    if (st % 2 == 0) {
+      d = (1u << 12) | ((st == 0 || st == 4) ? 1u << 13 : 0u);
+    } else if (st == 3) {  // XOR24: rows R = 4q + j with R % 3 == 0, limb R / 3
+      d = q == 0 ? (0u | (0u << 2) | (1u << 4) | (3u << 5) | (1u << 7) | (1u << 9))
+        : q == 1 ? (2u | (2u << 2) | (1u << 4))
+                 : (1u | (3u << 2) | (1u << 4));
+      d |= 1u << 10;
+    } else {  // XOR / XOR63: rows 0 and 2, limbs 2q and 2q + 1
+      d = 0u | ((2 * q) << 2) | (1u << 4) | (2u << 5) | ((2 * q + 1) << 7) | (1u << 9);
+      if (st == 7) d |= (1u << 10) | (1u << 11);
+    }
+    T.slot[p] = d;
+  }
   return T;
 }
 __constant__ __attribute__((aligned(16))) RowTable c_rows = make_rows();
 
+// `rows`: the RowTable staged in LDS (ROW_TABLE_WORDS words).
 __device__ __forceinline__ void quad_round(Quad& Q, uint64_t a, uint64_t b, uint64_t c,
                                            uint64_t d, uint64_t mx, uint64_t my, uint32_t p,
                                            const uint32_t* __restrict__ rows) {
@@ -367,6 +391,17 @@ __device__ __forceinline__ void quad_round(Quad& Q, uint64_t a, uint64_t b, uint
   const uint32_t carry = (uint32_t)(s1 < X) + (uint32_t)(S < s1);
   const uint64_t Z = X ^ Y, O = X & Y;
   const uint64_t W = st == 3 ? rotr64(Z, 24) : rotr64(Z, 63);
+  // operand slots A and B: limbs of X, Y, W, Z and the spreads of the first three
+  const uint32_t sd = rows[4 * G_QUADS + p];
+  const uint32_t jA = sd & 3u, shA = 16 * ((sd >> 2) & 3u), jB = (sd >> 5) & 3u, shB = 16 * ((sd >> 7) & 3u);
+  const bool vA = (sd >> 4) & 1u, vB = (sd >> 9) & 1u, has_w = (sd >> 10) & 1u, has_z = (sd >> 11) & 1u;
+  const bool dense = (sd >> 12) & 1u, has_m = (sd >> 13) & 1u;
+  const uint32_t xA = (uint32_t)(X >> shA) & 0xffffu, yA = (uint32_t)(Y >> shA) & 0xffffu;
+  const uint32_t xB = (uint32_t)(X >> shB) & 0xffffu, yB = (uint32_t)(Y >> shB) & 0xffffu;
+  const uint32_t wA = (uint32_t)(W >> shA) & 0xffffu, wB = (uint32_t)(W >> shB) & 0xffffu;
+  const uint32_t zA = ((uint32_t)(Z >> shA) & 0xffffu) >> 15, zB = ((uint32_t)(Z >> shB) & 0xffffu) >> 15;
+  const uint32_t sxA = spread16(xA), syA = spread16(yA), swA = spread16(wA);
+  const uint32_t sxB = spread16(xB), syB = spread16(yB), swB = spread16(wB);
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const uint32_t e = rows[4 * p + j];
@@ -377,18 +412,171 @@ __device__ __forceinline__ void quad_round(Quad& Q, uint64_t a, uint64_t b, uint
     const uint32_t v = (uint32_t)(V >> (sh + 8 * ((e >> 4) & 1u))) &
                        (mcode == 0 ? 0xffffu : mcode == 1 ? 0xffu : 0x7fffu);
     lrow(Q, j, v);
-    const uint32_t xk = (uint32_t)(X >> sh) & 0xffffu, yk = (uint32_t)(Y >> sh) & 0xffffu;
-    const uint32_t ops = (e >> 7) & 3u;
-    Q.c[A3][j] = ops == 1 ? xk : ops == 2 ? spread16(xk) : 0u;
-    Q.c[A4][j] = ops == 1 ? yk : ops == 2 ? spread16(yk) : 0u;
-    Q.c[A5][j] = (e >> 9) & 1u ? (uint32_t)(M >> sh) & 0xffffu : 0u;
-    Q.c[A6][j] = (e >> 11) & 1u ? ((uint32_t)(Z >> sh) & 0xffffu) >> 15 : 0u;
-    const uint32_t wk = (uint32_t)(W >> sh) & 0xffffu;
-    const bool hw = (e >> 10) & 1u;
-    Q.c[A7][j] = hw ? wk : 0u;
-    Q.c[A8][j] = hw ? spread16(wk) : 0u;
+    const bool isA = vA && jA == (uint32_t)j, isB = vB && jB == (uint32_t)j;
+    Q.c[A3][j] = dense ? (uint32_t)(X >> (16 * j)) & 0xffffu : isA ? sxA : isB ? sxB : 0u;
+    Q.c[A4][j] = dense ? (uint32_t)(Y >> (16 * j)) & 0xffffu : isA ? syA : isB ? syB : 0u;
+    Q.c[A5][j] = has_m ? (uint32_t)(M >> (16 * j)) & 0xffffu : 0u;
+    Q.c[A6][j] = has_z ? (isA ? zA : isB ? zB : 0u) : 0u;
+    Q.c[A7][j] = has_w ? (isA ? wA : isB ? wB : 0u) : 0u;
+    Q.c[A8][j] = has_w ? (isA ? swA : isB ? swB : 0u) : 0u;
     Q.c[A9][j] = (e >> 12) & 1u ? carry : 0u;
     Q.fx[j] = e >> 16;
+  }
+}
+
+// Operand words of one quad, loaded one tile ahead of its use.
+struct QuadOps {
+  uint64_t w[6];
+  uint32_t lq;      // quad inside its instance
+  uint32_t rounds;  // ~0u: no live quad (past the batch)
+};
+
+// Address computation and loads for the quad at `row` of instance `inst` (rows [o, o1)).
+__device__ __forceinline__ void quad_ops_at(QuadOps& P, uint64_t row, uint32_t inst, uint64_t o,
+                                            uint64_t o1, const b2f_input* __restrict__ in,
+                                            const uint64_t* __restrict__ rec, const uint8_t* Sg) {
+  const uint32_t rounds = ((uint32_t)(o1 - o) - FIXED_ROWS) / ROUND_ROWS;
+  const uint32_t lq = (uint32_t)((row - o) >> 2);
+  const b2f_input* x = in + inst;
+  const uint64_t* st0 = rec + 16ull * state_index(o, inst);
+  const uint64_t* fw = reinterpret_cast<const uint64_t*>(&x->rounds);  // rounds | f << 32
+  P.lq = lq;
+  P.rounds = rounds;
+  const uint64_t *p0 = fw, *p1 = fw, *p2 = fw, *p3 = fw, *p4 = fw, *p5 = fw;
+  uint32_t m = 0;
+  const uint32_t rq = lq - INIT_QUADS;
+  if (lq >= INIT_QUADS && rq < ROUND_QUADS * rounds) {
+    const uint32_t r = rq / ROUND_QUADS, g = (rq - r * ROUND_QUADS) / G_QUADS;
+    const uint64_t* st = st0 + 16ull * (2ull * r + (g >= 4));
+    // (a, b, c, d) of G g: column g (g < 4) or diagonal g - 4 of the 4x4 work matrix
+    const uint32_t gl = g & 3u, dg = g >> 2;
+    const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
+    p0 = st + gl;
+    p1 = st + 4 + ((gl + dg) & 3u);
+    p2 = st + 8 + ((gl + 2 * dg) & 3u);
+    p3 = st + 12 + ((gl + 3 * dg) & 3u);
+    p4 = x->m + sg[0];
+    p5 = x->m + sg[1];
+    m = 63;
+  } else if (lq < INIT_QUADS) {
+    if (lq < 26) {
+      p0 = lq < 8 ? x->h + lq : (lq < 24 ? x->m + (lq - 8) : x->t + (lq - 24));
+      m = 1;
+    } else if (lq == 26) {
+      m = 1;  // fmask: the f word
+    } else if (lq >= 35) {
+      const uint32_t a = (lq - 35) >> 1;
+      if (a < 2) p0 = x->t + a;
+      m = 1;  // v12 = IV4 ^ t0, v13 = IV5 ^ t1, v14 = IV6 ^ fmask(f)
+    }
+  } else {
+    const uint32_t a = (rq - ROUND_QUADS * rounds) >> 1;
+    const uint64_t* fin = st0 + 16ull * (2ull * rounds);
+    p0 = x->h + a;
+    p1 = fin + a;
+    p2 = fin + a + 8;
+    m = 7;
+  }
+  P.w[0] = (m & 1u) ? *p0 : 0ull;
+  P.w[1] = (m & 2u) ? *p1 : 0ull;
+  P.w[2] = (m & 4u) ? *p2 : 0ull;
+  P.w[3] = (m & 8u) ? *p3 : 0ull;
+  P.w[4] = (m & 16u) ? *p4 : 0ull;
+  P.w[5] = (m & 32u) ? *p5 : 0ull;
+}
+
+// Operand addresses of the quad at `row`, for instances first .. first + 7 with offsets
+// Off[0..8] (LDS or global), then the loads. Round quads: the four state words of their G at
+// the half-round start and the two message words; init quads: the input word they decompose
+// (h/m/t, or the `rounds | f << 32` word for the fmask); final quads: h_i and the final
+// v_i, v_{i+8}. Same data the fill_kernel reads (quad_cells / quad_round).
+// Everything the address computation reads is in registers or LDS (Off, Sg): on CDNA, vmcnt
+// counts stores and loads in issue order, so a global load here would wait for every store
+// the wave has in flight.
+__device__ __forceinline__ void quad_ops(QuadOps& P, uint64_t row, uint32_t first,
+                                         const uint64_t* Off, uint32_t n, uint64_t used_rows,
+                                         const b2f_input* __restrict__ in,
+                                         const uint64_t* __restrict__ rec, const uint8_t* Sg) {
+  P.rounds = ~0u;
+  P.lq = 0;
+#pragma unroll
+  for (int k = 0; k < 6; k++) P.w[k] = 0;
+  if (row >= used_rows || first >= n) return;
+  uint32_t i = 0;
+  while (i + 2 < NOFF && Off[i + 1] <= row) i++;
+  const uint64_t o = Off[i], o1 = Off[i + 1];
+  if (row < o || row >= o1 || first + i >= n) return;  // not for a layout the record kernel accepted
+  quad_ops_at(P, row, first + i, o, o1, in, rec, Sg);
+}
+
+// The same from a TileInfo held in scalar registers (the fill kernel): the instance is found by
+// a branch-free scan of the eight cached offsets.
+__device__ __forceinline__ void quad_ops_ti(QuadOps& P, uint64_t row, const TileInfo& ti,
+                                            uint32_t n, uint64_t used_rows,
+                                            const b2f_input* __restrict__ in,
+                                            const uint64_t* __restrict__ rec, const uint8_t* Sg) {
+  P.rounds = ~0u;
+  P.lq = 0;
+#pragma unroll
+  for (int k = 0; k < 6; k++) P.w[k] = 0;
+  if (row >= used_rows || ti.first >= n) return;
+  uint64_t o = ti.off[0], o1 = ti.off[1];
+  uint32_t i = 0;
+#pragma unroll
+  for (int k = 1; k + 1 < NOFF; k++)
+    if (ti.off[k] <= row) { o = ti.off[k]; o1 = ti.off[k + 1]; i = (uint32_t)k; }
+  if (row < o || row >= o1 || ti.first + i >= n) return;
+  quad_ops_at(P, row, ti.first + i, o, o1, in, rec, Sg);
+}
+
+// The operand word of init quad lq (< 41) of instance x: what quad_ops loads for it.
+__device__ __forceinline__ uint64_t init_word(const b2f_input* __restrict__ x, uint32_t lq) {
+  const uint64_t* fw = reinterpret_cast<const uint64_t*>(&x->rounds);
+  if (lq < 26) return lq < 8 ? x->h[lq] : (lq < 24 ? x->m[lq - 8] : x->t[lq - 24]);
+  if (lq == 26) return *fw;
+  if (lq < 35) return 0;
+  const uint32_t a = (lq - 35) >> 1;
+  return a < 2 ? x->t[a] : *fw;
+}
+
+// Init and final quads from their operand words (the fill's quad_cells, register-fed).
+__device__ __forceinline__ void quad_cells_ops(Quad& Q, const QuadOps& P, const uint64_t* IV) {
+  const QuadInfo d = decode_quad(P.lq, P.rounds);
+  switch (d.kind) {
+    case K_INW: {
+      const uint64_t W = P.w[0];
+#pragma unroll
+      for (int j = 0; j < 4; j++) lrow(Q, j, limb(W, j));
+      Q.c[A7][0] = (uint32_t)W;
+      Q.c[A8][0] = (uint32_t)(W >> 32);
+      Q.fx[0] = 1u << S_ABCD;
+      break;
+    }
+    case K_FMASK: {
+      const uint32_t f = (P.w[0] >> 32) ? 1u : 0u;
+#pragma unroll
+      for (int j = 0; j < 4; j++) lrow(Q, j, f ? 0xffffu : 0u);
+      Q.c[A5][0] = f;
+      Q.fx[0] = 1u << S_FMASK;
+      break;
+    }
+    case K_CONST: {
+      const uint64_t W = IV[d.a];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        lrow(Q, j, limb(W, j));
+        Q.fx[j] = (1u << S_CONST) | (limb(W, j) << 16);
+      }
+      break;
+    }
+    case K_XOR3:
+      q_xor3(Q, P.w[0], P.w[1], P.w[2], d.q);
+      break;
+    default: {  // init XORs (round quads never come here)
+      const uint64_t Y = d.a < 2 ? P.w[0] : ((P.w[0] >> 32) ? ~0ull : 0ull);
+      q_xor(Q, IV[4 + d.a], Y, d.q, S_XOR);
+      break;
+    }
   }
 }
 
@@ -950,6 +1138,10 @@ __device__ __forceinline__ uint32_t row_gates(const Tile& T, uint32_t sel, uint3
       return g_xor(T, r, false) ? 0u : sel;
     case (1u << S_XOR3) | (1u << S_DIGEST):
       return (g_xor(T, r, true) ? 0u : 1u << S_XOR3) | (g_digest(T, r) ? 0u : 1u << S_DIGEST);
+    case 1u << S_ABCD:  // input-word decompositions (26 per instance)
+      return gate_ok(T, S_ABCD, r, a9, k0) ? 0u : sel;
+    case 1u << S_FMASK:
+      return gate_ok(T, S_FMASK, r, a9, k0) ? 0u : sel;
     default:
       return gates_generic(T, sel, r, a9, k0);
   }

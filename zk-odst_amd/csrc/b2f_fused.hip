@@ -69,7 +69,7 @@ constexpr int F_WORDS = F_ACC + 22;
 static_assert(F_INFO % 4 == 0 && F_IV % 2 == 0 && F_IC % 4 == 0 && (F_IC + INIT_ROWS) % 4 == 0 && F_G % 4 == 0 &&
               F_CAR % 4 == 0 && F_GS % 4 == 0 && F_ACC % 2 == 0 && F_WS % 4 == 0 && F_TS % 4 == 0,
               "aligned carve");
-static_assert((F_WORDS + G_QUADS * 4) * 4 * 3 <= 160 * 1024, "three fused workgroups per CU");
+static_assert((F_WORDS + ROW_TABLE_WORDS) * 4 * 3 <= 160 * 1024, "three fused workgroups per CU");
 static_assert(check_table_ok<F_W, F_WS>(), "72 copy checks per G, fields in range");
 static_assert(F_GT_WORDS == GT_WORDS_ && F_MAX_G * LPG <= BLOCK, "G table layout / copy lanes");
 
@@ -106,136 +106,6 @@ struct Inject {
   uint32_t col;   // 0..9 advice a_col, 10 fixed
   uint32_t mask;
 };
-
-// Operand words of one quad, loaded one tile ahead of its use.
-struct QuadOps {
-  uint64_t w[6];
-  uint32_t lq;      // quad inside its instance
-  uint32_t rounds;  // ~0u: no live quad (past the batch)
-};
-
-// Operand addresses of the quad at `row`, for instances first .. first + 7 with offsets
-// Off[0..8] (LDS or global), then the loads. Round quads: the four state words of their G at
-// the half-round start and the two message words; init quads: the input word they decompose
-// (h/m/t, or the `rounds | f << 32` word for the fmask); final quads: h_i and the final
-// v_i, v_{i+8}. Same data the fill_kernel reads (quad_cells / quad_round).
-// Everything the address computation reads is in registers or LDS (Off, Sg): on CDNA, vmcnt
-// counts stores and loads in issue order, so a global load here would wait for every store
-// the wave has in flight.
-__device__ __forceinline__ void quad_ops(QuadOps& P, uint64_t row, uint32_t first,
-                                         const uint64_t* Off, uint32_t n, uint64_t used_rows,
-                                         const b2f_input* __restrict__ in,
-                                         const uint64_t* __restrict__ rec, const uint8_t* Sg) {
-  P.rounds = ~0u;
-  P.lq = 0;
-#pragma unroll
-  for (int k = 0; k < 6; k++) P.w[k] = 0;
-  if (row >= used_rows || first >= n) return;
-  uint32_t i = 0;
-  while (i + 2 < NOFF && Off[i + 1] <= row) i++;
-  const uint64_t o = Off[i], o1 = Off[i + 1];
-  if (row < o || row >= o1 || first + i >= n) return;  // not for a layout the record kernel accepted
-  const uint32_t inst = first + i;
-  const uint32_t rounds = ((uint32_t)(o1 - o) - FIXED_ROWS) / ROUND_ROWS;
-  const uint32_t lq = (uint32_t)((row - o) >> 2);
-  const b2f_input* x = in + inst;
-  const uint64_t* st0 = rec + 16ull * state_index(o, inst);
-  const uint64_t* fw = reinterpret_cast<const uint64_t*>(&x->rounds);  // rounds | f << 32
-  P.lq = lq;
-  P.rounds = rounds;
-  const uint64_t *p0 = fw, *p1 = fw, *p2 = fw, *p3 = fw, *p4 = fw, *p5 = fw;
-  uint32_t m = 0;
-  const uint32_t rq = lq - INIT_QUADS;
-  if (lq >= INIT_QUADS && rq < ROUND_QUADS * rounds) {
-    const uint32_t r = rq / ROUND_QUADS, g = (rq - r * ROUND_QUADS) / G_QUADS;
-    const uint64_t* st = st0 + 16ull * (2ull * r + (g >= 4));
-    // (a, b, c, d) of G g: column g (g < 4) or diagonal g - 4 of the 4x4 work matrix
-    const uint32_t gl = g & 3u, dg = g >> 2;
-    const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
-    p0 = st + gl;
-    p1 = st + 4 + ((gl + dg) & 3u);
-    p2 = st + 8 + ((gl + 2 * dg) & 3u);
-    p3 = st + 12 + ((gl + 3 * dg) & 3u);
-    p4 = x->m + sg[0];
-    p5 = x->m + sg[1];
-    m = 63;
-  } else if (lq < INIT_QUADS) {
-    if (lq < 26) {
-      p0 = lq < 8 ? x->h + lq : (lq < 24 ? x->m + (lq - 8) : x->t + (lq - 24));
-      m = 1;
-    } else if (lq == 26) {
-      m = 1;  // fmask: the f word
-    } else if (lq >= 35) {
-      const uint32_t a = (lq - 35) >> 1;
-      if (a < 2) p0 = x->t + a;
-      m = 1;  // v12 = IV4 ^ t0, v13 = IV5 ^ t1, v14 = IV6 ^ fmask(f)
-    }
-  } else {
-    const uint32_t a = (rq - ROUND_QUADS * rounds) >> 1;
-    const uint64_t* fin = st0 + 16ull * (2ull * rounds);
-    p0 = x->h + a;
-    p1 = fin + a;
-    p2 = fin + a + 8;
-    m = 7;
-  }
-  P.w[0] = (m & 1u) ? *p0 : 0ull;
-  P.w[1] = (m & 2u) ? *p1 : 0ull;
-  P.w[2] = (m & 4u) ? *p2 : 0ull;
-  P.w[3] = (m & 8u) ? *p3 : 0ull;
-  P.w[4] = (m & 16u) ? *p4 : 0ull;
-  P.w[5] = (m & 32u) ? *p5 : 0ull;
-}
-
-// The operand word of init quad lq (< 41) of instance x: what quad_ops loads for it.
-__device__ __forceinline__ uint64_t init_word(const b2f_input* __restrict__ x, uint32_t lq) {
-  const uint64_t* fw = reinterpret_cast<const uint64_t*>(&x->rounds);
-  if (lq < 26) return lq < 8 ? x->h[lq] : (lq < 24 ? x->m[lq - 8] : x->t[lq - 24]);
-  if (lq == 26) return *fw;
-  if (lq < 35) return 0;
-  const uint32_t a = (lq - 35) >> 1;
-  return a < 2 ? x->t[a] : *fw;
-}
-
-// Init and final quads from their operand words (the fill's quad_cells, register-fed).
-__device__ __forceinline__ void quad_cells_ops(Quad& Q, const QuadOps& P, const uint64_t* IV) {
-  const QuadInfo d = decode_quad(P.lq, P.rounds);
-  switch (d.kind) {
-    case K_INW: {
-      const uint64_t W = P.w[0];
-#pragma unroll
-      for (int j = 0; j < 4; j++) lrow(Q, j, limb(W, j));
-      Q.c[A7][0] = (uint32_t)W;
-      Q.c[A8][0] = (uint32_t)(W >> 32);
-      Q.fx[0] = 1u << S_ABCD;
-      break;
-    }
-    case K_FMASK: {
-      const uint32_t f = (P.w[0] >> 32) ? 1u : 0u;
-#pragma unroll
-      for (int j = 0; j < 4; j++) lrow(Q, j, f ? 0xffffu : 0u);
-      Q.c[A5][0] = f;
-      Q.fx[0] = 1u << S_FMASK;
-      break;
-    }
-    case K_CONST: {
-      const uint64_t W = IV[d.a];
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        lrow(Q, j, limb(W, j));
-        Q.fx[j] = (1u << S_CONST) | (limb(W, j) << 16);
-      }
-      break;
-    }
-    case K_XOR3:
-      q_xor3(Q, P.w[0], P.w[1], P.w[2], d.q);
-      break;
-    default: {  // init XORs (round quads never come here)
-      const uint64_t Y = d.a < 2 ? P.w[0] : ((P.w[0] >> 32) ? ~0ull : 0ull);
-      q_xor(Q, IV[4 + d.a], Y, d.q, S_XOR);
-      break;
-    }
-  }
-}
 
 template <bool INJ>
 __device__ __forceinline__ void build_quad(Quad& Q, const QuadOps& P, uint64_t gq,
@@ -372,7 +242,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
              uint32_t band, b2f_eval_report* __restrict__ rep, const int* __restrict__ status,
              Inject inj) {
   __shared__ __attribute__((aligned(16))) uint32_t L[F_WORDS];
-  __shared__ uint32_t rows[G_QUADS * 4];
+  __shared__ uint32_t rows[ROW_TABLE_WORDS];
   const int tid = threadIdx.x;
   if (*status) return;  // the record kernel rejected the layout: write nothing
   for (int i = tid; i < 12 * G_CHECKS; i += BLOCK)
@@ -380,7 +250,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
   if (tid < 40) L[F_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
   if (tid < 16) L[F_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
   if (tid < 16) L[F_XS + tid] = expected_sel((uint32_t)tid);
-  if (tid < G_QUADS * 4) rows[tid] = (&c_rows.r[0][0])[tid];
+  if (tid < ROW_TABLE_WORDS) rows[tid] = (&c_rows.r[0][0])[tid];
   if (tid < 20) L[F_ACC + tid] = 0;
   if (tid == 20) *reinterpret_cast<uint64_t*>(L + F_ACC + 20) = ~0ull;
   if (tid < 32) L[F_CAR + tid] = 0;

@@ -145,7 +145,10 @@ enum { FILL_COMPUTE = 1, FILL_NT = 2, FILL_FULL = 3 };
 
 // Tiles of 1024 rows are dealt round-robin over the (persistent) workgroups, so at any time
 // the chip writes a narrow band of every column: one DRAM-friendly front per column instead
-// of one per workgroup.
+// of one per workgroup. Software-pipelined one tile deep: the tile's instance context is read
+// with scalar loads and the operand words of tile t + grid (quad_ops) are loaded before tile
+// t's stores are issued (vmcnt counts loads and stores in issue order, so a load issued after
+// the stores would wait for them).
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK) fill_kernel(const b2f_input* __restrict__ in,
                                                     uint32_t n,
@@ -157,46 +160,58 @@ __global__ void __launch_bounds__(BLOCK) fill_kernel(const b2f_input* __restrict
                                                     const int* __restrict__ status,
                                                     const TileInfo* __restrict__ tinfo,
                                                     uint64_t n_tiles) {
-  __shared__ uint32_t rows[G_QUADS * 4];
-  if (threadIdx.x < G_QUADS * 4) rows[threadIdx.x] = (&c_rows.r[0][0])[threadIdx.x];
+  __shared__ uint32_t rows[ROW_TABLE_WORDS];
+  __shared__ __attribute__((aligned(16))) uint32_t sgiv[40 + 16];  // SIGMA bytes, IV
+  const int tid = threadIdx.x;
+  if (tid < ROW_TABLE_WORDS) rows[tid] = (&c_rows.r[0][0])[tid];
+  if (tid < 40) sgiv[tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
+  if (tid < 16) sgiv[40 + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
   __syncthreads();
   if (*status) return;  // the record kernel rejected the layout: write nothing
+  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(sgiv);
+  const uint64_t* IV = reinterpret_cast<const uint64_t*>(sgiv + 40);
   const uint64_t total_quads = total_rows >> 2;
   const uint64_t used_rows = off[n];
-  for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-    uint64_t gq = t * BLOCK + threadIdx.x;
-    if (gq >= total_quads) break;
-    uint64_t row = 4 * gq;
-    Quad Q;
-    zero(Q);
-    if ((MODE & FILL_COMPUTE) && row < used_rows) {
-      uint32_t inst = tinfo[t].first;
-      while (off[inst + 1] <= row) inst++;
-      uint64_t o = off[inst];
-      const b2f_input* x = in + inst;
-      uint32_t rounds = x->rounds;
-      const uint64_t* states = rec + 16ull * state_index(o, inst);
-      const uint32_t lq = (uint32_t)((row - o) >> 2), rq = lq - INIT_QUADS;
-      if (lq >= INIT_QUADS && rq < ROUND_QUADS * rounds) {
-        const uint32_t r = rq / ROUND_QUADS, w = rq - r * ROUND_QUADS;
-        const uint32_t g = w / G_QUADS, p = w - g * G_QUADS;
-        const uint64_t* st = states + 16ull * (2ull * r + (g >= 4));
-        const uint32_t gi = c_gidx_word[g];  // a | b << 8 | c << 16 | d << 24
-        const uint32_t sg = c_sigma_pair[r % 10][g];
-        quad_round(Q, st[gi & 0xff], st[(gi >> 8) & 0xff], st[(gi >> 16) & 0xff], st[gi >> 24],
-                   x->m[sg & 0xff], x->m[sg >> 8], p, rows);
-      } else {
-        quad_cells(Q, x, states, rounds, lq);  // init and final regions
+  const uint64_t G = gridDim.x;
+  auto ops = [&](QuadOps& R, uint64_t tt) {
+    R.rounds = ~0u;
+    R.lq = 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) R.w[k] = 0;
+    if (MODE & FILL_COMPUTE) {
+      const TileInfo ti = tinfo[tt];  // workgroup-uniform: scalar loads
+      quad_ops_ti(R, 4 * (tt * BLOCK + tid), ti, n, used_rows, in, rec, Sg);
+    }
+  };
+  uint64_t t = blockIdx.x;
+  QuadOps P;
+  if (t < n_tiles) ops(P, t);
+  for (; t < n_tiles; t += G) {
+    QuadOps Pn;
+    Pn.rounds = ~0u;
+    if (t + G < n_tiles) ops(Pn, t + G);
+    const uint64_t gq = t * BLOCK + tid;
+    if (gq < total_quads) {
+      Quad Q;
+      zero(Q);
+      if ((MODE & FILL_COMPUTE) && P.rounds != ~0u) {
+        const uint32_t rq = P.lq - INIT_QUADS;
+        if (P.lq >= INIT_QUADS && rq < ROUND_QUADS * P.rounds)
+          quad_round(Q, P.w[0], P.w[1], P.w[2], P.w[3], P.w[4], P.w[5], (rq % ROUND_QUADS) % G_QUADS, rows);
+        else
+          quad_cells_ops(Q, P, IV);  // init and final regions
+      }
+      const uint64_t row = 4 * gq;
+#pragma unroll
+      for (int c = 0; c < 11; c++) {
+        u32x4 v = c < 10 ? u32x4{Q.c[c][0], Q.c[c][1], Q.c[c][2], Q.c[c][3]}
+                         : u32x4{Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]};
+        u32x4* dst = reinterpret_cast<u32x4*>((c < 10 ? adv + (uint64_t)c * total_rows : fixed) + row);
+        if (MODE & FILL_NT) __builtin_nontemporal_store(v, dst);
+        else *dst = v;
       }
     }
-#pragma unroll
-    for (int c = 0; c < 11; c++) {
-      u32x4 v = c < 10 ? u32x4{Q.c[c][0], Q.c[c][1], Q.c[c][2], Q.c[c][3]}
-                       : u32x4{Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]};
-      u32x4* dst = reinterpret_cast<u32x4*>((c < 10 ? adv + (uint64_t)c * total_rows : fixed) + row);
-      if (MODE & FILL_NT) __builtin_nontemporal_store(v, dst);
-      else *dst = v;
-    }
+    P = Pn;
   }
 }
 
