@@ -498,6 +498,16 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
     }
     if (e0.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e0.lds]) = x0;
     if (e1.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e1.lds]) = x1;
+    // ---- lookups on the quad's 4 rows, from the loaded cells, before the barrier
+    if ((MODE & EVAL_LOOKUP) && t * BLOCK + tid < total_quads) {
+      const uint64_t r0 = 4 * (t * BLOCK + tid);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t tg = comp(q[A0], j), de = comp(q[A1], j), sp = comp(q[A2], j);
+        if (!(de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu)))
+          A.fail(r0 + j, B2F_CODE_LOOKUP);
+      }
+    }
     __syncthreads();
     // ---- prefetch tile t + G into registers while tile t is checked
     const uint64_t tn = t + G;
@@ -514,16 +524,6 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
       uint32_t x = a.x ^ b.w ^ cur9.x ^ curfx.y ^ L[L_W + 4 * tid] ^ L[L_IC + (tid & 255)] ^
                    L[L_INFO + (tid & 15)] ^ T.at(A3, 4 * tid + 13);
       if (x == 0x12345678u) A.fail(0, B2F_CODE_LOOKUP);
-    }
-    // ---- lookups on the 4 rows (before the G table barrier: they need only the staged tile)
-    if ((MODE & EVAL_LOOKUP) && gq < total_quads) {
-      const uint4 q0 = T.quad(A0, lr0), q1 = T.quad(A1, lr0), q2 = T.quad(A2, lr0);
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        uint32_t tg = comp(q0, j), de = comp(q1, j), sp = comp(q2, j);
-        bool ok = de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu);
-        if (!ok) A.fail(row0 + j, B2F_CODE_LOOKUP);
-      }
     }
     if (MODE & (EVAL_GATES | EVAL_COPIES)) {
       // ---- G tables: the first wave builds the next tile's (from INFO2) while this tile is
