@@ -4,8 +4,9 @@
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
 
-One step = fill (record + fill kernels) then eval of the whole per-GPU batch; inputs and the
-trace stay resident in HBM. N > 1: every rank runs its own 2^18 shard (weak scaling); the
+One step = fill (record + fill kernels) then eval of the whole per-GPU batch (--path split, the
+headline; --path fused runs b2f_fill_eval_dev instead; the other path is timed beside it as
+"other_path"); inputs and the trace stay resident in HBM. N > 1: every rank runs its own 2^18 shard (weak scaling); the
 step ends with one all_reduce of the verdict counters and one RCCL all_gather of the h'
 outputs. Rank 0 prints one JSON line.
 """
@@ -75,6 +76,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--export-rows", type=int, default=1 << 25,
                     help="rows of the Fp export timed after the headline loop (0 = skip)")
+    ap.add_argument("--path", choices=["split", "fused"], default="split",
+                    help="split: fill kernel then eval kernel (the headline); fused: "
+                         "b2f_fill_eval_dev, one kernel that checks each tile as it assigns it")
+    ap.add_argument("--aux-steps", type=int, default=5,
+                    help="steps of the other path timed after the headline loop (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
     args = ap.parse_args()
@@ -107,9 +113,15 @@ def main():
         gathered = torch.empty((world * n, 8), dtype=torch.int64, device=batch.h_out.device)
         verdict = torch.empty(20, dtype=torch.int64, device=batch.h_out.device)
 
+    def run_path(path):
+        if path == "fused":
+            batch.fill_evaluate(eng, stream)
+        else:
+            batch.fill(eng, stream)
+            batch.evaluate(eng, stream)
+
     def step():
-        batch.fill(eng, stream)
-        batch.evaluate(eng, stream)
+        run_path(args.path)
         if world > 1:
             r = batch.report.view(torch.int64)
             verdict[:18].copy_(r[:18])
@@ -155,16 +167,25 @@ def main():
     # roofline: algorithmic bytes per launch / average launch duration (HIP events)
     fill_bytes = n * INPUT_BYTES + rows * ROW_BYTES      # inputs read + trace written
     eval_bytes = rows * ROW_BYTES + 8 * (n + 1)          # trace + offsets read
-    kern = {}
-    for name, nbytes in (("fill", fill_bytes), ("eval", eval_bytes), ("record", None)):
-        tot, cnt = ktimes[name]
-        avg = tot / max(cnt, 1)
-        kern[name] = {"avg_ms": round(avg, 4), "launches": cnt}
-        if nbytes:
-            gbs = nbytes / (avg * 1e-3) / 1e9
-            kern[name].update({"bytes_per_launch": nbytes, "achieved_GBs": round(gbs, 1),
-                               "frac": round(gbs / HBM_PEAK_GBS, 4)})
-    dom = "eval" if kern["eval"]["avg_ms"] >= kern["fill"]["avg_ms"] else "fill"
+
+    def kernel_table(ktimes):
+        kern = {}
+        for name, nbytes in (("fill", fill_bytes), ("eval", eval_bytes),
+                             ("fill_eval", fill_bytes), ("record", None)):
+            tot, cnt = ktimes[name]
+            if not cnt:
+                continue
+            avg = tot / cnt
+            kern[name] = {"avg_ms": round(avg, 4), "launches": cnt}
+            if nbytes:
+                gbs = nbytes / (avg * 1e-3) / 1e9
+                kern[name].update({"bytes_per_launch": nbytes, "achieved_GBs": round(gbs, 1),
+                                   "frac": round(gbs / HBM_PEAK_GBS, 4)})
+        return kern
+
+    kern = kernel_table(ktimes)
+    big = [k for k in kern if k != "record"]
+    dom = max(big, key=lambda k: kern[k]["avg_ms"])
     traffic = None
     try:
         with open(args.traffic) as fh:
@@ -175,6 +196,26 @@ def main():
         pass
     roof = {"bound": "hbm", "achieved": kern[dom]["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": kern[dom]["frac"], "traffic": traffic, "kernel": dom}
+
+    # the other path, timed the same way (reported beside the headline, not part of it)
+    aux = None
+    other = "fused" if args.path == "split" else "split"
+    if args.aux_steps > 0 and world == 1:
+        run_path(other)
+        eng.sync(stream)
+        eng.set_timing(True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.aux_steps):
+            run_path(other)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t1
+        k2 = kernel_table(eng.kernel_times())
+        eng.sync(stream)
+        r2 = batch.report_dict()
+        aux = {"path": other, "value": round(n * args.aux_steps / el, 1),
+               "ms_per_step": round(1e3 * el / args.aux_steps, 4), "kernels": k2,
+               "verdict_clean": r2["first_failure"] == 2**64 - 1}
 
     # Fp export, reported beside the headline, not part of it:
     # Montgomery pallas limbs for a chunk of the resident trace (4 B read, 32 B written/cell)
@@ -213,8 +254,10 @@ def main():
                "config": {"workload": workload, "batch_per_gpu": n,
                           "rounds": "mix{1,4,12}" if mix else args.rounds,
                           "rows_per_gpu": rows, "trace_bytes_per_gpu": rows * ROW_BYTES,
+                          "path": args.path,
                           "parallelism": "dp%d (instance shards)" % world},
-               "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "fp_export": fp_export,
+               "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "other_path": aux,
+               "fp_export": fp_export,
                "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None}
         print(json.dumps(out), flush=True)
     if world > 1:

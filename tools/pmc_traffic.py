@@ -25,7 +25,8 @@ def per_kernel(d, counter):
             if r["Counter_Name"] != counter:
                 continue
             k = r["Kernel_Name"]
-            kind = "fill" if "fill_kernel" in k else "eval" if "eval_kernel" in k else None
+            kind = ("fill" if "fill_kernel" in k else "eval" if "eval_kernel" in k
+                    else "fill_eval" if "fused_kernel" in k else None)
             if kind is None:
                 continue
             per_dispatch[r["Dispatch_Id"]] += float(r["Counter_Value"])
@@ -41,7 +42,7 @@ def main():
     fetch = per_kernel(fetch_dir, "FETCH_SIZE")
     write = per_kernel(write_dir, "WRITE_SIZE")
     res = json.load(open(out)) if os.path.exists(out) else {}
-    for kind in ("fill", "eval"):
+    for kind in ("fill", "eval", "fill_eval"):
         if kind not in fetch or kind not in write:
             continue
         fb = 2.0 * fetch[kind] * 1024  # gfx950: FETCH_SIZE reads half of a wide stream
