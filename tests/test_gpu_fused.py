@@ -195,3 +195,35 @@ def test_fused_mixed_rounds_2p14(engine, orc):
         assert np.array_equal(batch.fixed[r0:r1].cpu().numpy().view(np.uint32), ofixed)
         assert np.array_equal(h_out[s:e], oh)
     del b2f
+
+
+def test_2p18_mixed_split_equals_fused(engine, orc):
+    """BASELINE config 5 at full size (2^18, rounds in {1, 4, 12}) through size-independent
+    properties: both paths' verdicts are clean, the fused trace and h' equal the split path's
+    bit for bit (compared on the device), and h' of a sample of instances equals the oracle's
+    BLAKE2f compression."""
+    import b2f
+    import torch
+
+    from b2f import synth
+
+    n = 1 << 18
+    x = synth.batch(n, rounds_mix=[1, 4, 12])
+    a = b2f.DeviceBatch(x)
+    a.fill(engine)
+    a.evaluate(engine)
+    engine.sync(_stream())
+    ra = a.report_dict()
+    assert ra["first_failure"] == NONE and sum(ra["gate_failures"]) == 0
+    adv, fx, h = a.advice.clone(), a.fixed.clone(), a.h_out.clone()
+    a.fill_evaluate(engine)
+    engine.sync(_stream())
+    assert a.report_dict() == ra
+    assert torch.equal(a.advice, adv) and torch.equal(a.fixed, fx) and torch.equal(a.h_out, h)
+    del adv, fx
+    rng = np.random.default_rng(50)
+    h_host = h.cpu().numpy().view(np.uint64)
+    for i in rng.integers(0, n, 256):
+        r = x[int(i)]
+        ref = orc.compress(int(r["rounds"]), r["h"], r["m"], r["t"], int(r["f"]))
+        assert np.array_equal(h_host[int(i)], ref), int(i)

@@ -993,6 +993,83 @@ __device__ __forceinline__ uint32_t g_xor63(const Tile& T, uint32_t r, uint32_t 
   return ((b2 ? 0u : 1u << S_B2) | (ijkl ? 0u : 1u << S_IJKL)) & sel;
 }
 
+// ---------------------------------------------------------------- per-tile G table
+// The G table of a tile (one wave, lane l = l-th G in row order whose start lies in
+// [base0 + shift - 51, base0 + shift + 1023]): per G its window / init-cache bases, message
+// rows, tile-local start and check-table row (g_pass / g_copies), plus QM[q] = position of
+// quad q in its G (0xff: not a round quad). base0 is the row of LDS coordinate 0 (eval: the
+// tile's first row; fused: 16 rows before it). The cached instances are walked in order (one
+// or two for 12-round instances; a lane-parallel walk with readlane broadcasts measured
+// slower). Init-region bases point into the init cache for the
+// tile's first instance (its init region may lie before the window) and into the window for
+// any later instance (which starts inside the tile). Instances past the cached eight cannot
+// occur in a valid layout (each is >= 228 rows); invalid layouts are flagged elsewhere
+// (offsets_check_kernel / the record kernel) and only have to stay in bounds here.
+struct GTCarve {
+  int qm, ng, gt;  // offsets inside the G set: QM bytes, entry count, entries
+  int ic, w, ws;   // LDS: init cache, window base, window stride
+  int qm_words, nq;
+  int shift;
+  int max_g;
+};
+__device__ __forceinline__ void build_g_table(uint32_t* S, const uint32_t* info, const uint8_t* Sg,
+                                              int64_t base0, uint32_t n, uint64_t total_rows,
+                                              uint32_t lane, const GTCarve& K) {
+  // one wave: its lanes reset QM, then mark their G's quads (LDS order within a wave)
+  if ((int)lane < K.qm_words) S[K.qm + lane] = 0xffffffffu;
+  if (lane == 0 && K.qm_words > 64) S[K.qm + 64] = 0xffffffffu;
+  const uint32_t first = info[0];
+  const uint64_t* Off = reinterpret_cast<const uint64_t*>(info + 2);
+  const int64_t lo = base0 + K.shift - (G_ROWS - 1), hi = base0 + K.shift + TILE_ROWS - 1;
+  uint32_t base = 0, m = 0;
+  int64_t o_mine = -1;
+  bool ofst = false;
+  for (int i = 0; i + 1 < NOFF; i++) {
+    if (first + (uint32_t)i >= n) break;
+    const uint64_t o = Off[i], o1 = Off[i + 1];
+    if ((int64_t)o > hi) break;
+    if (o1 <= o || o1 > total_rows || o1 - o > MAX_INSTANCE_ROWS) continue;
+    const uint32_t R = (uint32_t)(o1 - o);
+    if (R < FIXED_ROWS || (R - FIXED_ROWS) % ROUND_ROWS) continue;
+    const uint32_t n_g = 8 * ((R - FIXED_ROWS) / ROUND_ROWS);
+    // G m starts at g0 + 52 m; o > base0 - MAX_INSTANCE_ROWS, so these fit in 32 bits
+    const int64_t g0 = (int64_t)o + INIT_ROWS;
+    const int b = (int)(hi - g0);
+    if (n_g == 0 || b < 0) continue;
+    const int a = (int)(lo - g0);
+    const uint32_t m_lo = a <= 0 ? 0u : ((uint32_t)a + G_ROWS - 1) / G_ROWS;
+    uint32_t m_hi = (uint32_t)b / G_ROWS;
+    if (m_hi >= n_g) m_hi = n_g - 1;
+    if (m_lo > m_hi) continue;
+    const uint32_t cnt = m_hi - m_lo + 1;
+    if (o_mine < 0 && lane >= base && lane < base + cnt) {
+      o_mine = (int64_t)o;
+      m = m_lo + (lane - base);
+      ofst = i == 0;
+    }
+    base += cnt;
+  }
+  if (lane == 0) S[K.ng] = base < (uint32_t)K.max_g ? base : (uint32_t)K.max_g;
+  if (o_mine < 0 || lane >= (uint32_t)K.max_g) return;
+  const uint32_t r = m >> 3, g = m & 7u;
+  const int gl = (int)(o_mine + INIT_ROWS + (int64_t)G_ROWS * m - base0);
+  const int ob = ofst ? 0 : (int)(o_mine - base0 + HIST);  // later instances: in the window
+  const int ib0 = ofst ? K.ic : K.w + ob;
+  const int ib1 = ofst ? K.ic + (int)INIT_ROWS : K.w + K.ws + ob;
+  const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
+  uint32_t* gt = S + K.gt + GT_WORDS_ * lane;
+  *reinterpret_cast<uint4*>(gt) = make_uint4((uint32_t)(gl + HIST - CBIAS), (uint32_t)ib0,
+                                             (uint32_t)ib1, (uint32_t)(ib0 + 32 + 4 * sg[0]));
+  *reinterpret_cast<uint4*>(gt + 4) = make_uint4((uint32_t)(ib0 + 32 + 4 * sg[1]), (uint32_t)gl,
+                                                 (m < 4 ? 8 + g : g) * G_CHECKS, 0u);
+  uint8_t* qm = reinterpret_cast<uint8_t*>(S + K.qm);
+#pragma unroll
+  for (int p = 0; p < (int)G_QUADS; p++) {
+    const int q = (gl >> 2) + p;
+    if (q >= 0 && q < K.nq) qm[q] = (uint8_t)p;
+  }
+}
+
 // ---------------------------------------------------------------- per-tile G pass and copies
 // Shared by eval_kernel (check rows = selector rows / operand rows in [0, 1024) of the tile)
 // and fused_kernel (u coordinates: a block is checked where its last row lands, u in

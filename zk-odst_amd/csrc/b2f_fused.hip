@@ -132,66 +132,7 @@ __device__ __forceinline__ void build_quad(Quad& Q, const QuadOps& P, uint64_t g
   }
 }
 
-// G table of the check rows [base0 + 16, base0 + 1040) (the eval's build_g_table on u
-// coordinates): lane l = l-th G whose start lies in [base0 + 16 - 51, base0 + 1039].
-__device__ __forceinline__ void build_g_table_f(uint32_t* S, const uint32_t* info,
-                                                const uint8_t* Sg, int64_t base0, uint32_t n,
-                                                uint64_t total_rows, uint32_t lane) {
-  S[FS_QM + lane] = 0xffffffffu;
-  if (lane == 0) S[FS_QM + 64] = 0xffffffffu;
-  const uint32_t first = info[0];
-  const uint64_t* Off = reinterpret_cast<const uint64_t*>(info + 2);
-  const int64_t lo = base0 + SHIFT - (G_ROWS - 1), hi = base0 + U_END - 1;
-  uint32_t base = 0, m = 0;
-  int64_t o_mine = -1;
-  bool ofst = false;
-  for (int i = 0; i + 1 < NOFF; i++) {
-    if (first + (uint32_t)i >= n) break;
-    const uint64_t o = Off[i], o1 = Off[i + 1];
-    if ((int64_t)o > hi) break;
-    if (o1 <= o || o1 > total_rows || o1 - o > MAX_INSTANCE_ROWS) continue;
-    const uint32_t R = (uint32_t)(o1 - o);
-    if (R < FIXED_ROWS || (R - FIXED_ROWS) % ROUND_ROWS) continue;
-    const uint32_t n_g = 8 * ((R - FIXED_ROWS) / ROUND_ROWS);
-    const int64_t g0 = (int64_t)o + INIT_ROWS;
-    const int b = (int)(hi - g0);
-    if (n_g == 0 || b < 0) continue;
-    const int a = (int)(lo - g0);
-    const uint32_t m_lo = a <= 0 ? 0u : ((uint32_t)a + G_ROWS - 1) / G_ROWS;
-    uint32_t m_hi = (uint32_t)b / G_ROWS;
-    if (m_hi >= n_g) m_hi = n_g - 1;
-    if (m_lo > m_hi) continue;
-    const uint32_t cnt = m_hi - m_lo + 1;
-    if (o_mine < 0 && lane >= base && lane < base + cnt) {
-      o_mine = (int64_t)o;
-      m = m_lo + (lane - base);
-      ofst = i == 0;
-    }
-    base += cnt;
-  }
-  if (lane == 0) S[FS_NG] = base < (uint32_t)F_MAX_G ? base : (uint32_t)F_MAX_G;
-  if (o_mine < 0 || lane >= (uint32_t)F_MAX_G) return;
-  const uint32_t r = m >> 3, g = m & 7u;
-  const int gl = (int)(o_mine + INIT_ROWS + (int64_t)G_ROWS * m - base0);
-  const int ob = ofst ? 0 : (int)(o_mine - base0 + HIST);  // later instances: in the window
-  const int ib0 = ofst ? F_IC : F_W + ob;
-  const int ib1 = ofst ? F_IC + (int)INIT_ROWS : F_W + F_WS + ob;
-  const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
-  uint32_t* gt = S + FS_GT + F_GT_WORDS * lane;
-  gt[0] = (uint32_t)(gl + HIST - CBIAS);
-  gt[1] = (uint32_t)ib0;
-  gt[2] = (uint32_t)ib1;
-  gt[3] = (uint32_t)(ib0 + 32 + 4 * sg[0]);
-  gt[4] = (uint32_t)(ib0 + 32 + 4 * sg[1]);
-  gt[5] = (uint32_t)gl;
-  gt[6] = (m < 4 ? 8 + g : g) * G_CHECKS;
-  uint8_t* qm = reinterpret_cast<uint8_t*>(S + FS_QM);
-#pragma unroll
-  for (int p = 0; p < (int)G_QUADS; p++) {
-    const int q = (gl >> 2) + p;
-    if (q >= 0 && q < NQ) qm[q] = (uint8_t)p;
-  }
-}
+constexpr GTCarve kFusedGT{FS_QM, FS_NG, FS_GT, F_IC, F_W, F_WS, (NQ + 3) / 4, NQ, SHIFT, F_MAX_G};
 
 // Per-quad gates of a selector quad the G pass does not take (init/final blocks, any
 // non-canonical selector row): the gates of rows r0..r0+3 whose last row is in [lo, hi).
@@ -232,7 +173,8 @@ __device__ __forceinline__ void sts4(uint32_t* L, int w, const uint4& v) {
 // MODE: FZ_LOOKUP / FZ_GATES / FZ_COPIES which checks run, FZ_STORE write the trace to HBM,
 // FZ_INJECT the test-only fault injection. Product launches: FZ_FULL (diagnostic
 // variants via B2F_DIAG_FUSED).
-enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16, FZ_FULL = 27 };
+enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16, FZ_FULL = 27,
+       FZ_NOSTAGE = 32, FZ_NOGT = 64 };  // 32, 64: assignment-only diagnostics (no checks)
 
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK, B2F_FUSED_WAVES)
@@ -290,7 +232,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     quad_ops(P, 4 * (t * BLOCK + tid), info[0], Off, n, used_rows, in, rec, Sg);
     if (tid < (int)INIT_QUADS && info[0] < n) icw = init_word(in + info[0], tid);
     if (tid < 64)
-      build_g_table_f(L + F_GS, info, Sg, (int64_t)(t * TILE_ROWS) - SHIFT, n, total_rows, tid);
+      build_g_table(L + F_GS, info, Sg, (int64_t)(t * TILE_ROWS) - SHIFT, n, total_rows, tid, kFusedGT);
   }
   bool ic_now = true;  // the first tile of a band always (re)builds the init cache
   for (uint64_t i = 0; t < n_tiles; i++, t = seq(i)) {
@@ -381,6 +323,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     const uint32_t own_lq = P.lq, own_rounds = P.rounds;
     const uint4 fx = make_uint4(Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]);
     const uint4 a9 = make_uint4(Q.c[A9][0], Q.c[A9][1], Q.c[A9][2], Q.c[A9][3]);
+    if (!(MODE & FZ_NOSTAGE)) {
     if (!band_start && tid >= (TILE_ROWS - HIST) / 4 - SHIFT / 4) {
       // the rows this thread is about to overwrite become the history window (u - 1024)
 #pragma unroll
@@ -405,6 +348,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     sts4(L, F_G + 4 * F_TS + u0, make_uint4(Q.c[A6][0], Q.c[A6][1], Q.c[A6][2], Q.c[A6][3]));
     L[F_QSEL + SHIFT / 4 + tid] = (fx.x & 0xffffu) | (((fx.y | fx.z | fx.w) & 0xffffu) ? 1u << 16 : 0u);
     L[F_A9 + SHIFT / 4 + tid] = a9.x;
+    }
     if ((MODE & FZ_STORE) && gq < total_quads) {
 #pragma unroll
       for (int c = 0; c < 11; c++) {
@@ -424,9 +368,9 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     __syncthreads();
 
     // ---- C. build the next tile's G table, check this tile
-    if (has_next && (tid >> 6) == GT_WAVE)
-      build_g_table_f(L + F_GS + nxt * FSET, ninfo, Sg, (int64_t)(tn * TILE_ROWS) - SHIFT, n,
-                      total_rows, (uint32_t)tid & 63u);
+    if (!(MODE & FZ_NOGT) && has_next && (tid >> 6) == GT_WAVE)
+      build_g_table(L + F_GS + nxt * FSET, ninfo, Sg, (int64_t)(tn * TILE_ROWS) - SHIFT, n,
+                    total_rows, (uint32_t)tid & 63u, kFusedGT);
     const uint32_t* S = L + F_GS + cur * FSET;
     if ((MODE & FZ_LOOKUP) && gq < total_quads) {
       // the staged cells of this thread's rows (LDS, as every other check reads them)
@@ -513,6 +457,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                        n_tiles, band, d_rep, d_status, inj);                                  \
     break;
     B2F_FUSED(0) B2F_FUSED(2) B2F_FUSED(3) B2F_FUSED(10) B2F_FUSED(18) B2F_FUSED(8) B2F_FUSED(16)
+    B2F_FUSED(34) B2F_FUSED(66) B2F_FUSED(98)
     B2F_FUSED(FZ_FULL | FZ_INJECT)
     default: B2F_FUSED(FZ_FULL)
 #undef B2F_FUSED

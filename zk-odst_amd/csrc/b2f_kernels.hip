@@ -294,75 +294,7 @@ __device__ __forceinline__ int lds_cell(int c, int r) {
 }
 
 
-// G table of a tile (first wave, lane l = l-th G in row order whose start lies in
-// [tile0 - 51, tile0 + 1023], over the instances cached in INFO). GT words:
-//   0 window base of the G start - CBIAS     1, 2 init-region base of a_1, a_2
-//   3, 4 message x / y row bases             5 G start, tile-local      6 check-table row
-// Init-region bases point into the init cache for the tile's first instance (its init region
-// may lie before the window) and into the window for any later instance (which starts inside
-// the tile, so its init region is in the window). QM[q] = position of quad q in its G.
-// Instances past the cached eight cannot occur in a valid layout (each is >= 228 rows);
-// b2f_eval_dev flags invalid layouts separately (offsets_check_kernel).
-__device__ __forceinline__ void build_g_table(uint32_t* S, const uint32_t* info, const uint8_t* Sg,
-                                              uint64_t tile0, uint32_t n, uint64_t total_rows,
-                                              uint32_t lane) {
-  // one wave: its lanes reset QM, then mark their G's quads (LDS order within a wave)
-  S[GS_QM + lane] = 0xffffffffu;
-  const uint32_t first = info[0];
-  const uint64_t* Off = reinterpret_cast<const uint64_t*>(info + 2);
-  const int64_t lo = (int64_t)tile0 - (G_ROWS - 1), hi = (int64_t)tile0 + TILE_ROWS - 1;
-  uint32_t base = 0, m = 0;
-  int64_t o_mine = -1;
-  bool ofst = false;
-  for (int i = 0; i + 1 < NOFF; i++) {
-    if (first + (uint32_t)i >= n) break;
-    const uint64_t o = Off[i], o1 = Off[i + 1];
-    if ((int64_t)o > hi) break;
-    if (o1 <= o || o1 > total_rows || o1 - o > MAX_INSTANCE_ROWS) continue;
-    const uint32_t R = (uint32_t)(o1 - o);
-    if (R < FIXED_ROWS || (R - FIXED_ROWS) % ROUND_ROWS) continue;
-    const uint32_t n_g = 8 * ((R - FIXED_ROWS) / ROUND_ROWS);
-    // G m starts at g0 + 52 m; o > tile0 - MAX_INSTANCE_ROWS, so these fit in 32 bits
-    const int64_t g0 = (int64_t)o + INIT_ROWS;
-    const int b = (int)(hi - g0);
-    if (n_g == 0 || b < 0) continue;
-    const int a = (int)(lo - g0);
-    const uint32_t m_lo = a <= 0 ? 0u : ((uint32_t)a + G_ROWS - 1) / G_ROWS;
-    uint32_t m_hi = (uint32_t)b / G_ROWS;
-    if (m_hi >= n_g) m_hi = n_g - 1;
-    if (m_lo > m_hi) continue;
-    const uint32_t cnt = m_hi - m_lo + 1;
-    if (o_mine < 0 && lane >= base && lane < base + cnt) {
-      o_mine = (int64_t)o;
-      m = m_lo + (lane - base);
-      ofst = i == 0;
-    }
-    base += cnt;
-  }
-  if (lane == 0) S[GS_NG] = base < (uint32_t)MAX_TILE_G ? base : (uint32_t)MAX_TILE_G;
-  if (o_mine < 0 || lane >= (uint32_t)MAX_TILE_G) return;
-  const uint32_t r = m >> 3, g = m & 7u;
-  const int gl = (int)(o_mine + INIT_ROWS + (int64_t)G_ROWS * m - (int64_t)tile0);
-  const int64_t ob64 = o_mine - (int64_t)tile0 + HIST;  // instance start, window index
-  const int ob = ofst ? 0 : (int)ob64;                    // (later instances: in the window)
-  const int ib0 = ofst ? L_IC : L_W + ob;
-  const int ib1 = ofst ? L_IC + (int)INIT_ROWS : L_W + WSTRIDE + ob;
-  const uint8_t* sg = Sg + 16 * (r % 10) + 2 * g;
-  uint32_t* gt = S + GS_GT + GT_WORDS * lane;
-  gt[0] = (uint32_t)(gl + HIST - CBIAS);
-  gt[1] = (uint32_t)ib0;
-  gt[2] = (uint32_t)ib1;
-  gt[3] = (uint32_t)(ib0 + 32 + 4 * sg[0]);
-  gt[4] = (uint32_t)(ib0 + 32 + 4 * sg[1]);
-  gt[5] = (uint32_t)gl;
-  gt[6] = (m < 4 ? 8 + g : g) * G_CHECKS;
-  uint8_t* qm = reinterpret_cast<uint8_t*>(S + GS_QM);
-#pragma unroll
-  for (int p = 0; p < (int)G_QUADS; p++) {
-    int q = (gl >> 2) + p;
-    if (q >= 0 && q < BLOCK) qm[q] = (uint8_t)p;
-  }
-}
+constexpr GTCarve kEvalGT{GS_QM, GS_NG, GS_GT, L_IC, L_W, WSTRIDE, BLOCK / 4, BLOCK, 0, MAX_TILE_G};
 
 // MODE (diagnostics; the product uses EVAL_FULL): which checks run on a staged tile.
 enum { EVAL_LOOKUP = 1, EVAL_GATES = 2, EVAL_COPIES = 4, EVAL_FULL = 7, EVAL_TOUCH = 8 };
@@ -531,12 +463,13 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
       const uint32_t* S = L + L_GS + (iter & 1) * GSET;
       uint32_t* Sn = L + L_GS + ((iter + 1) & 1) * GSET;
       if (iter == 0) {  // nothing was built ahead for the first tile
-        if (tid < 64) build_g_table(L + L_GS, L + L_INFO, Sg, tile0, n, total_rows, (uint32_t)tid);
+        if (tid < 64)
+          build_g_table(L + L_GS, L + L_INFO, Sg, (int64_t)tile0, n, total_rows, (uint32_t)tid, kEvalGT);
         __syncthreads();
       }
       if ((tid >> 6) == GT_WAVE)  // the wave with the lightest G pass (XOR) builds ahead
-        build_g_table(Sn, L + L_INFO2, Sg, (t + G) * TILE_ROWS, t + G < n_tiles ? n : 0,
-                      total_rows, (uint32_t)tid & 63u);
+        build_g_table(Sn, L + L_INFO2, Sg, (int64_t)((t + G) * TILE_ROWS), t + G < n_tiles ? n : 0,
+                      total_rows, (uint32_t)tid & 63u, kEvalGT);
       const GCarve C{L_QSEL, L_A9, L_CT, L_G, TSTRIDE, 0, TILE_ROWS, false};
       const uint32_t ng = S[GS_NG];
       if (MODE & EVAL_GATES)
@@ -684,6 +617,14 @@ void timed_end(b2f_ctx* ctx, int i, hipStream_t s) {
 int diag_mode(const char* var, int full) {
   const char* v = getenv(var);
   return v ? atoi(v) : full;
+}
+
+// B2F_DIAG_FUSED: only the product variant (27) and the diagnostic ones that skip every check
+// (0, 2, 3, 10, 18, 8, 16, 34, 66, 98) are accepted; anything else runs the product kernel.
+int fused_mode() {
+  const int m = diag_mode("B2F_DIAG_FUSED", 27);
+  const bool safe = m == 27 || ((m & ~(1 | 2 | 8 | 16 | 32 | 64)) == 0 && ((m & (32 | 64)) == 0 || (m & 25) == 0));
+  return safe ? m : 27;
 }
 
 uint64_t layout_rows(uint32_t rounds) {
@@ -898,7 +839,7 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
   HIPCHK(ctx, launch_fill_eval(d_in, (uint32_t)n, d_offsets, total_rows, ctx->d_rec, d_advice,
                                d_fixed, ctx->d_tiles, nt, band, d_report, ctx->d_status,
                                ctx->inj_row, ctx->inj_col, ctx->inj_mask,
-                               diag_mode("B2F_DIAG_FUSED", 27), ctx->cu_count, s));
+                               fused_mode(), ctx->cu_count, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
