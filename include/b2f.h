@@ -134,6 +134,12 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
  * fused verdict equals b2f_eval_dev's / the oracle's on the trace actually written. */
 B2F_API int b2f_debug_inject(b2f_ctx* ctx, uint64_t row, uint32_t col, uint32_t mask);
 
+/* Diagnostics: eval-kernel phase cycle totals (s_memtime deltas summed over workgroups) of
+ * the B2F_DIAG_EVAL=23 (EVAL_CLOCK) variant since the previous call; out[8 * wave + phase],
+ * phases: stage+lookups, barrier 1, prefetch issue, G-table build, gate pass, copies,
+ * per-quad paths, barrier 2. Zeros when that variant never ran. Clears the totals. */
+B2F_API int b2f_debug_clock(b2f_ctx* ctx, uint64_t* out);
+
 /* Wait for `stream` and return the first device-side error of the fill/eval calls issued
  * since the previous b2f_sync (B2F_ERR_LAYOUT / B2F_ERR_ROUNDS), then clear it. */
 B2F_API int b2f_sync(b2f_ctx* ctx, void* stream);

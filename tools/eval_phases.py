@@ -1,0 +1,47 @@
+"""Eval-kernel phase breakdown (diagnostics): runs the EVAL_CLOCK variant (B2F_DIAG_EVAL=23)
+on a 2^18 x 12-round batch and prints, per wave of the workgroup, the share of s_memtime
+cycles spent in each phase of the tile loop. python tools/eval_phases.py [--batch N]"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "zk-odst_amd"))
+PHASES = ["stage+lookup", "barrier1", "prefetch", "gtable", "gpass", "copies", "perquad", "barrier2"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1 << 18)
+    args = ap.parse_args()
+    import torch
+
+    import b2f
+    from b2f import synth
+
+    x = synth.batch(args.batch, rounds=12)
+    batch = b2f.DeviceBatch(x)
+    eng = b2f.Engine(0)
+    s = torch.cuda.current_stream().cuda_stream
+    batch.fill(eng, s)
+    os.environ["B2F_DIAG_EVAL"] = "23"
+    batch.evaluate(eng, s)
+    eng.sync(s)
+    out = (ctypes.c_uint64 * 32)()
+    eng._check(eng.lib.b2f_debug_clock(eng.ctx, out))  # clear
+    eng.set_timing(True)
+    batch.evaluate(eng, s)
+    eng.sync(s)
+    ms = eng.kernel_times()["eval"][0]
+    eng._check(eng.lib.b2f_debug_clock(eng.ctx, out))
+    rep = batch.report_dict()
+    print("eval (clocked variant) %.3f ms, verdict clean: %s" % (ms, rep["first_failure"] == 2**64 - 1))
+    for w in range(4):
+        row = [out[8 * w + k] for k in range(8)]
+        tot = sum(row) or 1
+        print("wave %d: " % w + "  ".join("%s %4.1f%%" % (PHASES[k], 100.0 * row[k] / tot) for k in range(8)))
+
+
+if __name__ == "__main__":
+    main()

@@ -67,6 +67,7 @@ SIGNATURES = [
     ("b2f_eval_dev", I32, [P, P, P, P, SIZE, U64, P, P]),
     ("b2f_fill_eval_dev", I32, [P, P, SIZE, P, U64, P, P, P, P, P]),
     ("b2f_debug_inject", I32, [P, U64, ctypes.c_uint32, ctypes.c_uint32]),
+    ("b2f_debug_clock", I32, [P, P]),
     ("b2f_export_fp_dev", I32, [P, P, U64, U64, U64, ctypes.c_uint32, P, U64, P]),
     ("b2f_sync", I32, [P, P]),
     ("b2f_fill", I32, [P, P, SIZE, P, P, P]),
@@ -74,6 +75,8 @@ SIGNATURES = [
     ("b2f_set_timing", I32, [P, I32]),
     ("b2f_kernel_times", I32, [P, P, P]),
 ]
+
+OPTIONAL = {"b2f_debug_clock"}
 
 _lib = None
 
@@ -103,6 +106,8 @@ def load():
     _share_hip_runtime_with_torch()
     lib = ctypes.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
+        if name in OPTIONAL and not hasattr(lib, name):
+            continue  # diagnostics entry point absent from an older build (A/B runs)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -149,8 +149,11 @@ enum { FILL_COMPUTE = 1, FILL_NT = 2, FILL_FULL = 3 };
 // with scalar loads and the operand words of tile t + grid (quad_ops) are loaded before tile
 // t's stores are issued (vmcnt counts loads and stores in issue order, so a load issued after
 // the stores would wait for them).
+#ifndef B2F_FILL_WAVES
+#define B2F_FILL_WAVES 1  // minimum waves per SIMD the fill is compiled for (register bound)
+#endif
 template <int MODE>
-__global__ void __launch_bounds__(BLOCK) fill_kernel(const b2f_input* __restrict__ in,
+__global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_input* __restrict__ in,
                                                     uint32_t n,
                                                     const uint64_t* __restrict__ off,
                                                     uint64_t total_rows,
@@ -297,7 +300,8 @@ __device__ __forceinline__ int lds_cell(int c, int r) {
 constexpr GTCarve kEvalGT{GS_QM, GS_NG, GS_GT, L_IC, L_W, WSTRIDE, BLOCK / 4, BLOCK, 0, MAX_TILE_G};
 
 // MODE (diagnostics; the product uses EVAL_FULL): which checks run on a staged tile.
-enum { EVAL_LOOKUP = 1, EVAL_GATES = 2, EVAL_COPIES = 4, EVAL_FULL = 7, EVAL_TOUCH = 8 };
+enum { EVAL_LOOKUP = 1, EVAL_GATES = 2, EVAL_COPIES = 4, EVAL_FULL = 7, EVAL_TOUCH = 8,
+       EVAL_CLOCK = 16 };  // EVAL_CLOCK: per-phase s_memtime totals per wave (diagnostics)
 
 // The two extra (non-own-quad) loads a thread issues per tile, as a compact descriptor:
 // kind, LDS destination, and a base pointer the tile position is added to.
@@ -375,8 +379,17 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
                                                     const TileInfo* __restrict__ tinfo,
                                                     uint64_t n_tiles,
                                                     b2f_eval_report* __restrict__ rep,
-                                                    int* __restrict__ status) {
+                                                    int* __restrict__ status,
+                                                    unsigned long long* __restrict__ clk) {
   __shared__ __attribute__((aligned(16))) uint32_t L[LDS_WORDS];
+  uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
+  auto tick = [&](int k) {
+    if (MODE & EVAL_CLOCK) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      if (k >= 0) ck[k] += now - tp;
+      tp = now;
+    }
+  };
   const int tid = threadIdx.x;
   for (int i = tid; i < CHECK_WORDS; i += BLOCK)
     L[L_CT + i] = reinterpret_cast<const uint32_t*>(&c_checks)[i];
@@ -400,8 +413,11 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
   // rows its same-XCD neighbours just loaded, served from that XCD's L2 rather than refetched
   // (placement is only a speed hint; any placement gives the same result).
   uint64_t t = (G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
-  // fo / fo_next (first instance and its offset, per tile) are workgroup-uniform: SGPRs
-  uint4 q[NCOL_T], x0 = make_uint4(0, 0, 0, 0), x1 = x0, fo = x0, fo_next = x0;
+  // fo (first instance and its offset, per tile) is workgroup-uniform. Only the first tile's
+  // is a scalar load; the next tiles' come from the staged TileInfo in LDS (INFO2): on CDNA
+  // lgkmcnt counts scalar loads and LDS operations together, so a scalar load issued in the
+  // tile loop would make the first LDS read of the checks wait for a memory round trip.
+  uint4 q[NCOL_T], x0 = make_uint4(0, 0, 0, 0), x1 = x0, fo = x0;
   const Extra e0 = make_extra(tid, adv, total_rows, tinfo);
   const Extra e1 = make_extra(tid + BLOCK, adv, total_rows, tinfo);
   auto load_tile = [&](uint64_t tt, const uint4& f) {
@@ -417,9 +433,9 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
   if (layout_ok && t < n_tiles) {
     fo = *reinterpret_cast<const uint4*>(tinfo + t);
     load_tile(t, fo);
-    if (t + G < n_tiles) fo_next = *reinterpret_cast<const uint4*>(tinfo + t + G);
   }
   for (uint32_t iter = 0; layout_ok && t < n_tiles; t += G, iter++) {
+    tick(-1);
     // ---- stage tile t: registers -> LDS
 #pragma unroll
     for (int c = 0; c < 9; c++) *reinterpret_cast<uint4*>(&L[lds_cell(c, 4 * tid)]) = q[c];
@@ -440,13 +456,17 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
           A.fail(r0 + j, B2F_CODE_LOOKUP);
       }
     }
+    tick(0);
     __syncthreads();
+    tick(1);
     // ---- prefetch tile t + G into registers while tile t is checked
     const uint64_t tn = t + G;
     if (tn < n_tiles) {
+      // TileInfo of tile tn = t + G, staged from the INFO2 slots this iteration
+      const uint4 fo_next = make_uint4(L[L_INFO2], 0u, L[L_INFO2 + 2], L[L_INFO2 + 3]);
       load_tile(tn, fo_next);
-      if (tn + G < n_tiles) fo_next = *reinterpret_cast<const uint4*>(tinfo + tn + G);
     }
+    tick(2);
     const uint64_t tile0 = t * TILE_ROWS;
     const uint64_t gq = t * BLOCK + tid;
     const uint64_t row0 = 4 * gq;
@@ -470,11 +490,14 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
       if ((tid >> 6) == GT_WAVE)  // the wave with the lightest G pass (XOR) builds ahead
         build_g_table(Sn, L + L_INFO2, Sg, (int64_t)((t + G) * TILE_ROWS), t + G < n_tiles ? n : 0,
                       total_rows, (uint32_t)tid & 63u, kEvalGT);
+      tick(3);
       const GCarve C{L_QSEL, L_A9, L_CT, L_G, TSTRIDE, 0, TILE_ROWS, false};
       const uint32_t ng = S[GS_NG];
       if (MODE & EVAL_GATES)
         g_pass(T, A, L, S + GS_GT, ng, (int64_t)tile0, (uint32_t)tid & 63u, (uint32_t)tid >> 6, C);
+      tick(4);
       if (MODE & EVAL_COPIES) g_copies(A, L, S + GS_GT, ng, (int64_t)tile0, (uint32_t)tid, C);
+      tick(5);
       // ---- per quad: selector rows the G pass does not take, and init/final-block copies
       if (gq < total_quads) {
         const uint32_t pq = reinterpret_cast<const uint8_t*>(S + GS_QM)[tid];
@@ -516,7 +539,13 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
         }
       }
     }
+    tick(6);
     __syncthreads();
+    tick(7);
+  }
+  if ((MODE & EVAL_CLOCK) && (tid & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) atomicAdd(&clk[8 * (tid >> 6) + k], (unsigned long long)ck[k]);
   }
   // ---- flush the workgroup's counters: one global atomic per non-zero counter
   __syncthreads();
@@ -571,6 +600,7 @@ struct b2f_ctx {
   std::vector<hipEvent_t> pool;  // event pairs, reused after every b2f_kernel_times
   std::vector<int> kinds;        // kernel kind of pair i
   int cu_count;
+  unsigned long long* d_clock;  // 32 u64: EVAL_CLOCK phase totals (diagnostics)
   uint64_t inj_row;    // b2f_debug_inject (UINT64_MAX: off)
   uint32_t inj_col, inj_mask;
 };
@@ -724,6 +754,7 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
   (void)hipFree(ctx->d_status);
   (void)hipFree(ctx->d_rec);
   (void)hipFree(ctx->d_tiles);
+  (void)hipFree(ctx->d_clock);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   delete ctx;
 }
@@ -803,7 +834,7 @@ B2F_API int b2f_fill_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const ui
   uint64_t nt = n_tiles_of(total_rows);
   rc = launch_tile_index(ctx, d_offsets, n, nt, s);
   if (rc) return rc;
-  uint32_t wgs = grid_for(ctx, nt, 8);
+  uint32_t wgs = grid_for(ctx, nt, diag_mode("B2F_FILL_WGS", 8));
   int tk = timed_begin(ctx, B2F_KERNEL_FILL, s);
   switch (diag_mode("B2F_DIAG_FILL", FILL_FULL)) {
 #define B2F_FILL(M)                                                                            \
@@ -844,6 +875,17 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
   return B2F_OK;
 }
 
+B2F_API int b2f_debug_clock(b2f_ctx* ctx, uint64_t* out) {
+  if (!ctx || !out) return B2F_ERR_ARG;
+  for (int i = 0; i < 32; i++) out[i] = 0;
+  if (!ctx->d_clock) return B2F_OK;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipDeviceSynchronize());
+  HIPCHK(ctx, hipMemcpy(out, ctx->d_clock, 32 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIPCHK(ctx, hipMemset(ctx->d_clock, 0, 32 * sizeof(uint64_t)));
+  return B2F_OK;
+}
+
 B2F_API int b2f_debug_inject(b2f_ctx* ctx, uint64_t row, uint32_t col, uint32_t mask) {
   if (!ctx) return B2F_ERR_ARG;
   if (row != UINT64_MAX && col > B2F_NUM_ADVICE)
@@ -876,15 +918,21 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
   int rc = launch_tile_index(ctx, d_offsets, n, nt, s);
   if (rc) return rc;
   uint32_t wgs = grid_for(ctx, nt, 3);
+  const int emode = diag_mode("B2F_DIAG_EVAL", EVAL_FULL);
+  if ((emode & EVAL_CLOCK) && !ctx->d_clock) {
+    HIPCHK(ctx, hipMalloc(&ctx->d_clock, 32 * sizeof(unsigned long long)));
+    HIPCHK(ctx, hipMemset(ctx->d_clock, 0, 32 * sizeof(unsigned long long)));
+  }
   int tk = timed_begin(ctx, B2F_KERNEL_EVAL, s);
-  switch (diag_mode("B2F_DIAG_EVAL", EVAL_FULL)) {
+  switch (emode) {
 #define B2F_EVAL(M)                                                                             \
   case M:                                                                                       \
     hipLaunchKernelGGL(eval_kernel<M>, dim3(wgs), dim3(BLOCK), 0, s, d_advice, d_fixed,         \
                        d_offsets, (uint32_t)n, total_rows, ctx->d_tiles, nt, d_report,          \
-                       ctx->d_status + 1);                                                      \
+                       ctx->d_status + 1, ctx->d_clock);                                        \
     break;
     B2F_EVAL(1) B2F_EVAL(2) B2F_EVAL(3) B2F_EVAL(4) B2F_EVAL(5) B2F_EVAL(6) B2F_EVAL(8)
+    B2F_EVAL(EVAL_FULL | EVAL_CLOCK)
     default: B2F_EVAL(7)
 #undef B2F_EVAL
   }
