@@ -36,13 +36,19 @@ def test_eval_clean_matches_oracle(engine, orc):
     assert sum(rep["gate_failures"]) == rep["lookup_failures"] == rep["copy_failures"] == 0
 
 
-def test_eval_corruptions_match_oracle(engine, orc):
-    """Flip cells all over the trace; the GPU verdict must equal the oracle's exactly."""
-    x = random_inputs(6, (0, 1, 2), 6)
+@pytest.mark.parametrize("rounds_choices,n,seed", [((0, 1, 2), 6, 6), ((0, 1, 4, 12), 14, 9)])
+def test_eval_corruptions_match_oracle(engine, orc, rounds_choices, n, seed):
+    """Flip cells all over the trace, and the copy sources in each tile's history window (rows
+    just before a tile starts); the GPU verdict must equal the oracle's exactly."""
+    x = random_inputs(n, rounds_choices, seed)
+    band = 1 if n < 10 else 2
     adv, fixed, h_out, off = engine.fill_host(x)
     rng = np.random.default_rng(7)
     total = adv.shape[1]
     cases = [(c, r) for c in range(10) for r in rng.integers(0, total, 40)]
+    if band > 1:  # copy sources in the carried history window: rows just before tile starts
+        cases += [(c, 1024 * t - d) for t in range(1, total // 1024) for d in (1, 7, 52, 170, 383)
+                  for c in (1, 2, 7, 8)]
     flagged = 0
     for c, r in cases:
         a2 = adv.copy()

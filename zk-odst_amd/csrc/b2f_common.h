@@ -1163,6 +1163,9 @@ __device__ __forceinline__ void g_pass(const Tile& T, EvalAcc& A, const uint32_t
 // entry once and then issuing its checks' LDS reads independently (source cell at per-G base
 // + table offset, operand cell at its row). A check belongs to the tile holding its operand row.
 constexpr int LPG = 10;
+#ifndef B2F_COPY_UNROLL
+#define B2F_COPY_UNROLL 4
+#endif
 #ifndef B2F_GT_WAVE
 #define B2F_GT_WAVE 1
 #endif
@@ -1174,7 +1177,7 @@ __device__ __forceinline__ void g_copies(EvalAcc& A, const uint32_t* L, const ui
   if (gi >= ng) return;
   const uint4 g0 = *reinterpret_cast<const uint4*>(gt_base + GT_WORDS_ * gi);
   const uint4 g1 = *reinterpret_cast<const uint4*>(gt_base + GT_WORDS_ * gi + 4);
-#pragma unroll 4
+#pragma unroll B2F_COPY_UNROLL
   for (int j = 0; j < (G_CHECKS + LPG - 1) / LPG; j++) {
     const uint32_t ci = c0 + LPG * j;
     if (ci >= (uint32_t)G_CHECKS) break;
