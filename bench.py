@@ -81,6 +81,8 @@ def main():
                          "b2f_fill_eval_dev, one kernel that checks each tile as it assigns it")
     ap.add_argument("--aux-steps", type=int, default=5,
                     help="steps of the other path timed after the headline loop (0 = skip)")
+    ap.add_argument("--floor-reps", type=int, default=3,
+                    help="launches of each diagnostic floor variant (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
     args = ap.parse_args()
@@ -197,6 +199,31 @@ def main():
     roof = {"bound": "hbm", "achieved": kern[dom]["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": kern[dom]["frac"], "traffic": traffic, "kernel": dom}
 
+    # same-box floors (diagnostic kernel variants, reported beside the headline): the fill with
+    # its stores but no cell computation (B2F_DIAG_FILL=2) and the eval with its loads, staging
+    # and lookups but no gates or copies (B2F_DIAG_EVAL=1). Boxes differ by up to ~25 % on the
+    # store-bound fill, so the achieved/floor ratio is the comparable number.
+    floors = None
+    if world == 1 and args.floor_reps > 0:
+        floors = {}
+        for var, val, kname in (("B2F_DIAG_FILL", "2", "fill"), ("B2F_DIAG_EVAL", "1", "eval")):
+            os.environ[var] = val
+            try:
+                eng.set_timing(True)
+                for _ in range(args.floor_reps):
+                    if kname == "fill":
+                        batch.fill(eng, stream)
+                    else:
+                        batch.evaluate(eng, stream)
+                tot, cnt = eng.kernel_times()[kname]
+            finally:
+                os.environ.pop(var, None)
+            floors[kname + "_floor_ms"] = round(tot / max(cnt, 1), 4)
+            floors[kname + "_over_floor"] = round(kern[kname]["avg_ms"] / (tot / max(cnt, 1)), 4) \
+                if kname in kern else None
+        batch.fill(eng, stream)  # leave a real trace behind
+        eng.sync(stream)
+
     # the other path, timed the same way (reported beside the headline, not part of it)
     aux = None
     other = "fused" if args.path == "split" else "split"
@@ -256,7 +283,8 @@ def main():
                           "rows_per_gpu": rows, "trace_bytes_per_gpu": rows * ROW_BYTES,
                           "path": args.path,
                           "parallelism": "dp%d (instance shards)" % world},
-               "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "other_path": aux,
+               "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "floors": floors,
+               "other_path": aux,
                "fp_export": fp_export,
                "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None}
         print(json.dumps(out), flush=True)
