@@ -14,6 +14,7 @@ PHASES = ["stage+lookup", "barrier1", "prefetch", "gtable", "gpass", "copies", "
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1 << 18)
+    ap.add_argument("--fused", action="store_true", help="the fused kernel (B2F_DIAG_FUSED=155)")
     args = ap.parse_args()
     import torch
 
@@ -25,18 +26,23 @@ def main():
     eng = b2f.Engine(0)
     s = torch.cuda.current_stream().cuda_stream
     batch.fill(eng, s)
-    os.environ["B2F_DIAG_EVAL"] = "23"
-    batch.evaluate(eng, s)
+    run = batch.fill_evaluate if args.fused else batch.evaluate
+    os.environ["B2F_DIAG_FUSED" if args.fused else "B2F_DIAG_EVAL"] = "155" if args.fused else "23"
+    if args.fused:
+        global PHASES
+        PHASES = ["loads+1", "band+ic", "assign+stage", "store", "ti+barrier1", "gtable",
+                  "lookup+gpass+copies", "perquad+barrier2"]
+    run(eng, s)
     eng.sync(s)
     out = (ctypes.c_uint64 * 32)()
     eng._check(eng.lib.b2f_debug_clock(eng.ctx, out))  # clear
     eng.set_timing(True)
-    batch.evaluate(eng, s)
+    run(eng, s)
     eng.sync(s)
-    ms = eng.kernel_times()["eval"][0]
+    ms = eng.kernel_times()["fill_eval" if args.fused else "eval"][0]
     eng._check(eng.lib.b2f_debug_clock(eng.ctx, out))
     rep = batch.report_dict()
-    print("eval (clocked variant) %.3f ms, verdict clean: %s" % (ms, rep["first_failure"] == 2**64 - 1))
+    print(("fused" if args.fused else "eval") + " (clocked variant) %.3f ms, verdict clean: %s" % (ms, rep["first_failure"] == 2**64 - 1))
     for w in range(4):
         row = [out[8 * w + k] for k in range(8)]
         tot = sum(row) or 1

@@ -174,7 +174,8 @@ __device__ __forceinline__ void sts4(uint32_t* L, int w, const uint4& v) {
 // FZ_INJECT the test-only fault injection. Product launches: FZ_FULL (diagnostic
 // variants via B2F_DIAG_FUSED).
 enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16, FZ_FULL = 27,
-       FZ_NOSTAGE = 32, FZ_NOGT = 64 };  // 32, 64: assignment-only diagnostics (no checks)
+       FZ_NOSTAGE = 32, FZ_NOGT = 64,  // 32, 64: assignment-only diagnostics (no checks)
+       FZ_CLOCK = 128 };  // per-phase s_memtime totals per wave (diagnostics, b2f_debug_clock)
 
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK, B2F_FUSED_WAVES)
@@ -182,8 +183,16 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
              uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
              uint32_t* __restrict__ fixed, const TileInfo* __restrict__ tinfo, uint64_t n_tiles,
              uint32_t band, b2f_eval_report* __restrict__ rep, const int* __restrict__ status,
-             Inject inj) {
+             Inject inj, unsigned long long* __restrict__ clk) {
   __shared__ __attribute__((aligned(16))) uint32_t L[F_WORDS];
+  uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
+  auto tick = [&](int k) {
+    if (MODE & FZ_CLOCK) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      if (k >= 0) ck[k] += now - tp;
+      tp = now;
+    }
+  };
   __shared__ uint32_t rows[ROW_TABLE_WORDS];
   const int tid = threadIdx.x;
   if (*status) return;  // the record kernel rejected the layout: write nothing
@@ -249,6 +258,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     const uint32_t* ninfo = info_of(i + 1);
     const uint32_t first = info[0];
 
+    tick(-1);
     // ---- A0. loads for tile i + 1
     QuadOps Pn;
     uint64_t icw_n = 0;
@@ -260,6 +270,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
       if (ic_next && tid < (int)INIT_QUADS && ninfo[0] < n) icw_n = init_word(in + ninfo[0], tid);
     }
 
+    tick(0);
     // ---- A1. first tile of a band: recompute rows [tile0 - 400, tile0) (history window and
     // the carried quads) from the previous tile's instance context
     if (band_start && tid < HIST_QUADS) {
@@ -317,6 +328,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
       sts4(L, F_IC + INIT_ROWS + 4 * tid, make_uint4(Qi.c[A2][0], Qi.c[A2][1], Qi.c[A2][2], Qi.c[A2][3]));
     }
 
+    tick(1);
     // ---- A3. assign the quad, check its lookups, stage it, store it
     Quad Q;
     build_quad<(MODE & FZ_INJECT) != 0>(Q, P, gq, rows, IV, inj);
@@ -349,6 +361,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     L[F_QSEL + SHIFT / 4 + tid] = (fx.x & 0xffffu) | (((fx.y | fx.z | fx.w) & 0xffffu) ? 1u << 16 : 0u);
     L[F_A9 + SHIFT / 4 + tid] = a9.x;
     }
+    tick(2);
     if ((MODE & FZ_STORE) && gq < total_quads) {
 #pragma unroll
       for (int c = 0; c < 11; c++) {
@@ -359,6 +372,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
       }
     }
 
+    tick(3);
     // ---- A4. TileInfo: stage the one of tile i + 2, load the one of tile i + 3
     if (tid < 6) {
       sts4(L, F_INFO + 24 * (uint32_t)((i + 2) % 3) + 4 * tid, ti);
@@ -366,12 +380,14 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
       ti = t3 < n_tiles ? reinterpret_cast<const uint4*>(tinfo + t3)[tid] : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
+    tick(4);
 
     // ---- C. build the next tile's G table, check this tile
     if (!(MODE & FZ_NOGT) && has_next && (tid >> 6) == GT_WAVE)
       build_g_table(L + F_GS + nxt * FSET, ninfo, Sg, (int64_t)(tn * TILE_ROWS) - SHIFT, n,
                     total_rows, (uint32_t)tid & 63u, kFusedGT);
     const uint32_t* S = L + F_GS + cur * FSET;
+    tick(5);
     if ((MODE & FZ_LOOKUP) && gq < total_quads) {
       // the staged cells of this thread's rows (LDS, as every other check reads them)
       const uint4 q0 = T.quad(A0, (uint32_t)u0), q1 = T.quad(A1, (uint32_t)u0), q2 = T.quad(A2, (uint32_t)u0);
@@ -386,6 +402,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     const uint32_t ng = S[FS_NG];
     if (MODE & FZ_GATES) g_pass(T, A, L, S + FS_GT, ng, base0, (uint32_t)tid & 63u, (uint32_t)tid >> 6, C);
     if (MODE & FZ_COPIES) g_copies(A, L, S + FS_GT, ng, base0, (uint32_t)tid, C);
+    tick(6);
     const int hi = last_tile ? U_END + F_HALO : U_END;
     if ((MODE & (FZ_GATES | FZ_COPIES)) && !canonical_quad(L, S, SHIFT / 4 + tid, fx)) {
       if (MODE & FZ_GATES) quad_gates_f(T, A, fx, a9, u0, SHIFT, hi, base0);
@@ -408,9 +425,14 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
       sts4(L, F_CAR + 16 + 4 * qc, a9);
     }
     __syncthreads();
+    tick(7);
     P = Pn;
     icw = icw_n;
     ic_now = ic_next;
+  }
+  if ((MODE & FZ_CLOCK) && (tid & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) atomicAdd(&clk[8 * (tid >> 6) + k], (unsigned long long)ck[k]);
   }
   // ---- flush the workgroup's counters: one global atomic per non-zero counter
   if (tid < 18) {
@@ -438,7 +460,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                             uint32_t* d_fixed, const void* tinfo, uint64_t n_tiles, uint32_t band,
                             b2f_eval_report* d_rep, const int* d_status, uint64_t inj_row,
                             uint32_t inj_col, uint32_t inj_mask, int mode, int cu_count,
-                            hipStream_t s) {
+                            unsigned long long* clk, hipStream_t s) {
   if (band == 0) band = 1;
   const uint64_t n_bands = (n_tiles + band - 1) / band;
   const uint64_t cap = (uint64_t)cu_count * 3;
@@ -454,10 +476,10 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   case M:                                                                                     \
     hipLaunchKernelGGL(fused_kernel<M>, dim3(grid), dim3(BLOCK), 0, s, d_in, n, d_off,        \
                        total_rows, rec, d_adv, d_fixed, reinterpret_cast<const TileInfo*>(tinfo), \
-                       n_tiles, band, d_rep, d_status, inj);                                  \
+                       n_tiles, band, d_rep, d_status, inj, clk);                             \
     break;
     B2F_FUSED(0) B2F_FUSED(2) B2F_FUSED(3) B2F_FUSED(10) B2F_FUSED(18) B2F_FUSED(8) B2F_FUSED(16)
-    B2F_FUSED(34) B2F_FUSED(66) B2F_FUSED(98)
+    B2F_FUSED(34) B2F_FUSED(66) B2F_FUSED(98) B2F_FUSED(FZ_FULL | FZ_CLOCK)
     B2F_FUSED(FZ_FULL | FZ_INJECT)
     default: B2F_FUSED(FZ_FULL)
 #undef B2F_FUSED

@@ -40,7 +40,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                             uint32_t* d_fixed, const void* tinfo, uint64_t n_tiles, uint32_t band,
                             b2f_eval_report* d_rep, const int* d_status, uint64_t inj_row,
                             uint32_t inj_col, uint32_t inj_mask, int mode, int cu_count,
-                            hipStream_t s);  // b2f_fused.hip
+                            unsigned long long* clk, hipStream_t s);  // b2f_fused.hip
 }
 
 namespace {
@@ -653,7 +653,8 @@ int diag_mode(const char* var, int full) {
 // (0, 2, 3, 10, 18, 8, 16, 34, 66, 98) are accepted; anything else runs the product kernel.
 int fused_mode() {
   const int m = diag_mode("B2F_DIAG_FUSED", 27);
-  const bool safe = m == 27 || ((m & ~(1 | 2 | 8 | 16 | 32 | 64)) == 0 && ((m & (32 | 64)) == 0 || (m & 25) == 0));
+  const bool safe = m == 27 || m == (27 | 128) ||
+                    ((m & ~(1 | 2 | 8 | 16 | 32 | 64)) == 0 && ((m & (32 | 64)) == 0 || (m & 25) == 0));
   return safe ? m : 27;
 }
 
@@ -866,11 +867,16 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
   rc = launch_tile_index(ctx, d_offsets, n, nt, s, 16);
   if (rc) return rc;
   const uint32_t band = (uint32_t)diag_mode("B2F_BAND", 16);
+  const int fmode = fused_mode();
+  if ((fmode & 128) && !ctx->d_clock) {
+    HIPCHK(ctx, hipMalloc(&ctx->d_clock, 32 * sizeof(unsigned long long)));
+    HIPCHK(ctx, hipMemset(ctx->d_clock, 0, 32 * sizeof(unsigned long long)));
+  }
   const int tk = timed_begin(ctx, B2F_KERNEL_FILL_EVAL, s);
   HIPCHK(ctx, launch_fill_eval(d_in, (uint32_t)n, d_offsets, total_rows, ctx->d_rec, d_advice,
                                d_fixed, ctx->d_tiles, nt, band, d_report, ctx->d_status,
                                ctx->inj_row, ctx->inj_col, ctx->inj_mask,
-                               fused_mode(), ctx->cu_count, s));
+                               fmode, ctx->cu_count, ctx->d_clock, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
