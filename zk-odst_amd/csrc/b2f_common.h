@@ -1163,6 +1163,9 @@ __device__ __forceinline__ void g_pass(const Tile& T, EvalAcc& A, const uint32_t
 // entry once and then issuing its checks' LDS reads independently (source cell at per-G base
 // + table offset, operand cell at its row). A check belongs to the tile holding its operand row.
 constexpr int LPG = 10;
+#ifndef B2F_COPY_REMAP
+#define B2F_COPY_REMAP 1
+#endif
 #ifndef B2F_COPY_UNROLL
 #define B2F_COPY_UNROLL 4
 #endif
@@ -1173,7 +1176,10 @@ constexpr int GT_WAVE = B2F_GT_WAVE;  // wave that builds the next tile's G tabl
 __device__ __forceinline__ void g_copies(EvalAcc& A, const uint32_t* L, const uint32_t* gt_base,
                                          uint32_t ng, int64_t row_base, uint32_t tid,
                                          const GCarve& C) {
-  const uint32_t gi = tid / LPG, c0 = tid - gi * LPG;
+  // the wave that built the G table takes the last slice of lanes (the fewest G entries)
+  const uint32_t w = tid >> 6, slot = w == (uint32_t)GT_WAVE ? 3u : (w < (uint32_t)GT_WAVE ? w : w - 1);
+  const uint32_t ctid = (B2F_COPY_REMAP ? slot : w) * 64 + (tid & 63u);
+  const uint32_t gi = ctid / LPG, c0 = ctid - gi * LPG;
   if (gi >= ng) return;
   const uint4 g0 = *reinterpret_cast<const uint4*>(gt_base + GT_WORDS_ * gi);
   const uint4 g1 = *reinterpret_cast<const uint4*>(gt_base + GT_WORDS_ * gi + 4);
