@@ -152,6 +152,17 @@ B2F_API int b2f_eval(b2f_ctx* ctx, const uint32_t* advice, const uint32_t* fixed
                      const uint64_t* offsets, size_t n, uint64_t total_rows,
                      b2f_eval_report* report);
 
+/* Multi-block chaining (the reference gadget's Blake2f::update /
+ * finalize, blake2f.rs:101-168): writes the b2f_input records of one block step for messages
+ * 0 .. n-1 -- h from the previous step's outputs h' (d_h_prev, n x 8; the initial state for the
+ * first block), the block's 16 message words (d_blocks, n x 16), the byte counter after the
+ * block (d_t, n x 2), the final-block flag (d_f, n; non-zero = 1) and `rounds` (12 for
+ * BLAKE2b). A host orders its messages by block count so that the messages still running at
+ * a step are a prefix (b2f/hasher.py). Asynchronous on `stream`. */
+B2F_API int b2f_chain_inputs_dev(b2f_ctx* ctx, const uint64_t* d_h_prev, const uint64_t* d_blocks,
+                                 const uint64_t* d_t, const uint32_t* d_f, uint32_t rounds,
+                                 size_t n, b2f_input* d_out, void* stream);
+
 /* Fp export: advice cells as pallas::Base elements (pasta_curves
  * 0.5.1 Fp, p = 0x40000000000000000000000000000000224698fc094cf91b992d30ed00000001), the
  * form halo2's prover keeps its advice columns in. Rows [row_begin, row_begin + nrows) of

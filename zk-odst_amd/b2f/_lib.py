@@ -68,6 +68,7 @@ SIGNATURES = [
     ("b2f_fill_eval_dev", I32, [P, P, SIZE, P, U64, P, P, P, P, P]),
     ("b2f_debug_inject", I32, [P, U64, ctypes.c_uint32, ctypes.c_uint32]),
     ("b2f_debug_clock", I32, [P, P]),
+    ("b2f_chain_inputs_dev", I32, [P, P, P, P, P, ctypes.c_uint32, SIZE, P, P]),
     ("b2f_export_fp_dev", I32, [P, P, U64, U64, U64, ctypes.c_uint32, P, U64, P]),
     ("b2f_sync", I32, [P, P]),
     ("b2f_fill", I32, [P, P, SIZE, P, P, P]),

@@ -89,6 +89,11 @@ class Engine:
         r = 2**64 - 1 if row is None else int(row)
         self._check(self.lib.b2f_debug_inject(self.ctx, r, int(col), int(mask) & 0xffffffff))
 
+    def chain_inputs_dev(self, d_h_prev, d_blocks, d_t, d_f, rounds, n, d_out, stream=0):
+        self._check(self.lib.b2f_chain_inputs_dev(self.ctx, _vp(d_h_prev), _vp(d_blocks), _vp(d_t),
+                                                  _vp(d_f), int(rounds), int(n), _vp(d_out),
+                                                  _vp(stream)))
+
     def export_fp_dev(self, d_adv, total_rows, row_begin, nrows, form, d_out, out_rows,
                       stream=0):
         self._check(self.lib.b2f_export_fp_dev(self.ctx, _vp(d_adv), int(total_rows),

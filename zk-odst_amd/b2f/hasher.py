@@ -1,0 +1,210 @@
+"""Multi-block BLAKE2b over the chip (the chaining half).
+
+Mirrors the reference gadget's hasher API, blake2f-circuit/src/blake2f.rs:81-180:
+`Blake2f::new` (state from the chip's IV, :90-98), `update` (absorb data, compress each full
+block, :101-147), `finalize` (pad and compress the last block, take the digest, :150-168) and
+the one-shot `digest` (:172-179). The reference's gadget is unfinished -- it is the SHA-256
+gadget's shape (32-bit BlockWords, `length += len * 32`, no byte counter, no final-block flag),
+so its chaining would not compute BLAKE2b. The hasher here follows RFC 7693 BLAKE2b instead
+(parameter block in h[0], byte counter t, final flag f, optional key block, digest truncation)
+and is pinned to `hashlib.blake2b` by tests/test_hasher.py and tests/test_gpu_hasher.py.
+
+A batch of messages runs one block step at a time: every step is one fill (+ eval) of the
+chip over the messages that still have blocks, with their compression inputs built on the
+device from the previous step's outputs (b2f_chain_inputs_dev). Messages are ordered by block
+count, longest first, so the messages still running at step j are a prefix 0 .. active[j] - 1
+and every step's trace, offsets and outputs are prefixes of one allocation.
+"""
+import numpy as np
+
+from . import _lib
+from .layout import rows
+
+BLOCK_BYTES = 128
+BLAKE2B_ROUNDS = 12
+IV = np.array([0x6A09E667F3BCC908, 0xBB67AE8584CAA73B, 0x3C6EF372FE94F82B, 0xA54FF53A5F1D36F1,
+               0x510E527FADE682D1, 0x9B05688C2B3E6C1F, 0x1F83D9ABFB41BD6B, 0x5BE0CD19137E2179],
+              dtype=np.uint64)
+
+
+def param_state(digest_size=64, key_len=0):
+    """h0 = IV ^ parameter block (RFC 7693 §3.3: fanout 1, depth 1, key length, digest
+    length; the rest zero)."""
+    if not 1 <= digest_size <= 64:
+        raise _lib.B2FError(_lib.ERR_ARG, "digest_size %d not in 1..64" % digest_size)
+    if not 0 <= key_len <= 64:
+        raise _lib.B2FError(_lib.ERR_ARG, "key length %d > 64" % key_len)
+    h = IV.copy()
+    h[0] ^= np.uint64(0x01010000 | (key_len << 8) | digest_size)
+    return h
+
+
+class Plan:
+    """Host side of a batch: every compression's message words, byte counter and final flag,
+    step-major (step j's messages at rows start[j] .. start[j] + active[j] - 1, in `order`)."""
+
+    def __init__(self, messages, digest_size=64, key=b""):
+        key = bytes(key)
+        self.digest_size = int(digest_size)
+        self.h0 = param_state(self.digest_size, len(key))
+        prefix = key.ljust(BLOCK_BYTES, b"\0") if key else b""
+        datas = [prefix + bytes(m) for m in messages]
+        self.n = len(datas)
+        nblocks = np.array([max(1, -(-len(d) // BLOCK_BYTES)) for d in datas], dtype=np.int64)
+        self.order = np.argsort(-nblocks, kind="stable")
+        nb_sorted = nblocks[self.order]
+        self.steps = int(nb_sorted[0]) if self.n else 0
+        self.active = np.array([int((nb_sorted > j).sum()) for j in range(self.steps)],
+                               dtype=np.int64)
+        self.start = np.concatenate([[0], np.cumsum(self.active)]).astype(np.int64)
+        total = int(self.start[-1])
+        self.blocks = np.zeros((total, 16), dtype=np.uint64)
+        self.t = np.zeros((total, 2), dtype=np.uint64)
+        self.f = np.zeros(total, dtype=np.uint32)
+        for pos, i in enumerate(self.order):
+            d = datas[i]
+            nb = int(nblocks[i])
+            idx = self.start[:nb] + pos
+            self.blocks[idx] = np.frombuffer(d.ljust(nb * BLOCK_BYTES, b"\0"),
+                                             dtype="<u8").reshape(nb, 16)
+            self.t[idx, 0] = np.minimum(np.arange(1, nb + 1, dtype=np.uint64) * BLOCK_BYTES,
+                                        np.uint64(len(d)))
+            self.f[idx[-1]] = 1
+
+    def step(self, j):
+        """(blocks, t, f) of step j: arrays over messages 0 .. active[j] - 1 (sorted order)."""
+        s, e = int(self.start[j]), int(self.start[j + 1])
+        return self.blocks[s:e], self.t[s:e], self.f[s:e]
+
+    def digests(self, final_h):
+        """final_h: [n, 8] u64 in sorted order -> digests (bytes) in the callers' order."""
+        out = [b""] * self.n
+        raw = np.ascontiguousarray(final_h, dtype="<u8")
+        for pos, i in enumerate(self.order):
+            out[int(i)] = raw[pos].tobytes()[:self.digest_size]
+        return out
+
+
+class ChainResult:
+    def __init__(self, plan, reports, final_sorted):
+        self.plan = plan
+        self.reports = reports  # one MockProver report per block step
+        self._final_sorted = final_sorted  # [n, 8] u64, sorted order
+
+    @property
+    def final_h(self):
+        """[n, 8] u64 final chaining values, callers' order."""
+        fin = np.empty_like(self._final_sorted)
+        fin[self.plan.order] = self._final_sorted
+        return fin
+
+    @property
+    def digests(self):
+        """Digest bytes per message, callers' order (built on first access)."""
+        if not hasattr(self, "_digests"):
+            self._digests = self.plan.digests(self._final_sorted)
+        return self._digests
+
+    @property
+    def verified(self):
+        return all(r["first_failure"] == 2**64 - 1 for r in self.reports)
+
+
+def blake2b_batch(engine, messages, digest_size=64, key=b"", path="split", device="cuda:0",
+                  stream=None):
+    """BLAKE2b digests of `messages` (a list of bytes-like) through the chip on one GPU, every
+    block step witnessed (fill) and checked (eval); path "fused" uses b2f_fill_eval_dev."""
+    return run_plan(engine, Plan(messages, digest_size, key), path, device, stream)
+
+
+def run_plan(engine, plan, path="split", device="cuda:0", stream=None):
+    """The device half of blake2b_batch for a prebuilt Plan."""
+    import torch
+
+    if path not in ("split", "fused"):
+        raise _lib.B2FError(_lib.ERR_ARG, "path must be 'split' or 'fused'")
+    n = plan.n
+    if n == 0:
+        return ChainResult(plan, [], np.zeros((0, 8), dtype=np.uint64))
+    dev = torch.device(device)
+    s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+
+    def up(a):
+        return torch.from_numpy(np.ascontiguousarray(a).view(
+            np.int64 if a.dtype == np.uint64 else np.int32).copy()).to(dev)
+
+    d_blocks, d_t, d_f = up(plan.blocks), up(plan.t), up(plan.f)
+    R = rows(BLAKE2B_ROUNDS)
+    # h' of every compression, step-major like the plan: step j's outputs are rows
+    # start[j] .. start[j] + active[j] - 1, and step j + 1 reads its h from that prefix
+    h0 = up(np.broadcast_to(plan.h0, (n, 8)))
+    hs = torch.empty((int(plan.start[-1]), 8), dtype=torch.int64, device=dev)
+    inputs = torch.empty(n * 216, dtype=torch.uint8, device=dev)
+    offsets = torch.arange(n + 1, dtype=torch.int64, device=dev) * R
+    advice = torch.empty((_lib.NUM_ADVICE, R * n), dtype=torch.int32, device=dev)
+    fixed = torch.empty(R * n, dtype=torch.int32, device=dev)
+    report = torch.empty((plan.steps, _lib.REPORT_BYTES // 8), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)  # the uploads above ran on torch's stream
+    for j in range(plan.steps):
+        a = int(plan.active[j])
+        s0 = int(plan.start[j])
+        h_prev = h0 if j == 0 else hs[int(plan.start[j - 1])]
+        engine.chain_inputs_dev(h_prev.data_ptr(), d_blocks[s0].data_ptr(), d_t[s0].data_ptr(),
+                                d_f[s0:].data_ptr(), BLAKE2B_ROUNDS, a, inputs.data_ptr(), s)
+        total = R * a
+        h_out = hs[s0].data_ptr()
+        if path == "fused":
+            engine.fill_eval_dev(inputs.data_ptr(), a, offsets.data_ptr(), total,
+                                 advice.data_ptr(), fixed.data_ptr(), h_out,
+                                 report[j].data_ptr(), s)
+        else:
+            engine.fill_dev(inputs.data_ptr(), a, offsets.data_ptr(), total, advice.data_ptr(),
+                            fixed.data_ptr(), h_out, s)
+            engine.eval_dev(advice.data_ptr(), fixed.data_ptr(), offsets.data_ptr(), a, total,
+                            report[j].data_ptr(), s)
+    engine.sync(s)
+    hs_host = hs.cpu().numpy().view(np.uint64)
+    raw = report.cpu().numpy().view(np.uint64)
+    reps = [_lib.EvalReport.from_buffer_copy(raw[j].tobytes()).as_dict()
+            for j in range(plan.steps)]
+    # message at sorted position p ends at step nblocks - 1, i.e. at row start[nb - 1] + p
+    last = (plan.active[None, :] > np.arange(n)[:, None]).sum(1) - 1
+    return ChainResult(plan, reps, hs_host[plan.start[last] + np.arange(n)])
+
+
+class Blake2f:
+    """The reference gadget's hasher (blake2f.rs:81-180) over the GPU chip, for one message:
+    new -> update* -> finalize, or the one-shot digest. Data is buffered until finalize (BLAKE2b
+    cannot compress a full block before it knows whether it is the last one); finalize runs
+    every block step through the chip and raises B2FError if any step's trace fails its
+    constraints."""
+
+    def __init__(self, engine, digest_size=64, key=b"", device="cuda:0", path="split"):
+        param_state(digest_size, len(key))  # validates
+        self.engine, self.digest_size, self.key = engine, digest_size, bytes(key)
+        self.device, self.path = device, path
+        self._buf = bytearray()
+        self.length = 0
+
+    @classmethod
+    def new(cls, engine, **kw):
+        return cls(engine, **kw)
+
+    def update(self, data):
+        data = bytes(data)
+        self._buf += data
+        self.length += len(data)
+        return self
+
+    def finalize(self):
+        res = blake2b_batch(self.engine, [bytes(self._buf)], self.digest_size, self.key,
+                            self.path, self.device)
+        if not res.verified:
+            bad = next(r for r in res.reports if r["first_failure"] != 2**64 - 1)
+            raise _lib.B2FError(_lib.ERR_INPUT, "chip constraints failed at row %d"
+                                % bad["first_failure"])
+        return res.digests[0]
+
+    @classmethod
+    def digest(cls, engine, data, **kw):
+        return cls(engine, **kw).update(data).finalize()

@@ -576,6 +576,27 @@ __global__ void offsets_check_kernel(const uint64_t* __restrict__ off, uint32_t 
   if (bad) atomicOr(status, 1 << B2F_ERR_LAYOUT);
 }
 
+// Multi-block chaining (Blake2f::update/finalize, blake2f.rs:101-168): the inputs of one block
+// step for messages 0 .. n-1 (the host orders messages by block count, so the messages still
+// running at a step are a prefix): h from the previous step's outputs, the step's words.
+__global__ void chain_inputs_kernel(const uint64_t* __restrict__ h_prev,
+                                    const uint64_t* __restrict__ blocks,
+                                    const uint64_t* __restrict__ t, const uint32_t* __restrict__ f,
+                                    uint32_t rounds, uint32_t n, b2f_input* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  b2f_input x;
+#pragma unroll
+  for (int k = 0; k < 8; k++) x.h[k] = h_prev[8ull * i + k];
+#pragma unroll
+  for (int k = 0; k < 16; k++) x.m[k] = blocks[16ull * i + k];
+  x.t[0] = t[2ull * i];
+  x.t[1] = t[2ull * i + 1];
+  x.rounds = rounds;
+  x.f = f[i] ? 1u : 0u;
+  out[i] = x;
+}
+
 __global__ void report_init_kernel(b2f_eval_report* rep, uint64_t total_rows) {
   for (int s = 0; s < B2F_NUM_GATES; s++) rep->gate_failures[s] = 0;
   rep->lookup_failures = 0;
@@ -944,6 +965,23 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
   }
   HIPCHK(ctx, hipGetLastError());
   timed_end(ctx, tk, s);
+  return B2F_OK;
+}
+
+B2F_API int b2f_chain_inputs_dev(b2f_ctx* ctx, const uint64_t* d_h_prev, const uint64_t* d_blocks,
+                                 const uint64_t* d_t, const uint32_t* d_f, uint32_t rounds,
+                                 size_t n, b2f_input* d_out, void* stream) {
+  if (!ctx) return B2F_ERR_ARG;
+  if (!d_h_prev || !d_blocks || !d_t || !d_f || !d_out)
+    return set_err(ctx, B2F_ERR_ARG, "chain: null buffer");
+  if (rounds > B2F_MAX_ROUNDS) return set_err(ctx, B2F_ERR_ROUNDS, "chain: rounds > %u", B2F_MAX_ROUNDS);
+  if (n > 0xffffffffull) return set_err(ctx, B2F_ERR_ARG, "chain: more than 2^32 messages");
+  if (n == 0) return B2F_OK;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(chain_inputs_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_h_prev,
+                     d_blocks, d_t, d_f, rounds, (uint32_t)n, d_out);
+  HIPCHK(ctx, hipGetLastError());
   return B2F_OK;
 }
 
