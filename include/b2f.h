@@ -179,6 +179,31 @@ B2F_API int b2f_export_fp_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t t
                               uint64_t row_begin, uint64_t nrows, uint32_t form,
                               uint64_t* d_out, uint64_t out_rows, void* stream);
 
+/* Lookup-argument prover columns of the spread lookup
+ * (spread_table.rs:443-453), as halo2_proofs 0.3.0's lookup prover builds them
+ * (plonk/lookup/prover.rs: commit_permuted, permute_expression_pair, commit_product), for
+ * n_circuits circuits cut from the trace: circuit c covers trace rows d_row_begin[c] ..
+ * + usable_rows - 1 (rows past total_rows read as zero rows, i.e. table row 0), and the
+ * table columns hold the 2^16 spread-table rows then the row-0 default up to usable_rows
+ * (the layouter's fill_from_row). usable_rows = 2^k - blinding_factors - 1 is the caller's,
+ * in [2^16, 2^32). Challenges theta, beta, gamma: canonical field elements (4 LE u64 limbs).
+ * Output, per circuit c and column j, d_out[((c * 5 + j) * out_rows + row) * 4 + limb]:
+ *   j = 0  A:  compressed input   theta^2 a_0 + theta a_1 + a_2   (rows < usable_rows)
+ *   j = 1  S:  compressed table                                     (rows < usable_rows)
+ *   j = 2  A': permuted input (ascending canonical order)           (rows < usable_rows)
+ *   j = 3  S': permuted table (A'[i] == S'[i] or A'[i] == A'[i-1])  (rows < usable_rows)
+ *   j = 4  z:  lookup grand product, z[0] = 1                       (rows <= usable_rows)
+ * in `form` (B2F_FP_MONTGOMERY / B2F_FP_CANONICAL); out_rows >= usable_rows + 1, blinding
+ * rows are the prover's. d_first_bad[c] receives the first circuit row whose (a_0, a_1, a_2)
+ * is not a table row (halo2's ConstraintSystemFailure), UINT64_MAX if none; that circuit's
+ * columns are then meaningless. Asynchronous on `stream`. */
+B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t total_rows,
+                                   const uint64_t* d_row_begin, uint32_t n_circuits,
+                                   uint64_t usable_rows, const uint64_t theta[4],
+                                   const uint64_t beta[4], const uint64_t gamma[4], uint32_t form,
+                                   uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
+                                   void* stream);
+
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel the
  * fill/eval calls launch (no host synchronization while recording). b2f_set_timing(ctx, 1)
  * clears the log and starts recording; b2f_kernel_times waits for the recorded events and
@@ -189,7 +214,8 @@ B2F_API int b2f_export_fp_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t t
 #define B2F_KERNEL_EVAL 2   /* constraint evaluation */
 #define B2F_KERNEL_EXPORT 3 /* Fp export */
 #define B2F_KERNEL_FILL_EVAL 4 /* fused trace expansion + constraint evaluation */
-#define B2F_NUM_KERNELS 5
+#define B2F_KERNEL_LOOKUP 5 /* lookup-argument prover columns (all passes of one call) */
+#define B2F_NUM_KERNELS 6
 B2F_API int b2f_set_timing(b2f_ctx* ctx, int enable);
 B2F_API int b2f_kernel_times(b2f_ctx* ctx, double* total_ms, uint32_t* count);
 

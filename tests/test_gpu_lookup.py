@@ -1,0 +1,97 @@
+"""GPU parity of the lookup-argument prover columns (b2f_lookup_columns_dev, SURVEY.md §8(f)
+row 4) with the CPU restatement of halo2_proofs 0.3.0's lookup prover (oracle/lookup.py):
+A, S, A', S' and z bit-exact, in Montgomery and canonical form, for circuits inside the trace,
+straddling its end and almost entirely past it; a corrupted lookup cell is reported at its
+row. Needs an MI355X (`-m gpu`)."""
+import numpy as np
+import pytest
+
+from conftest import random_inputs
+
+pytestmark = pytest.mark.gpu
+
+R256 = 1 << 256
+
+
+def _chal(seed):
+    import lookup as lk
+
+    r = np.random.default_rng(seed)
+    return [int.from_bytes(r.bytes(32), "little") % lk.P for _ in range(3)]
+
+
+def _col_ints(t):
+    """int64 [rows, 4] limbs -> list of Python ints."""
+    a = t.cpu().numpy().view(np.uint64).astype(object)
+    return [int(v) for v in (a[:, 0] | (a[:, 1] << 64) | (a[:, 2] << 128) | (a[:, 3] << 192))]
+
+
+def _circuit_rows(adv, total, begin, usable):
+    a = np.zeros((3, usable), dtype=np.uint32)
+    n = max(0, min(usable, total - begin))
+    a[:, :n] = adv[:3, begin:begin + n]
+    return a
+
+
+@pytest.fixture(scope="module")
+def trace(engine):
+    import b2f
+    import torch
+
+    x = random_inputs(26, (12,), 61)
+    batch = b2f.DeviceBatch(x)
+    batch.fill(engine)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    return batch
+
+
+@pytest.mark.parametrize("form", [1, 0])
+def test_lookup_columns_equal_oracle(engine, trace, form):
+    import lookup as lk
+    import torch
+
+    usable = (1 << 17) - 7
+    total = trace.total_rows
+    begins = [0, total - 20000, total - 5]
+    theta, beta, gamma = _chal(7 + form)
+    out, bad = trace.lookup_columns(engine, begins, usable, theta, beta, gamma, form=form)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    assert (bad.cpu().numpy().view(np.uint64) == np.uint64(2**64 - 1)).all()
+    adv, _ = trace.host_trace()
+    for c, b in enumerate(begins):
+        a = _circuit_rows(adv, total, b, usable)
+        ref = lk.columns(a[0], a[1], a[2], usable, theta, beta, gamma)
+        for j, name in enumerate(["A", "S", "A'", "S'", "z"]):
+            n = usable + 1 if j == 4 else usable
+            got = _col_ints(out[c, j, :n])
+            want = ref[j] if form == 0 else [v * R256 % lk.P for v in ref[j]]
+            if got != want:
+                i = next(i for i in range(n) if got[i] != want[i])
+                pytest.fail("circuit %d column %s differs first at row %d" % (c, name, i))
+
+
+def test_lookup_min_usable_and_bad_row(engine, trace):
+    """usable = 2^16 (the table exactly fills the circuit); a flipped spread cell in the trace
+    is reported at its circuit row (and only for the circuits holding it)."""
+    import lookup as lk
+    import torch
+
+    usable = 1 << 16
+    theta, beta, gamma = _chal(11)
+    out, bad = trace.lookup_columns(engine, [3 * usable], usable, theta, beta, gamma)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    adv, _ = trace.host_trace()
+    a = _circuit_rows(adv, trace.total_rows, 3 * usable, usable)
+    ref = lk.columns(a[0], a[1], a[2], usable, theta, beta, gamma)
+    assert _col_ints(out[0, 3, :usable]) == [v * R256 % lk.P for v in ref[3]]
+    assert _col_ints(out[0, 4, :usable + 1]) == [v * R256 % lk.P for v in ref[4]]
+    row = 70000
+    saved = trace.advice[2, row].item()
+    trace.advice[2, row] = saved ^ 0x10
+    try:
+        out, bad = trace.lookup_columns(engine, [0, 60000, 71000], usable, theta, beta, gamma)
+        engine.sync(torch.cuda.current_stream().cuda_stream)
+        b = bad.cpu().numpy().view(np.uint64)
+        assert int(b[0]) == 2**64 - 1 and int(b[1]) == row - 60000 and int(b[2]) == 2**64 - 1
+    finally:
+        trace.advice[2, row] = saved

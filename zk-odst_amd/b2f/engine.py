@@ -100,6 +100,16 @@ class Engine:
                                                int(row_begin), int(nrows), int(form),
                                                _vp(d_out), int(out_rows), _vp(stream)))
 
+    def lookup_columns_dev(self, d_adv, total_rows, d_row_begin, n_circuits, usable_rows, theta,
+                           beta, gamma, form, d_out, out_rows, d_first_bad, stream=0):
+        """b2f_lookup_columns_dev; theta/beta/gamma are Python ints (canonical Fp)."""
+        lim = [(ctypes.c_uint64 * 4)(*[(int(v) >> (64 * k)) & (2**64 - 1) for k in range(4)])
+               for v in (theta, beta, gamma)]
+        self._check(self.lib.b2f_lookup_columns_dev(
+            self.ctx, _vp(d_adv), int(total_rows), _vp(d_row_begin), int(n_circuits),
+            int(usable_rows), lim[0], lim[1], lim[2], int(form), _vp(d_out), int(out_rows),
+            _vp(d_first_bad), _vp(stream)))
+
     def sync(self, stream=0):
         self._check(self.lib.b2f_sync(self.ctx, _vp(stream)))
 
@@ -175,6 +185,23 @@ class DeviceBatch:
         eng.export_fp_dev(self.advice.data_ptr(), self.total_rows, row_begin, nrows, form,
                           out.data_ptr(), out.shape[1], s)
         return out
+
+    def lookup_columns(self, eng, row_begin, usable_rows, theta, beta, gamma,
+                       form=_lib.FP_MONTGOMERY, stream=None):
+        """Lookup-argument prover columns for circuits starting at trace rows `row_begin`:
+        (out int64 [n_circuits, 5 (A, S, A', S', z), usable_rows + 1, 4], first_bad int64
+        [n_circuits]) -- see b2f_lookup_columns_dev."""
+        torch = self.torch
+        dev = self.advice.device
+        rb = torch.tensor([int(r) for r in row_begin], dtype=torch.int64, device=dev)
+        nc = len(row_begin)
+        out = torch.empty((nc, 5, usable_rows + 1, 4), dtype=torch.int64, device=dev)
+        bad = torch.empty(nc, dtype=torch.int64, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        eng.lookup_columns_dev(self.advice.data_ptr(), self.total_rows, rb.data_ptr(), nc,
+                               usable_rows, theta, beta, gamma, form, out.data_ptr(),
+                               usable_rows + 1, bad.data_ptr(), s)
+        return out, bad
 
     def report_dict(self):
         raw = self.report.cpu().numpy().view(np.uint64)

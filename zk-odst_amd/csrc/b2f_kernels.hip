@@ -32,6 +32,12 @@
 using namespace b2f;
 
 namespace b2f {
+size_t lookup_scratch_bytes(uint32_t group, uint64_t usable_rows);
+hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
+                         const uint64_t* d_row_begin, uint32_t n_circuits, uint64_t usable_rows,
+                         const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
+                         uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
+                         void* scratch, uint32_t group, hipStream_t s);
 hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
                             uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
                             int cu_count, hipStream_t s);  // b2f_export.hip
@@ -624,6 +630,8 @@ struct b2f_ctx {
   unsigned long long* d_clock;  // 32 u64: EVAL_CLOCK phase totals (diagnostics)
   uint64_t inj_row;    // b2f_debug_inject (UINT64_MAX: off)
   uint32_t inj_col, inj_mask;
+  void* d_lk;          // lookup-column scratch (b2f_lookup.hip carve)
+  size_t lk_cap;
 };
 
 namespace {
@@ -777,6 +785,7 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
   (void)hipFree(ctx->d_rec);
   (void)hipFree(ctx->d_tiles);
   (void)hipFree(ctx->d_clock);
+  (void)hipFree(ctx->d_lk);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   delete ctx;
 }
@@ -1004,6 +1013,56 @@ B2F_API int b2f_export_fp_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t t
   int tk = timed_begin(ctx, B2F_KERNEL_EXPORT, s);
   HIPCHK(ctx, launch_export_fp(d_advice, total_rows, row_begin, nrows, form, d_out, out_rows,
                                ctx->cu_count, s));
+  timed_end(ctx, tk, s);
+  return B2F_OK;
+}
+
+B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t total_rows,
+                                   const uint64_t* d_row_begin, uint32_t n_circuits,
+                                   uint64_t usable_rows, const uint64_t theta[4],
+                                   const uint64_t beta[4], const uint64_t gamma[4], uint32_t form,
+                                   uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
+                                   void* stream) {
+  if (!ctx) return B2F_ERR_ARG;
+  if (!d_advice || !d_row_begin || !theta || !beta || !gamma || !d_out || !d_first_bad)
+    return set_err(ctx, B2F_ERR_ARG, "lookup: null buffer");
+  if (form != B2F_FP_CANONICAL && form != B2F_FP_MONTGOMERY)
+    return set_err(ctx, B2F_ERR_ARG, "lookup: unknown form %u", form);
+  if ((uintptr_t)d_out & 15) return set_err(ctx, B2F_ERR_ARG, "lookup: d_out must be 16-byte aligned");
+  if (usable_rows < (1ull << 16) || usable_rows >= (1ull << 32))
+    return set_err(ctx, B2F_ERR_ROWS, "lookup: usable_rows %llu not in [2^16, 2^32)",
+                   (unsigned long long)usable_rows);
+  if (out_rows < usable_rows + 1)
+    return set_err(ctx, B2F_ERR_ROWS, "lookup: out_rows < usable_rows + 1");
+  auto canon = [](const uint64_t* v) {  // < p = 2^254 + d
+    static const uint64_t p[4] = {0x992d30ed00000001ull, 0x224698fc094cf91bull, 0, 0x4000000000000000ull};
+    for (int i = 3; i >= 0; i--)
+      if (v[i] != p[i]) return v[i] < p[i];
+    return false;
+  };
+  if (!canon(theta) || !canon(beta) || !canon(gamma))
+    return set_err(ctx, B2F_ERR_ARG, "lookup: challenge not a canonical field element");
+  if (n_circuits == 0) return B2F_OK;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  // circuits per pass: per-circuit scratch is 1 MiB + 64 B per row + 64 B per 64-row chunk;
+  // keep it under 1 GiB
+  const uint64_t per = (4ull << 18) + usable_rows * 64 + ((usable_rows + 63) / 64) * 64;
+  uint32_t group = (uint32_t)((1ull << 30) / per);
+  if (group < 1) group = 1;
+  if (group > n_circuits) group = n_circuits;
+  const size_t need = lookup_scratch_bytes(group, usable_rows);
+  if (need > ctx->lk_cap) {
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    if (ctx->d_lk) HIPCHK(ctx, hipFree(ctx->d_lk));
+    ctx->d_lk = nullptr;
+    ctx->lk_cap = 0;
+    HIPCHK(ctx, hipMalloc(&ctx->d_lk, need));
+    ctx->lk_cap = need;
+  }
+  int tk = timed_begin(ctx, B2F_KERNEL_LOOKUP, s);
+  HIPCHK(ctx, launch_lookup(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, theta, beta,
+                            gamma, form, d_out, out_rows, d_first_bad, ctx->d_lk, group, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
