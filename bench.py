@@ -79,6 +79,12 @@ def main():
     ap.add_argument("--path", choices=["split", "fused"], default="split",
                     help="split: fill kernel then eval kernel (the headline); fused: "
                          "b2f_fill_eval_dev, one kernel that checks each tile as it assigns it")
+    ap.add_argument("--lookup-circuits", type=int, default=64,
+                    help="lookup-argument columns for this many 2^17-row circuits of the trace "
+                         "(reported beside the headline; 0 skips)")
+    ap.add_argument("--hasher-messages", type=int, default=1 << 16,
+                    help="multi-block BLAKE2b over the chip: this many 1 KiB messages "
+                         "(reported beside the headline; 0 skips)")
     ap.add_argument("--aux-steps", type=int, default=5,
                     help="steps of the other path timed after the headline loop (0 = skip)")
     ap.add_argument("--floor-reps", type=int, default=3,
@@ -265,6 +271,63 @@ def main():
                      "frac": round(nbytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         del out
 
+    # Lookup-argument prover columns for circuits cut from the resident
+    # trace, and the multi-block hasher (row 3): reported beside the headline, not part of it
+    lookup = None
+    if world == 1 and args.lookup_circuits > 0:
+        try:
+            usable = (1 << 17) - 7
+            nc = min(args.lookup_circuits, batch.total_rows // usable)
+            dev = batch.advice.device
+            rb = torch.arange(nc, dtype=torch.int64, device=dev) * usable
+            lout = torch.empty((nc, 5, usable + 1, 4), dtype=torch.int64, device=dev)
+            lbad = torch.empty(nc, dtype=torch.int64, device=dev)
+            chal = (0x1234567 << 200, 0x89ABCDEF << 180, 0x13579BDF << 190)
+
+            def lk_call():
+                eng.lookup_columns_dev(batch.advice.data_ptr(), batch.total_rows, rb.data_ptr(), nc,
+                                       usable, *chal, 1, lout.data_ptr(), usable + 1,
+                                       lbad.data_ptr(), stream)
+            lk_call()
+            eng.sync(stream)
+            eng.set_timing(True)
+            for _ in range(3):
+                lk_call()
+            tot, cnt = eng.kernel_times()["lookup"]
+            avg = tot / max(cnt, 1)
+            lrows = nc * usable
+            lookup = {"circuits": nc, "usable_rows": usable, "avg_ms": round(avg, 4),
+                      "rows_per_s": round(lrows / (avg * 1e-3)),
+                      "algorithmic_GBs": round(lrows * 176 / (avg * 1e-3) / 1e9, 1),
+                      "all_rows_in_table": bool((lbad == -1).all().item())}
+            del lout
+        except Exception as e:  # reported, never masks the headline
+            lookup = {"error": repr(e)}
+    hasher_aux = None
+    if world == 1 and args.hasher_messages > 0:
+        try:
+            import hashlib
+
+            from b2f import hasher
+            hm = args.hasher_messages
+            buf = np.random.default_rng(3).integers(0, 256, (hm, 1024), dtype=np.uint8)
+            msgs = [bytes(r) for r in buf]
+            plan = hasher.Plan(msgs)
+            hasher.run_plan(eng, plan)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            res = hasher.run_plan(eng, plan)
+            el2 = time.perf_counter() - t2
+            ok = res.verified and all(res.digests[i] == hashlib.blake2b(msgs[i]).digest()
+                                      for i in range(0, hm, max(1, hm // 64)))
+            hasher_aux = {"messages": hm, "bytes_each": 1024, "block_steps": plan.steps,
+                          "compressions": int(plan.start[-1]), "ms": round(el2 * 1e3, 3),
+                          "compressions_per_s": round(int(plan.start[-1]) / el2),
+                          "digests_match_hashlib": ok,
+                          "note": "wall clock incl. block upload and h' download"}
+        except Exception as e:
+            hasher_aux = {"error": repr(e)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.rounds, mix, args.cpu_seconds)
@@ -285,7 +348,7 @@ def main():
                           "parallelism": "dp%d (instance shards)" % world},
                "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "floors": floors,
                "other_path": aux,
-               "fp_export": fp_export,
+               "fp_export": fp_export, "lookup_columns": lookup, "hasher": hasher_aux,
                "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None}
         print(json.dumps(out), flush=True)
     if world > 1:
