@@ -58,7 +58,15 @@ def cpu_baseline(rounds, mix, target_s):
         dt2 += run(seed)
         n2 += chunk
         seed += 1
+    # one thread, one chunk of 256: the per-core rate
+    x1 = synth.batch(256, rounds=rounds, rounds_mix=mix, seed=99)
+    o1 = np.frombuffer(x1.tobytes(), dtype=oracle.INPUT_DTYPE).copy()
+    t1 = time.perf_counter()
+    a1, f1, _, off1 = oracle.fill(o1, nthreads=1)
+    oracle.evaluate(a1, f1, off1, nthreads=1)
+    single = 256 / (time.perf_counter() - t1)
     return {"value": n2 / dt2, "unit": "compressions/s", "cores": threads, "kind": "port",
+            "single_thread": round(single, 1), "host_cpus": os.cpu_count(),
             "sample": "%d x %s-round compressions in chunks of %d, oracle fill + eval "
                       "(%.1f s timed, %d threads)"
                       % (n2, "mixed" if mix else rounds, chunk, dt2, threads)}
@@ -168,6 +176,27 @@ def main():
             raise SystemExit("eval flagged a shard")
     if rep["first_failure"] != 2**64 - 1:
         raise SystemExit("eval flagged the trace: %s" % rep)
+
+    # the step's collectives alone (all-gather time reported separately)
+    collectives = None
+    if world > 1:
+        def exchange():
+            dist.all_reduce(verdict[:18], op=dist.ReduceOp.SUM)
+            dist.all_reduce(verdict[18:19], op=dist.ReduceOp.MIN)
+            dist.all_gather_into_tensor(gathered, batch.h_out)
+        verdict.zero_()
+        dist.barrier()
+        torch.cuda.synchronize()
+        tc = time.perf_counter()
+        for _ in range(args.steps):
+            exchange()
+        torch.cuda.synchronize()
+        ct = torch.tensor([time.perf_counter() - tc], dtype=torch.float64,
+                          device=batch.h_out.device)
+        dist.all_reduce(ct, op=dist.ReduceOp.MAX)
+        collectives = {"ms_per_step": round(1e3 * float(ct.item()) / args.steps, 4),
+                       "all_gather_bytes_per_rank": n * 64,
+                       "note": "2 all_reduce (verdict) + 1 all_gather (h'), timed alone"}
 
     value = world * n * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
@@ -348,6 +377,7 @@ def main():
                           "parallelism": "dp%d (instance shards)" % world},
                "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "floors": floors,
                "other_path": aux,
+               "collectives": collectives,
                "fp_export": fp_export, "lookup_columns": lookup, "hasher": hasher_aux,
                "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None}
         print(json.dumps(out), flush=True)
