@@ -54,3 +54,24 @@ def test_many_equal_messages(engine):
     assert res.verified and len(res.reports) == 8
     for i in rng.integers(0, len(msgs), 64):
         assert res.digests[int(i)] == hashlib.blake2b(msgs[int(i)]).digest()
+
+
+def test_chain_inputs_errors(engine):
+    import torch
+
+    import b2f
+
+    dev = torch.device("cuda:0")
+    h = torch.zeros((4, 8), dtype=torch.int64, device=dev)
+    m = torch.zeros((4, 16), dtype=torch.int64, device=dev)
+    t = torch.zeros((4, 2), dtype=torch.int64, device=dev)
+    f = torch.zeros(4, dtype=torch.int32, device=dev)
+    out = torch.empty(4 * 216, dtype=torch.uint8, device=dev)
+    with pytest.raises(b2f.B2FError) as e:
+        engine.chain_inputs_dev(h.data_ptr(), m.data_ptr(), t.data_ptr(), f.data_ptr(),
+                                b2f._lib.MAX_ROUNDS + 1, 4, out.data_ptr())
+    assert e.value.code == b2f._lib.ERR_ROUNDS
+    with pytest.raises(b2f.B2FError):
+        engine.chain_inputs_dev(0, m.data_ptr(), t.data_ptr(), f.data_ptr(), 12, 4, out.data_ptr())
+    engine.chain_inputs_dev(h.data_ptr(), m.data_ptr(), t.data_ptr(), f.data_ptr(), 12, 0,
+                            out.data_ptr())  # n = 0: nothing to do

@@ -95,3 +95,31 @@ def test_lookup_min_usable_and_bad_row(engine, trace):
         assert int(b[0]) == 2**64 - 1 and int(b[1]) == row - 60000 and int(b[2]) == 2**64 - 1
     finally:
         trace.advice[2, row] = saved
+
+
+def test_lookup_argument_errors(engine, trace):
+    """Argument checks of b2f_lookup_columns_dev (all before any launch)."""
+    import lookup as lk
+    import torch
+
+    import b2f
+
+    dev = trace.advice.device
+    rb = torch.zeros(1, dtype=torch.int64, device=dev)
+    bad = torch.empty(1, dtype=torch.int64, device=dev)
+    u = 1 << 16
+    out = torch.empty((1, 5, u + 1, 4), dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+
+    def call(usable=u, theta=3, form=1, out_rows=u + 1):
+        engine.lookup_columns_dev(trace.advice.data_ptr(), trace.total_rows, rb.data_ptr(), 1,
+                                  usable, theta, 5, 7, form, out.data_ptr(), out_rows,
+                                  bad.data_ptr(), s)
+
+    for kw, code in [({"usable": u - 1}, b2f._lib.ERR_ROWS), ({"out_rows": u}, b2f._lib.ERR_ROWS),
+                     ({"theta": lk.P}, b2f._lib.ERR_ARG), ({"form": 2}, b2f._lib.ERR_ARG)]:
+        with pytest.raises(b2f.B2FError) as e:
+            call(**kw)
+        assert e.value.code == code, kw
+    call()  # valid arguments still run
+    engine.sync(s)
