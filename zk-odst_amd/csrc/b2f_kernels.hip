@@ -2,7 +2,7 @@
 // include/b2f.h. Trace contract: docs/LAYOUT.md. Design notes: DESIGN.md.
 //
 // Kernels (one stream, in order):
-//   record_kernel  thread per instance: the BLAKE2f compression itself (RFC 7693 / EIP-152,
+//   record_kernel  a DPP quad per instance: the BLAKE2f compression itself (RFC 7693 / EIP-152,
 //                  blake2f-circuit/src/README.md:1-97), writing the work vector at the start
 //                  of every half-round (the only cross-step state the row expansion needs)
 //                  and h'. O(KB) per instance.
@@ -54,6 +54,19 @@ namespace {
 
 // ------------------------------------------------------------------------- record kernel
 
+// Four lanes (a DPP quad) per instance: lane c holds column c of the state (v[c], v[c+4],
+// v[c+8], v[c+12]) and runs the column step's G(c, c+4, c+8, c+12); for the diagonal step the
+// b, c and d rows are rotated by 1, 2 and 3 lanes so that lane c runs G(c, 4+(c+1)%4,
+// 8+(c+2)%4, 12+(c+3)%4), then rotated back. Every half-round state is dumped (128 B per
+// quad) for the fill's quad builders.
+template <int CTRL>
+__device__ __forceinline__ uint64_t quad_dpp64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, true);
+  return ((uint64_t)hi << 32) | lo;
+}
+constexpr int QROT1 = 0x39, QROT2 = 0x4E, QROT3 = 0x93;  // lane j <- lane (j + k) % 4
+
 __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restrict__ in,
                                                       uint32_t n,
                                                       const uint64_t* __restrict__ off,
@@ -62,64 +75,65 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
                                                       uint64_t* __restrict__ rec,
                                                       uint64_t* __restrict__ h_out,
                                                       int* __restrict__ status) {
-  uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t gt = blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t i = gt >> 2, c = gt & 3u;  // the quad's four lanes share instance i
   if (i >= n) return;
   const b2f_input* x = in + i;
   uint32_t rounds = x->rounds;
   uint64_t o0 = off[i], o1 = off[i + 1];
-  if (rounds > B2F_MAX_ROUNDS) { atomicOr(status, 1 << B2F_ERR_ROUNDS); return; }
+  if (rounds > B2F_MAX_ROUNDS) {
+    if (c == 0) atomicOr(status, 1 << B2F_ERR_ROUNDS);
+    return;
+  }
   uint64_t R = (uint64_t)FIXED_ROWS + (uint64_t)ROUND_ROWS * rounds;
   bool bad = (o1 - o0 != R) || o1 > total_rows || (i == 0 && o0 != 0) ||
              (o0 < (uint64_t)FIXED_ROWS * i) || ((o0 - (uint64_t)FIXED_ROWS * i) % ROUND_ROWS);
   uint64_t st = bad ? 0 : state_index(o0, i);
   if (!bad && st + 2ull * rounds + 1 > states_cap) bad = true;
-  if (bad) { atomicOr(status, 1 << B2F_ERR_LAYOUT); return; }
+  if (bad) {
+    if (c == 0) atomicOr(status, 1 << B2F_ERR_LAYOUT);
+    return;
+  }
 
-  uint64_t v[16], h[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) { h[k] = x->h[k]; v[k] = h[k]; v[k + 8] = c_iv[k]; }
-  v[12] ^= x->t[0];
-  v[13] ^= x->t[1];
-  if (x->f) v[14] = ~v[14];
+  const uint64_t h0 = x->h[c], h1 = x->h[c + 4];
+  uint64_t va = h0, vb = h1, vc = c_iv[c], vd = c_iv[c + 4];
+  if (c == 0) vd ^= x->t[0];
+  if (c == 1) vd ^= x->t[1];
+  if (c == 2 && x->f) vd = ~vd;
 
-  uint64_t* s = rec + st * 16;
+  uint64_t* s = rec + st * 16 + c;
   auto dump = [&](void) {
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-      ulonglong2 p; p.x = v[k]; p.y = v[k + 1];
-      *reinterpret_cast<ulonglong2*>(s + k) = p;
-    }
+    s[0] = va;
+    s[4] = vb;
+    s[8] = vc;
+    s[12] = vd;
     s += 16;
   };
+  auto G = [&](uint64_t mx, uint64_t my) {
+    va = va + vb + mx; vd = rotr64(vd ^ va, 32);
+    vc = vc + vd;      vb = rotr64(vb ^ vc, 24);
+    va = va + vb + my; vd = rotr64(vd ^ va, 16);
+    vc = vc + vd;      vb = rotr64(vb ^ vc, 63);
+  };
   dump();
-#define B2F_G(a, b, c, d, xx, yy)                                     \
-  do {                                                               \
-    v[a] = v[a] + v[b] + (xx); v[d] = rotr64(v[d] ^ v[a], 32);       \
-    v[c] = v[c] + v[d];        v[b] = rotr64(v[b] ^ v[c], 24);       \
-    v[a] = v[a] + v[b] + (yy); v[d] = rotr64(v[d] ^ v[a], 16);       \
-    v[c] = v[c] + v[d];        v[b] = rotr64(v[b] ^ v[c], 63);       \
-  } while (0)
   for (uint32_t r = 0; r < rounds; r++) {
     const uint8_t* sg = c_sigma[r % 10];
-    // SIGMA indexes m at run time: gather from the (cached) input record, not registers.
-    uint64_t mm[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) mm[k] = x->m[sg[k]];
-    B2F_G(0, 4, 8, 12, mm[0], mm[1]);
-    B2F_G(1, 5, 9, 13, mm[2], mm[3]);
-    B2F_G(2, 6, 10, 14, mm[4], mm[5]);
-    B2F_G(3, 7, 11, 15, mm[6], mm[7]);
+    const uint64_t m0 = x->m[sg[2 * c]], m1 = x->m[sg[2 * c + 1]];
+    const uint64_t m2 = x->m[sg[8 + 2 * c]], m3 = x->m[sg[9 + 2 * c]];
+    G(m0, m1);  // column step
     dump();
-    B2F_G(0, 5, 10, 15, mm[8], mm[9]);
-    B2F_G(1, 6, 11, 12, mm[10], mm[11]);
-    B2F_G(2, 7, 8, 13, mm[12], mm[13]);
-    B2F_G(3, 4, 9, 14, mm[14], mm[15]);
+    vb = quad_dpp64<QROT1>(vb);
+    vc = quad_dpp64<QROT2>(vc);
+    vd = quad_dpp64<QROT3>(vd);
+    G(m2, m3);  // diagonal step
+    vb = quad_dpp64<QROT3>(vb);
+    vc = quad_dpp64<QROT2>(vc);
+    vd = quad_dpp64<QROT1>(vd);
     dump();
   }
-#undef B2F_G
   if (h_out) {
-#pragma unroll
-    for (int k = 0; k < 8; k++) h_out[8 * (uint64_t)i + k] = h[k] ^ v[k] ^ v[k + 8];
+    h_out[8 * (uint64_t)i + c] = h0 ^ va ^ vc;
+    h_out[8 * (uint64_t)i + c + 4] = h1 ^ vb ^ vd;
   }
 }
 
@@ -844,7 +858,7 @@ int fill_prologue(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const uint64_t*
   HIPCHK(ctx, hipMemsetAsync(ctx->d_status, 0, sizeof(int), s));
   uint32_t nn = (uint32_t)n;
   int tk = timed_begin(ctx, B2F_KERNEL_RECORD, s);
-  hipLaunchKernelGGL(record_kernel, dim3((nn + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d_in, nn,
+  hipLaunchKernelGGL(record_kernel, dim3((uint32_t)((4ull * nn + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, d_in, nn,
                      d_offsets, total_rows, ctx->rec_cap, ctx->d_rec, d_h_out, ctx->d_status);
   HIPCHK(ctx, hipGetLastError());
   timed_end(ctx, tk, s);
