@@ -90,3 +90,20 @@ def test_null_context_calls_fail_cleanly():
     assert lib.b2f_fill_dev(None, None, 0, None, 0, None, None, None, None) == 1
     assert lib.b2f_eval(None, None, None, None, 0, 0, None) == 1
     assert lib.b2f_last_error(None) == b"null context"
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No fallback: without the HIP library every entry point raises (checked in a fresh
+    interpreter so the loaded library of this session is not reused)."""
+    import os
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import b2f\n"
+            "try:\n    b2f.load()\nexcept OSError as e:\n    print('raised', 'not found' in str(e))\n"
+            "try:\n    b2f.Engine(0)\nexcept OSError as e:\n    print('raised2')\n") % (ROOT + "/zk-odst_amd")
+    env = dict(os.environ, B2F_LIB=str(tmp_path / "absent.so"))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert "raised True" in out.stdout and "raised2" in out.stdout, out.stdout + out.stderr
