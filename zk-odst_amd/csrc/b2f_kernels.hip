@@ -323,6 +323,15 @@ constexpr GTCarve kEvalGT{GS_QM, GS_NG, GS_GT, L_IC, L_W, WSTRIDE, BLOCK / 4, BL
 enum { EVAL_LOOKUP = 1, EVAL_GATES = 2, EVAL_COPIES = 4, EVAL_FULL = 7, EVAL_TOUCH = 8,
        EVAL_CLOCK = 16 };  // EVAL_CLOCK: per-phase s_memtime totals per wave (diagnostics)
 
+// Tiles per band: a workgroup checks EVAL_BAND consecutive tiles, then jumps a grid's worth of
+// bands (XCD-aware over bands). Inside a band the history window of a tile is the previous
+// tile's tail, moved in LDS instead of loaded again.
+#ifndef B2F_EVAL_BAND
+#define B2F_EVAL_BAND 8
+#endif
+constexpr uint64_t EVAL_BAND = B2F_EVAL_BAND;
+__device__ __forceinline__ bool hist_in_lds(uint64_t t) { return EVAL_BAND > 1 && t % EVAL_BAND != 0; }
+
 // The two extra (non-own-quad) loads a thread issues per tile, as a compact descriptor:
 // kind, LDS destination, and a base pointer the tile position is added to.
 enum { XK_NONE = 0, XK_HIST, XK_HALO, XK_INIT, XK_INFO, XK_INFO2 };
@@ -374,16 +383,16 @@ __device__ __forceinline__ Extra make_extra(int slot, const uint32_t* adv, uint6
 // 16-byte load whatever the slot kind (a switch around the loads serialises their issue).
 __device__ __forceinline__ uint4 extra_load(const Extra& x, uint64_t t, const uint4& fo, uint32_t n,
                                             uint64_t total_rows, uint64_t total_quads,
-                                            uint64_t G, uint64_t n_tiles) {
+                                            uint64_t tnext, uint64_t n_tiles) {
   const uint64_t tile0 = t * TILE_ROWS;
   const uint64_t of = ((uint64_t)fo.w << 32) | fo.z;
   const uint32_t k = x.kind;
-  const uint64_t w = k == XK_INIT ? of : k == XK_INFO ? 24 * t : k == XK_INFO2 ? 24 * (t + G) : tile0;
-  const bool ok = k == XK_HIST    ? tile0 >= (uint64_t)HIST
+  const uint64_t w = k == XK_INIT ? of : k == XK_INFO ? 24 * t : k == XK_INFO2 ? 24 * tnext : tile0;
+  const bool ok = k == XK_HIST    ? tile0 >= (uint64_t)HIST && !hist_in_lds(t)
                 : k == XK_HALO    ? (t + 1) * BLOCK + x.q < total_quads
                 : k == XK_INIT    ? fo.x < n && of + INIT_ROWS <= total_rows
                 : k == XK_INFO    ? true
-                : k == XK_INFO2   ? t + G < n_tiles
+                : k == XK_INFO2   ? tnext < n_tiles
                                   : false;
   return ok ? *reinterpret_cast<const uint4*>(x.base + w) : make_uint4(0, 0, 0, 0);
 }
@@ -432,7 +441,9 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
   // XCD a contiguous run of G / 8 tiles per band. A tile's history window and halo are then the
   // rows its same-XCD neighbours just loaded, served from that XCD's L2 rather than refetched
   // (placement is only a speed hint; any placement gives the same result).
-  uint64_t t = (G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+  const uint64_t b0 = (G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+  auto seq = [&](uint64_t k) { return (b0 + (k / EVAL_BAND) * G) * EVAL_BAND + k % EVAL_BAND; };
+  uint64_t t = seq(0);
   // fo (first instance and its offset, per tile) is workgroup-uniform. Only the first tile's
   // is a scalar load; the next tiles' come from the staged TileInfo in LDS (INFO2): on CDNA
   // lgkmcnt counts scalar loads and LDS operations together, so a scalar load issued in the
@@ -440,22 +451,31 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
   uint4 q[NCOL_T], x0 = make_uint4(0, 0, 0, 0), x1 = x0, fo = x0;
   const Extra e0 = make_extra(tid, adv, total_rows, tinfo);
   const Extra e1 = make_extra(tid + BLOCK, adv, total_rows, tinfo);
-  auto load_tile = [&](uint64_t tt, const uint4& f) {
+  auto load_tile = [&](uint64_t tt, const uint4& f, uint64_t tt_next) {
     const uint64_t gq = tt * BLOCK + tid;
 #pragma unroll
     for (int c = 0; c < NCOL_T; c++)
       q[c] = gq < total_quads
                  ? *reinterpret_cast<const uint4*>((c < 10 ? adv + (uint64_t)c * total_rows : fixed) + 4 * gq)
                  : make_uint4(0, 0, 0, 0);
-    x0 = extra_load(e0, tt, f, n, total_rows, total_quads, G, n_tiles);
-    x1 = extra_load(e1, tt, f, n, total_rows, total_quads, G, n_tiles);
+    x0 = extra_load(e0, tt, f, n, total_rows, total_quads, tt_next, n_tiles);
+    x1 = extra_load(e1, tt, f, n, total_rows, total_quads, tt_next, n_tiles);
   };
   if (layout_ok && t < n_tiles) {
     fo = *reinterpret_cast<const uint4*>(tinfo + t);
-    load_tile(t, fo);
+    load_tile(t, fo, seq(1));
   }
-  for (uint32_t iter = 0; layout_ok && t < n_tiles; t += G, iter++) {
+  for (uint32_t iter = 0; layout_ok && t < n_tiles; iter++, t = seq(iter)) {
     tick(-1);
+    const bool hist_lds = hist_in_lds(t);
+    if (hist_lds && tid >= (TILE_ROWS - HIST) / 4) {
+      // the previous tile's tail (still staged) becomes this tile's history window
+#pragma unroll
+      for (int ci = 0; ci < 4; ci++) {
+        const int w = L_W + ci * WSTRIDE + HIST + 4 * tid;
+        *reinterpret_cast<uint4*>(&L[w - TILE_ROWS]) = *reinterpret_cast<const uint4*>(&L[w]);
+      }
+    }
     // ---- stage tile t: registers -> LDS
 #pragma unroll
     for (int c = 0; c < 9; c++) *reinterpret_cast<uint4*>(&L[lds_cell(c, 4 * tid)]) = q[c];
@@ -464,8 +484,8 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
       L[L_QSEL + tid] = (curfx.x & 0xffffu) | (((curfx.y | curfx.z | curfx.w) & 0xffffu) ? 1u << 16 : 0u);
       L[L_A9 + tid] = cur9.x;
     }
-    if (e0.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e0.lds]) = x0;
-    if (e1.kind != XK_NONE) *reinterpret_cast<uint4*>(&L[e1.lds]) = x1;
+    if (e0.kind != XK_NONE && !(hist_lds && e0.kind == XK_HIST)) *reinterpret_cast<uint4*>(&L[e0.lds]) = x0;
+    if (e1.kind != XK_NONE && !(hist_lds && e1.kind == XK_HIST)) *reinterpret_cast<uint4*>(&L[e1.lds]) = x1;
     // ---- lookups on the quad's 4 rows, from the loaded cells, before the barrier
     if ((MODE & EVAL_LOOKUP) && t * BLOCK + tid < total_quads) {
       const uint64_t r0 = 4 * (t * BLOCK + tid);
@@ -479,12 +499,12 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
     tick(0);
     __syncthreads();
     tick(1);
-    // ---- prefetch tile t + G into registers while tile t is checked
-    const uint64_t tn = t + G;
+    // ---- prefetch this workgroup's next tile into registers while tile t is checked
+    const uint64_t tn = seq(iter + 1);
     if (tn < n_tiles) {
-      // TileInfo of tile tn = t + G, staged from the INFO2 slots this iteration
+      // TileInfo of tile tn, staged from the INFO2 slots this iteration
       const uint4 fo_next = make_uint4(L[L_INFO2], 0u, L[L_INFO2 + 2], L[L_INFO2 + 3]);
-      load_tile(tn, fo_next);
+      load_tile(tn, fo_next, seq(iter + 2));
     }
     tick(2);
     const uint64_t tile0 = t * TILE_ROWS;
@@ -508,7 +528,7 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
         __syncthreads();
       }
       if ((tid >> 6) == GT_WAVE)  // the wave with the lightest G pass (XOR) builds ahead
-        build_g_table(Sn, L + L_INFO2, Sg, (int64_t)((t + G) * TILE_ROWS), t + G < n_tiles ? n : 0,
+        build_g_table(Sn, L + L_INFO2, Sg, (int64_t)(tn * TILE_ROWS), tn < n_tiles ? n : 0,
                       total_rows, (uint32_t)tid & 63u, kEvalGT);
       tick(3);
       const GCarve C{L_QSEL, L_A9, L_CT, L_G, TSTRIDE, 0, TILE_ROWS, false};
@@ -967,7 +987,7 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
   uint64_t nt = n_tiles_of(total_rows);
   int rc = launch_tile_index(ctx, d_offsets, n, nt, s);
   if (rc) return rc;
-  uint32_t wgs = grid_for(ctx, nt, 3);
+  uint32_t wgs = grid_for(ctx, (nt + EVAL_BAND - 1) / EVAL_BAND, 3);
   const int emode = diag_mode("B2F_DIAG_EVAL", EVAL_FULL);
   if ((emode & EVAL_CLOCK) && !ctx->d_clock) {
     HIPCHK(ctx, hipMalloc(&ctx->d_clock, 32 * sizeof(unsigned long long)));
