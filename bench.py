@@ -93,6 +93,9 @@ def main():
     ap.add_argument("--hasher-messages", type=int, default=1 << 16,
                     help="multi-block BLAKE2b over the chip: this many 1 KiB messages "
                          "(reported beside the headline; 0 skips)")
+    ap.add_argument("--witness-gather", type=int, default=1 << 13,
+                    help="N > 1: instances per rank of a separate batch whose whole witness "
+                         "table is all-gathered to every rank (timed apart; 0 skips)")
     ap.add_argument("--aux-steps", type=int, default=5,
                     help="steps of the other path timed after the headline loop (0 = skip)")
     ap.add_argument("--floor-reps", type=int, default=3,
@@ -197,6 +200,43 @@ def main():
         collectives = {"ms_per_step": round(1e3 * float(ct.item()) / args.steps, 4),
                        "all_gather_bytes_per_rank": n * 64,
                        "note": "2 all_reduce (verdict) + 1 all_gather (h'), timed alone"}
+
+    # optional: reassemble a (smaller) batch's whole witness table on every rank, the
+    # north_star's all-gather, for a batch that fits; timed apart
+    witness_gather = None
+    if world > 1 and args.witness_gather > 0:
+        try:
+            from b2f import dist as bdist
+            xw = synth.batch(args.witness_gather, rounds=args.rounds, rounds_mix=mix,
+                             seed=1000 + rank)
+            wb = b2f.DeviceBatch(xw)
+            wb.fill(eng, stream)
+            eng.sync(stream)
+            rows_w = torch.tensor([wb.total_rows], dtype=torch.int64, device=wb.advice.device)
+            all_rows = [torch.zeros_like(rows_w) for _ in range(world)]
+            dist.all_gather(all_rows, rows_w)
+            srows = [int(r.item()) for r in all_rows]
+            bdist.gather_trace(wb.advice, wb.fixed, srows, dist, torch)  # warm-up
+            dist.barrier()
+            torch.cuda.synchronize()
+            tw = time.perf_counter()
+            ga, gf = bdist.gather_trace(wb.advice, wb.fixed, srows, dist, torch)
+            torch.cuda.synchronize()
+            wt = torch.tensor([time.perf_counter() - tw], dtype=torch.float64,
+                              device=wb.advice.device)
+            dist.all_reduce(wt, op=dist.ReduceOp.MAX)
+            gathered_bytes = sum(srows) * ROW_BYTES
+            witness_gather = {"instances_per_rank": args.witness_gather,
+                              "trace_bytes_per_rank": wb.total_rows * ROW_BYTES,
+                              "gathered_bytes_per_rank": gathered_bytes,
+                              "ms": round(float(wt.item()) * 1e3, 3),
+                              "GBs_received_per_rank": round(
+                                  (gathered_bytes - wb.total_rows * ROW_BYTES)
+                                  / float(wt.item()) / 1e9, 1),
+                              "note": "one all_gather of the 11 columns + reassembly copy"}
+            del ga, gf, wb
+        except Exception as e:
+            witness_gather = {"error": repr(e)}
 
     value = world * n * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
@@ -377,7 +417,7 @@ def main():
                           "parallelism": "dp%d (instance shards)" % world},
                "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "floors": floors,
                "other_path": aux,
-               "collectives": collectives,
+               "collectives": collectives, "witness_gather": witness_gather,
                "fp_export": fp_export, "lookup_columns": lookup, "hasher": hasher_aux,
                "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None}
         print(json.dumps(out), flush=True)

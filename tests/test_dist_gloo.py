@@ -41,7 +41,11 @@ def _worker(rank, world, port, inputs_bytes, q):
     rep = oracle.evaluate(adv, fixed, off)
     combined = bdist.reduce_report(rep, dist, torch, "cpu")
     h = bdist.gather_h_out(torch.from_numpy(h_out.view(np.int64)), shards, dist, torch)
-    q.put((rank, combined, h.numpy().view(np.uint64).tobytes(), shards))
+    srows = [int(bdist.offsets(x[a:b])[-1]) for a, b in shards]
+    ga, gf = bdist.gather_trace(torch.from_numpy(adv.view(np.int32)),
+                                torch.from_numpy(fixed.view(np.int32)), srows, dist, torch)
+    q.put((rank, combined, h.numpy().view(np.uint64).tobytes(), shards,
+           ga.numpy().view(np.uint32).tobytes(), gf.numpy().view(np.uint32).tobytes()))
     dist.destroy_process_group()
 
 
@@ -73,8 +77,16 @@ def test_gloo_world2_matches_single_process(orc):
         p.join(timeout=60)
         assert p.exitcode == 0
     ox = np.frombuffer(x.tobytes(), dtype=orc.INPUT_DTYPE).copy()
-    _, _, h_ref, _ = orc.fill(ox)
-    for rank, combined, hbytes, shards in res:
+    adv_ref, fixed_ref, h_ref, off_ref = orc.fill(ox)
+    adv_ref = adv_ref.copy()
+    for rank, combined, hbytes, shards, abytes, fbytes in res:
         assert np.array_equal(np.frombuffer(hbytes, dtype=np.uint64).reshape(-1, 8), h_ref)
+        # the reassembled witness table is the single-process trace (with rank 1's corrupted
+        # cell at its global row)
+        ga = np.frombuffer(abytes, dtype=np.uint32).reshape(10, -1)
+        want = adv_ref.copy()
+        want[1, int(off_ref[shards[1][0]]) + 5] += 1
+        assert np.array_equal(ga, want)
+        assert np.array_equal(np.frombuffer(fbytes, dtype=np.uint32), fixed_ref)
         assert combined["lookup_failures"] >= 1 and combined["first_failure"] != 2**64 - 1
         assert combined["rows_checked"] == int(orc.offsets(ox)[-1])

@@ -3,7 +3,9 @@
 Instances are independent: each rank fills and evaluates a contiguous shard with no
 data-path collective. The only exchanges are the results: the verdict counters
 (all_reduce) and the 64-byte h' per instance (one all_gather). RCCL has no all_gather_v, so
-unequal shards are padded to the largest shard.
+unequal shards are padded to the largest shard. Reassembling the whole witness table on every
+rank (gather_trace, one all_gather of the 11 columns) is an optional step for batches that
+fit one GPU (2^18 x 12 rounds x 8 ranks would be 480 GB).
 """
 import numpy as np
 
@@ -62,3 +64,20 @@ def gather_h_out(h_local, shards, dist, torch, group=None):
     dist.all_gather_into_tensor(out, pad, group=group)
     parts = [out[r * width: r * width + (hi - lo)] for r, (lo, hi) in enumerate(shards)]
     return torch.cat(parts, dim=0)
+
+
+def gather_trace(adv_local, fixed_local, shard_rows, dist, torch, group=None):
+    """The whole batch's trace on every rank: adv_local [10, rows_r] and fixed_local
+    [rows_r] (int32 bit patterns, rows_r = shard_rows[rank]) -> (advice [10, total],
+    fixed [total]) with the ranks' rows in order, by one all_gather of the 11 columns padded
+    to the largest shard, then one device copy into the column-major layout."""
+    world = len(shard_rows)
+    width = max(shard_rows)
+    rows = adv_local.shape[1]
+    pad = torch.zeros((11, width), dtype=adv_local.dtype, device=adv_local.device)
+    pad[:10, :rows] = adv_local
+    pad[10, :rows] = fixed_local
+    out = torch.empty((world, 11, width), dtype=adv_local.dtype, device=adv_local.device)
+    dist.all_gather_into_tensor(out.view(world * 11, width), pad, group=group)
+    cols = torch.cat([out[r, :, :n] for r, n in enumerate(shard_rows)], dim=1)  # [11, total]
+    return cols[:10].contiguous(), cols[10].contiguous()
