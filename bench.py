@@ -209,7 +209,7 @@ def main():
             from b2f import dist as bdist
             xw = synth.batch(args.witness_gather, rounds=args.rounds, rounds_mix=mix,
                              seed=1000 + rank)
-            wb = b2f.DeviceBatch(xw)
+            wb = b2f.DeviceBatch(xw, device="cuda:%d" % local)
             wb.fill(eng, stream)
             eng.sync(stream)
             rows_w = torch.tensor([wb.total_rows], dtype=torch.int64, device=wb.advice.device)
