@@ -115,9 +115,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    # rehearsal of the N > 1 code path on a one-GPU box (never for measurements): every rank
+    # on cuda:0, collectives over gloo
+    rehearse = os.environ.get("B2F_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     mix = [1, 4, 12] if args.mix else None
     n = args.batch
