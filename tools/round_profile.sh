@@ -9,7 +9,7 @@ mkdir -p $OUT
 cd $R
 timeout -k 10 400 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 1
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o p --output-format csv -- python3 $R/bench.py --no-cpu > $OUT/bench_prof.json 2> $OUT/bench_prof.err || exit 2
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o p --output-format csv -- python3 $R/bench.py --no-cpu --hasher-messages 0 > $OUT/bench_prof.json 2> $OUT/bench_prof.err || exit 2
 cd $R && bash tools/pmc_traffic.sh > $OUT/traffic.log 2>&1 || exit 3
 cp profiles/pmc_traffic.json $OUT/ 2>/dev/null
 # bench again so its roofline.traffic picks up the PMC numbers just measured
