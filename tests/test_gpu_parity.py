@@ -177,6 +177,60 @@ def test_device_batch_2p16_bitexact(engine, orc):
         assert np.array_equal(h_out[s:e], oh)
 
 
+def test_2p18_corruptions_past_2p30_rows(engine, orc):
+    """BASELINE config 3 at full size (2^18 x 12 rounds, 1.37 G rows, 5.5 GB per column)
+    through a size-independent property: the clean trace passes, and single-cell faults in
+    instances whose rows lie past 2^30 (and past 4 GiB of column bytes) are reported exactly
+    as the oracle reports them on those instances alone (counters summed, first failure =
+    the smallest global row). Instances are independent, so checking each faulted instance
+    by itself is the whole verdict."""
+    import b2f
+    import torch
+
+    from b2f import synth
+
+    n = 1 << 18
+    x = synth.batch(n, rounds=12)
+    batch = b2f.DeviceBatch(x)
+    stream = torch.cuda.current_stream().cuda_stream
+    batch.fill(engine)
+    batch.evaluate(engine)
+    engine.sync(stream)
+    clean = batch.report_dict()
+    assert clean["first_failure"] == 2**64 - 1 and clean["rows_checked"] == batch.used_rows
+    off = batch.offsets_host
+    # (instance, column, row inside the instance, bit): an a1 output limb (a copy source), an
+    # XOR63 re-split cell, an a2 operand (a copy), a c2 carry, the last digest row of the batch
+    faults = [(n - 1, 1, 164 + 416 * 11 + 3, 5), (n - 7, 8, 164 + 416 * 6 + 52 * 3 + 46, 0),
+              (231017, 4, 164 + 416 * 2 + 29, 17), (240000, 9, 164 + 416 * 9 + 52 * 5 + 40, 1),
+              (n - 1, 7, 164 + 416 * 12 + 8 * 7, 3)]
+    assert int(off[231017]) > 1 << 30
+    for i, c, r, b in faults:
+        batch.advice[c, int(off[i]) + r] ^= 1 << b
+    batch.evaluate(engine)
+    engine.sync(stream)
+    got = batch.report_dict()
+    want = {"gate_failures": [0] * 16, "lookup_failures": 0, "copy_failures": 0,
+            "first_failure": 2**64 - 1, "rows_checked": batch.used_rows}
+    for i in sorted({f[0] for f in faults}):
+        r0, r1 = int(off[i]), int(off[i + 1])
+        adv = batch.advice[:, r0:r1].cpu().numpy().view(np.uint32)
+        fx = batch.fixed[r0:r1].cpu().numpy().view(np.uint32)
+        o = orc.evaluate(adv, fx, np.array([0, r1 - r0], dtype=np.uint64))
+        assert o["first_failure"] != 2**64 - 1, "fault in instance %d not flagged" % i
+        want["gate_failures"] = [a + b for a, b in zip(want["gate_failures"], o["gate_failures"])]
+        want["lookup_failures"] += o["lookup_failures"]
+        want["copy_failures"] += o["copy_failures"]
+        first = o["first_failure"] + (r0 << 8)  # (row << 8) | code, row made global
+        want["first_failure"] = min(want["first_failure"], first)
+    assert got == want
+    for i, c, r, b in faults:  # undo: the trace is clean again
+        batch.advice[c, int(off[i]) + r] ^= 1 << b
+    batch.evaluate(engine)
+    engine.sync(stream)
+    assert batch.report_dict() == clean
+
+
 def test_padded_tail_rows_zero(engine, orc):
     import b2f
     import torch
