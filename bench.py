@@ -3,12 +3,18 @@
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+    ... bench.py --gpus 8 --global-batch 1048576                 (BASELINE configs[3])
 
 One step = fill (record + fill kernels) then eval of the whole per-GPU batch (--path split, the
 headline; --path fused runs b2f_fill_eval_dev instead; the other path is timed beside it as
-"other_path"); inputs and the trace stay resident in HBM. N > 1: every rank runs its own 2^18 shard (weak scaling); the
-step ends with one all_reduce of the verdict counters and one RCCL all_gather of the h'
-outputs. Rank 0 prints one JSON line.
+"other_path"); inputs and the trace stay resident in HBM. N > 1: by default every rank runs its
+own 2^18 batch (weak scaling); --global-batch G shards G instances over the ranks with the
+row-balanced dist.plan_shards (strong scaling). Either way the step ends with one all_reduce of
+the verdict counters and one RCCL all_gather of the h' outputs. The whole witness table is
+reassembled on every rank (dist.gather_trace: one all-gather per column into the final
+column-major buffers) where it fits in HBM, timed apart ("witness_gather"); at N = 8 a
+BASELINE configs[3] leg (2^20 sharded, gather of the full 241 GB table) runs after the headline
+unless --config4 0. Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -31,45 +37,87 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(rounds, mix, target_s):
+def host_cpus():
+    """The host's CPUs as this process sees them: logical CPUs, physical cores (distinct
+    (package, core) pairs of /proc/cpuinfo), the affinity mask, the cgroup CPU quota."""
+    info = {"logical": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    cores = set()
+    try:
+        pkg = core = None
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                k, _, v = line.partition(":")
+                k = k.strip()
+                if k == "physical id":
+                    pkg = v.strip()
+                elif k == "core id":
+                    core = v.strip()
+                elif not k and pkg is not None:
+                    cores.add((pkg, core))
+                    pkg = core = None
+        if pkg is not None:
+            cores.add((pkg, core))
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    info["physical_cores"] = len(cores) or None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    return info
+
+
+def cpu_baseline(rounds, mix, target_s, threads):
     """Time the CPU oracle (oracle/, a C port of the same fill + eval) on a bounded sample of
-    the same workload, all host threads it is given. Test infrastructure: the checker."""
+    the same workload: `threads` OpenMP threads (the box's CPU share for one GPU), then one
+    thread (the per-core rate). Test infrastructure: the checker."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from b2f import synth
 
-    threads = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
+    chunk = max(2048, 64 * threads)  # ~0.5 GB of trace per 2,048 instances: memory bounded
 
-    chunk = 2048  # ~0.5 GB of trace per chunk at 12 rounds: memory stays bounded
-
-    def run(seed):
-        x = synth.batch(chunk, rounds=rounds, rounds_mix=mix, seed=seed)
+    def run(seed, n, nt):
+        x = synth.batch(n, rounds=rounds, rounds_mix=mix, seed=seed)
         ox = np.frombuffer(x.tobytes(), dtype=oracle.INPUT_DTYPE).copy()
         t0 = time.perf_counter()
-        adv, fixed, h_out, off = oracle.fill(ox, nthreads=threads)
-        rep = oracle.evaluate(adv, fixed, off, nthreads=threads)
+        adv, fixed, h_out, off = oracle.fill(ox, nthreads=nt)
+        rep = oracle.evaluate(adv, fixed, off, nthreads=nt)
         dt = time.perf_counter() - t0
         assert rep["first_failure"] == 2**64 - 1
         return dt
 
-    run(1)  # warm the thread pool and the allocator
+    run(1, chunk, threads)  # warm the thread pool and the allocator
     n2, dt2, seed = 0, 0.0, 2
     while dt2 < target_s:
-        dt2 += run(seed)
+        dt2 += run(seed, chunk, threads)
         n2 += chunk
         seed += 1
-    # one thread, one chunk of 256: the per-core rate (SURVEY.md §8(d))
-    x1 = synth.batch(256, rounds=rounds, rounds_mix=mix, seed=99)
-    o1 = np.frombuffer(x1.tobytes(), dtype=oracle.INPUT_DTYPE).copy()
-    t1 = time.perf_counter()
-    a1, f1, _, off1 = oracle.fill(o1, nthreads=1)
-    oracle.evaluate(a1, f1, off1, nthreads=1)
-    single = 256 / (time.perf_counter() - t1)
-    return {"value": n2 / dt2, "unit": "compressions/s", "cores": threads, "kind": "port",
-            "single_thread": round(single, 1), "host_cpus": os.cpu_count(),
-            "sample": "%d x %s-round compressions in chunks of %d, oracle fill + eval "
-                      "(%.1f s timed, %d threads)"
-                      % (n2, "mixed" if mix else rounds, chunk, dt2, threads)}
+    n1, dt1 = 0, 0.0
+    while dt1 < max(1.0, target_s / 5):
+        dt1 += run(1000 + n1, 128, 1)
+        n1 += 128
+    rate, single = n2 / dt2, n1 / dt1
+    hc = host_cpus()
+    eff = rate / (threads * single)
+    out = {"value": round(rate, 1), "unit": "compressions/s", "cores": threads, "kind": "port",
+           "single_thread": round(single, 1), "scaling_efficiency": round(eff, 3),
+           "host_cpus": hc["logical"], "host": hc,
+           "sample": "%d x %s-round compressions in chunks of %d, oracle fill + eval "
+                     "(%.1f s timed, %d threads; 1 thread: %d in %.1f s)"
+                     % (n2, "mixed" if mix else rounds, chunk, dt2, threads, n1, dt1)}
+    if hc["physical_cores"]:
+        # not measured: the per-thread rate times every physical core at the measured
+        # efficiency (the box's CPU share is `threads`; see DESIGN.md §5)
+        out["projected_all_physical_cores"] = round(single * hc["physical_cores"] * eff, 1)
+    return out
 
 
 def main():
@@ -77,10 +125,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1 << 18, help="instances per GPU")
+    ap.add_argument("--batch", type=int, default=1 << 18, help="instances per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="instances over all GPUs, row-balanced shards (strong scaling; "
+                         "BASELINE configs[3] is 1048576 at 8 GPUs)")
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--mix", action="store_true", help="rounds uniform in {1,4,12} (config 5)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="oracle threads for the CPU baseline: the box's CPU share for one GPU")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--export-rows", type=int, default=1 << 25,
                     help="rows of the Fp export timed after the headline loop (0 = skip)")
@@ -94,8 +147,12 @@ def main():
                     help="multi-block BLAKE2b over the chip: this many 1 KiB messages "
                          "(reported beside the headline; 0 skips)")
     ap.add_argument("--witness-gather", type=int, default=1 << 13,
-                    help="N > 1: instances per rank of a separate batch whose whole witness "
-                         "table is all-gathered to every rank (timed apart; 0 skips)")
+                    help="N > 1, weak scaling: instances per rank of a separate batch whose "
+                         "whole witness table is all-gathered to every rank (timed apart; 0 "
+                         "skips). With --global-batch the step's own trace is gathered if it fits")
+    ap.add_argument("--config4", type=int, default=1 << 20,
+                    help="N = 8 without --global-batch: after the headline, run BASELINE "
+                         "configs[3] (this many instances sharded, full witness gather); 0 skips")
     ap.add_argument("--aux-steps", type=int, default=5,
                     help="steps of the other path timed after the headline loop (0 = skip)")
     ap.add_argument("--floor-reps", type=int, default=3,
@@ -108,6 +165,7 @@ def main():
     import torch.distributed as dist
 
     import b2f
+    from b2f import dist as bdist
     from b2f import synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,130 +184,188 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
+    device = "cuda:%d" % local
     mix = [1, 4, 12] if args.mix else None
-    n = args.batch
-    x = synth.batch(n, rounds=args.rounds, rounds_mix=mix, first=rank * n)
-    batch = b2f.DeviceBatch(x, device="cuda:%d" % local)
     eng = b2f.Engine(local)
     stream = torch.cuda.current_stream().cuda_stream
-    rows = batch.used_rows
-    log("rank %d: %d instances, %d rows, trace %.1f GB" % (rank, n, rows, rows * ROW_BYTES / 1e9))
 
-    if world > 1:
-        gathered = torch.empty((world * n, 8), dtype=torch.int64, device=batch.h_out.device)
-        verdict = torch.empty(20, dtype=torch.int64, device=batch.h_out.device)
+    def make_batch(global_n):
+        """This rank's batch: its own weak-scaling batch (global_n = 0) or its row-balanced
+        shard of global_n instances. Returns (batch, shard info)."""
+        if not global_n:
+            n = args.batch
+            x = synth.batch(n, rounds=args.rounds, rounds_mix=mix, first=rank * n)
+            return b2f.DeviceBatch(x, device=device), {
+                "rows": [0] * world, "base": 0, "window": None, "shards": None, "n_local": n}
+        # shard plan from the rounds alone (synth's rounds depend only on the index)
+        xr = synth.rounds_of(global_n, rounds=args.rounds, rounds_mix=mix)
+        shards = bdist.plan_shards(xr, world)
+        srows, sbase = bdist.shard_rows(xr, shards)
+        w = bdist.trace_window(srows)
+        lo, hi = shards[rank]
+        x = synth.batch(hi - lo, rounds=args.rounds, rounds_mix=mix, first=lo)
+        return b2f.DeviceBatch(x, device=device, total_rows=w), {
+            "rows": srows, "base": sbase[rank], "window": w, "shards": shards,
+            "n_local": hi - lo}
 
-    def run_path(path):
+    def run_path(batch, path):
         if path == "fused":
             batch.fill_evaluate(eng, stream)
         else:
             batch.fill(eng, stream)
             batch.evaluate(eng, stream)
 
-    def step():
-        run_path(args.path)
+    def timed_loop(batch, info, path, steps, warmup, global_n):
+        """Warm-up, then `steps` timed steps between barriers; returns (elapsed max over
+        ranks, kernel times, verdict dict, h' gather buffer)."""
+        gathered = verdict = None
         if world > 1:
-            r = batch.report.view(torch.int64)
-            verdict[:18].copy_(r[:18])
-            first = r[18]
-            verdict[18] = torch.where(first == -1, torch.iinfo(torch.int64).max, first)
-            dist.all_reduce(verdict[:18], op=dist.ReduceOp.SUM)
-            dist.all_reduce(verdict[18:19], op=dist.ReduceOp.MIN)
-            dist.all_gather_into_tensor(gathered, batch.h_out)
+            width = max(hi - lo for lo, hi in info["shards"]) if info["shards"] else info["n_local"]
+            gathered = torch.empty((world * width, 8), dtype=torch.int64, device=device)
+            hpad = torch.zeros((width, 8), dtype=torch.int64, device=device)
 
-    for _ in range(args.warmup):
-        step()
-    eng.sync(stream)
-    rep = batch.report_dict()
-    if rep["first_failure"] != 2**64 - 1:
-        raise SystemExit("eval flagged the trace: %s" % rep)
+        def step():
+            run_path(batch, path)
+            nonlocal verdict
+            if world > 1:
+                verdict = bdist.all_reduce_verdict(
+                    bdist.verdict_words(batch.report, info["base"], torch), dist)
+                hsrc = batch.h_out
+                if hsrc.shape[0] != hpad.shape[0]:
+                    hpad[: hsrc.shape[0]].copy_(hsrc)
+                    hsrc = hpad
+                dist.all_gather_into_tensor(gathered, hsrc)
 
-    eng.set_timing(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ktimes = eng.kernel_times()
-    eng.sync(stream)
-    rep = batch.report_dict()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=batch.h_out.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        if int(verdict[18].item()) != torch.iinfo(torch.int64).max or int(verdict[:18].sum()) != 0:
-            raise SystemExit("eval flagged a shard")
-    if rep["first_failure"] != 2**64 - 1:
-        raise SystemExit("eval flagged the trace: %s" % rep)
+        for _ in range(warmup):
+            step()
+        eng.sync(stream)
+        rep = batch.report_dict()
+        if rep["first_failure"] != 2**64 - 1:
+            raise SystemExit("eval flagged the trace: %s" % rep)
+        eng.set_timing(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        ktimes = eng.kernel_times()
+        eng.sync(stream)
+        rep = batch.report_dict()
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            v = verdict.tolist()
+            if v[19] != bdist.NONE or sum(v[:19]) != 0:
+                raise SystemExit("eval flagged a shard: %s" % v)
+        if rep["first_failure"] != 2**64 - 1:
+            raise SystemExit("eval flagged the trace: %s" % rep)
+        return elapsed, ktimes, rep
 
-    # the step's collectives alone (all-gather time reported separately)
-    collectives = None
-    if world > 1:
-        def exchange():
-            dist.all_reduce(verdict[:18], op=dist.ReduceOp.SUM)
-            dist.all_reduce(verdict[18:19], op=dist.ReduceOp.MIN)
-            dist.all_gather_into_tensor(gathered, batch.h_out)
-        verdict.zero_()
+    def collectives_alone(batch, info, steps):
+        """The step's collectives timed alone (all-gather time apart)."""
+        width = max(hi - lo for lo, hi in info["shards"]) if info["shards"] else info["n_local"]
+        gathered = torch.empty((world * width, 8), dtype=torch.int64, device=device)
+        hpad = torch.zeros((width, 8), dtype=torch.int64, device=device)
+        hpad[: batch.n].copy_(batch.h_out)
+        words = bdist.verdict_words(batch.report, info["base"], torch)
         dist.barrier()
         torch.cuda.synchronize()
         tc = time.perf_counter()
-        for _ in range(args.steps):
-            exchange()
+        for _ in range(steps):
+            bdist.all_reduce_verdict(words, dist)
+            dist.all_gather_into_tensor(gathered, hpad)
         torch.cuda.synchronize()
-        ct = torch.tensor([time.perf_counter() - tc], dtype=torch.float64,
-                          device=batch.h_out.device)
+        ct = torch.tensor([time.perf_counter() - tc], dtype=torch.float64, device=device)
         dist.all_reduce(ct, op=dist.ReduceOp.MAX)
-        collectives = {"ms_per_step": round(1e3 * float(ct.item()) / args.steps, 4),
-                       "all_gather_bytes_per_rank": n * 64,
-                       "note": "2 all_reduce (verdict) + 1 all_gather (h'), timed alone"}
+        return {"ms_per_step": round(1e3 * float(ct.item()) / steps, 4),
+                "all_gather_bytes_per_rank": width * 64,
+                "note": "2 all_reduce (verdict) + 1 all_gather (h'), timed alone"}
 
-    # optional: reassemble a (smaller) batch's whole witness table on every rank, the
-    # north_star's all-gather, for a batch that fits; timed apart
-    witness_gather = None
-    if world > 1 and args.witness_gather > 0:
-        try:
-            from b2f import dist as bdist
-            xw = synth.batch(args.witness_gather, rounds=args.rounds, rounds_mix=mix,
-                             seed=1000 + rank)
-            wb = b2f.DeviceBatch(xw, device="cuda:%d" % local)
-            wb.fill(eng, stream)
-            eng.sync(stream)
-            rows_w = torch.tensor([wb.total_rows], dtype=torch.int64, device=wb.advice.device)
-            all_rows = [torch.zeros_like(rows_w) for _ in range(world)]
-            dist.all_gather(all_rows, rows_w)
-            srows = [int(r.item()) for r in all_rows]
-            bdist.gather_trace(wb.advice, wb.fixed, srows, dist, torch)  # warm-up
+    def fits_everywhere(nbytes, margin=2 << 30):
+        """True on every rank iff every rank has nbytes + margin of free HBM (collective)."""
+        free = torch.cuda.mem_get_info(local)[0]
+        ok = torch.tensor([1 if free >= nbytes + margin else 0], dtype=torch.int64, device=device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        return bool(ok.item()), free
+
+    def witness_gather(adv, fixed, srows, x_note, reps=2):
+        """Reassemble the whole witness table on every rank (gather_trace) and time it; the
+        result is checked against the local shard (rank k's rows at its global offset)."""
+        need = bdist.gather_trace_bytes(srows)
+        ok, free = fits_everywhere(need)
+        if not ok:
+            return {"skipped": "needs %.1f GB per rank, %.1f GB free on rank %d"
+                               % (need / 1e9, free / 1e9, rank)}
+        buf = torch.empty((11, world * bdist.trace_window(srows)), dtype=adv.dtype, device=device)
+        best = None
+        for _ in range(reps):
             dist.barrier()
             torch.cuda.synchronize()
             tw = time.perf_counter()
-            ga, gf = bdist.gather_trace(wb.advice, wb.fixed, srows, dist, torch)
+            ga, gf = bdist.gather_trace(adv, fixed, srows, dist, torch, out=buf)
             torch.cuda.synchronize()
-            wt = torch.tensor([time.perf_counter() - tw], dtype=torch.float64,
-                              device=wb.advice.device)
+            wt = torch.tensor([time.perf_counter() - tw], dtype=torch.float64, device=device)
             dist.all_reduce(wt, op=dist.ReduceOp.MAX)
-            gathered_bytes = sum(srows) * ROW_BYTES
-            witness_gather = {"instances_per_rank": args.witness_gather,
-                              "trace_bytes_per_rank": wb.total_rows * ROW_BYTES,
-                              "gathered_bytes_per_rank": gathered_bytes,
-                              "ms": round(float(wt.item()) * 1e3, 3),
-                              "GBs_received_per_rank": round(
-                                  (gathered_bytes - wb.total_rows * ROW_BYTES)
-                                  / float(wt.item()) / 1e9, 1),
-                              "note": "one all_gather of the 11 columns + reassembly copy"}
-            del ga, gf, wb
-        except Exception as e:
-            witness_gather = {"error": repr(e)}
+            best = float(wt.item()) if best is None else min(best, float(wt.item()))
+        base = sum(srows[:rank])
+        mine = srows[rank]
+        same = bool(torch.equal(ga[:, base: base + mine], adv[:, :mine])) and \
+            bool(torch.equal(gf[base: base + mine], fixed[:mine]))
+        total = sum(srows)
+        recv = (total - mine) * ROW_BYTES
+        res = {"batch": x_note, "table_rows": total, "table_bytes": total * ROW_BYTES,
+               "buffer_bytes_per_rank": need, "ms": round(best * 1e3, 3),
+               "GBs_received_per_rank": round(recv / best / 1e9, 1),
+               "own_rows_in_place": same,
+               "note": "11 per-column all_gather_into_tensor into the final column-major "
+                       "buffers (one RCCL group) + in-place compaction of padded windows"}
+        del ga, gf, buf
+        torch.cuda.empty_cache()
+        return res
 
-    value = world * n * args.steps / elapsed
+    global_n = args.global_batch
+    batch, info = make_batch(global_n)
+    n_local = batch.n
+    rows = batch.used_rows
+    log("rank %d: %d instances, %d rows, trace %.1f GB"
+        % (rank, n_local, rows, batch.total_rows * ROW_BYTES / 1e9))
+
+    elapsed, ktimes, rep = timed_loop(batch, info, args.path, args.steps, args.warmup, global_n)
+    total_n = global_n if global_n else world * n_local
+    value = total_n * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
 
+    collectives = None
+    witness = None
+    if world > 1:
+        collectives = collectives_alone(batch, info, args.steps)
+        if global_n:
+            witness = witness_gather(batch.advice, batch.fixed, info["rows"],
+                                     "the step's own trace (%d instances)" % global_n)
+        elif args.witness_gather > 0:
+            try:
+                nw = args.witness_gather
+                xr = synth.rounds_of(world * nw, rounds=args.rounds, rounds_mix=mix)
+                wshards = [(r * nw, (r + 1) * nw) for r in range(world)]
+                wrows, _ = bdist.shard_rows(xr, wshards)
+                xw = synth.batch(nw, rounds=args.rounds, rounds_mix=mix, first=rank * nw)
+                wb = b2f.DeviceBatch(xw, device=device, total_rows=bdist.trace_window(wrows))
+                wb.fill(eng, stream)
+                eng.sync(stream)
+                witness = witness_gather(wb.advice, wb.fixed, wrows,
+                                         "a separate %d-instance batch per rank" % nw)
+                del wb
+            except Exception as e:
+                witness = {"error": repr(e)}
+
     # roofline: algorithmic bytes per launch / average launch duration (HIP events)
+    n = n_local
     fill_bytes = n * INPUT_BYTES + rows * ROW_BYTES      # inputs read + trace written
     eval_bytes = rows * ROW_BYTES + 8 * (n + 1)          # trace + offsets read
 
@@ -282,42 +398,49 @@ def main():
     roof = {"bound": "hbm", "achieved": kern[dom]["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": kern[dom]["frac"], "traffic": traffic, "kernel": dom}
 
-    # same-box floors (diagnostic kernel variants, reported beside the headline): the fill with
-    # its stores but no cell computation (B2F_DIAG_FILL=2) and the eval with its loads, staging
-    # and lookups but no gates or copies (B2F_DIAG_EVAL=1). Boxes differ by up to ~25 % on the
-    # store-bound fill, so the achieved/floor ratio is the comparable number.
+    # same-box floors, from the diagnostics library (libb2f_diag.so; the product library has
+    # no diagnostic variants): the fill with its stores but no cell computation
+    # (B2F_DIAG_FILL=2) and the eval with its loads, staging and lookups but no gates or copies
+    # (B2F_DIAG_EVAL=1). Boxes differ by up to ~25 % on the store-bound fill, so the
+    # achieved/floor ratio is the comparable number.
     floors = None
     if world == 1 and args.floor_reps > 0:
-        floors = {}
-        for var, val, kname in (("B2F_DIAG_FILL", "2", "fill"), ("B2F_DIAG_EVAL", "1", "eval")):
-            os.environ[var] = val
-            try:
-                eng.set_timing(True)
-                for _ in range(args.floor_reps):
-                    if kname == "fill":
-                        batch.fill(eng, stream)
-                    else:
-                        batch.evaluate(eng, stream)
-                tot, cnt = eng.kernel_times()[kname]
-            finally:
-                os.environ.pop(var, None)
-            floors[kname + "_floor_ms"] = round(tot / max(cnt, 1), 4)
-            floors[kname + "_over_floor"] = round(kern[kname]["avg_ms"] / (tot / max(cnt, 1)), 4) \
-                if kname in kern else None
-        batch.fill(eng, stream)  # leave a real trace behind
-        eng.sync(stream)
+        try:
+            deng = b2f.Engine(local, diag=True)
+            floors = {}
+            for var, val, kname in (("B2F_DIAG_FILL", "2", "fill"), ("B2F_DIAG_EVAL", "1", "eval")):
+                os.environ[var] = val
+                try:
+                    deng.set_timing(True)
+                    for _ in range(args.floor_reps):
+                        if kname == "fill":
+                            batch.fill(deng, stream)
+                        else:
+                            batch.evaluate(deng, stream)
+                    tot, cnt = deng.kernel_times()[kname]
+                finally:
+                    os.environ.pop(var, None)
+                floors[kname + "_floor_ms"] = round(tot / max(cnt, 1), 4)
+                floors[kname + "_over_floor"] = round(kern[kname]["avg_ms"] / (tot / max(cnt, 1)), 4) \
+                    if kname in kern else None
+            deng.sync(stream)
+            deng.close()
+            batch.fill(eng, stream)  # leave a real trace behind
+            eng.sync(stream)
+        except (OSError, b2f.B2FError) as e:
+            floors = {"error": repr(e)}
 
     # the other path, timed the same way (reported beside the headline, not part of it)
     aux = None
     other = "fused" if args.path == "split" else "split"
     if args.aux_steps > 0 and world == 1:
-        run_path(other)
+        run_path(batch, other)
         eng.sync(stream)
         eng.set_timing(True)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(args.aux_steps):
-            run_path(other)
+            run_path(batch, other)
         torch.cuda.synchronize()
         el = time.perf_counter() - t1
         k2 = kernel_table(eng.kernel_times())
@@ -330,7 +453,7 @@ def main():
     # Fp export, reported beside the headline, not part of it:
     # Montgomery pallas limbs for a chunk of the resident trace (4 B read, 32 B written/cell)
     fp_export = None
-    if args.export_rows > 0:
+    if args.export_rows > 0 and world == 1:
         nr = min(args.export_rows, batch.total_rows)
         out = torch.empty((10, nr, 4), dtype=torch.int64, device=batch.advice.device)
         batch.export_fp(eng, nrows=nr, out=out, stream=stream)
@@ -405,29 +528,56 @@ def main():
         except Exception as e:
             hasher_aux = {"error": repr(e)}
 
+    # BASELINE configs[3] after a weak-scaling headline at N = 8: 2^20 instances sharded over
+    # the ranks, fill + eval timed the same way, then the whole witness table gathered
+    config4 = None
+    if world == 8 and not global_n and args.config4 > 0:
+        try:
+            del batch
+            torch.cuda.empty_cache()
+            b4, i4 = make_batch(args.config4)
+            el4, _, _ = timed_loop(b4, i4, args.path, args.steps, 1, args.config4)
+            config4 = {"global_batch": args.config4, "rows_per_rank": i4["rows"],
+                       "value": round(args.config4 * args.steps / el4, 1),
+                       "ms_per_step": round(1e3 * el4 / args.steps, 4), "scaling": "strong",
+                       "witness_gather": witness_gather(b4.advice, b4.fixed, i4["rows"],
+                                                        "the step's own trace (%d instances)"
+                                                        % args.config4, reps=1)}
+            del b4
+        except Exception as e:
+            config4 = {"error": repr(e)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.rounds, mix, args.cpu_seconds)
+        cpu = cpu_baseline(args.rounds, mix, args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
-        workload = ("%d x %s-round BLAKE2f compressions per GPU: Table16 witness fill + "
-                    "constraint eval (LAYOUT v1)" % (n, "{1,4,12}-mixed" if mix else args.rounds))
+        if global_n:
+            workload = ("%d x %s-round BLAKE2f compressions sharded over %d GPUs (row-balanced): "
+                        "Table16 witness fill + constraint eval (LAYOUT v1)"
+                        % (global_n, "{1,4,12}-mixed" if mix else args.rounds, world))
+        else:
+            workload = ("%d x %s-round BLAKE2f compressions per GPU: Table16 witness fill + "
+                        "constraint eval (LAYOUT v1)"
+                        % (n, "{1,4,12}-mixed" if mix else args.rounds))
         out = {"metric": "BLAKE2f compressions/sec (witness+constraint eval), 2^18 batch, "
                          "1/2/4/8 GPU",
                "value": round(value, 1), "unit": "compressions/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+               "higher_is_better": True, "scaling": "strong" if global_n else "weak",
+               "vs_baseline": None, "dtype": "u32",
                "data": "synthetic (seeded splitmix64 h/m/t/f)",
-               "config": {"workload": workload, "batch_per_gpu": n,
+               "config": {"workload": workload, "batch_per_gpu": n, "global_batch": total_n,
                           "rounds": "mix{1,4,12}" if mix else args.rounds,
                           "rows_per_gpu": rows, "trace_bytes_per_gpu": rows * ROW_BYTES,
                           "path": args.path,
                           "parallelism": "dp%d (instance shards)" % world},
                "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "floors": floors,
                "other_path": aux,
-               "collectives": collectives, "witness_gather": witness_gather,
+               "collectives": collectives, "witness_gather": witness, "config4": config4,
                "fp_export": fp_export, "lookup_columns": lookup, "hasher": hasher_aux,
-               "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None}
+               "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
+               "gpu_vs_cpu_threads": cpu["cores"] if cpu else None}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -14,11 +14,15 @@
  * batch of independent compressions; one b2f_eval call is the MockProver check of the
  * resulting trace. The trace contract is docs/LAYOUT.md (LAYOUT v1).
  *
- * Threading: one context per device, externally synchronized. `*_dev` calls are
- * stream-ordered and asynchronous; b2f_sync() waits and returns any device-side error.
- * Host-pointer calls block. No call aborts; errors come back as B2F_* status codes with a
- * message in b2f_last_error(). They map onto halo2's plonk::Error at a Rust call site:
- * B2F_ERR_ROWS -> NotEnoughRowsAvailable, the others -> Synthesis.
+ * Threading: one context per device, externally synchronized, and used on ONE stream at a
+ * time: a context owns per-call scratch (half-round states, tile index, lookup scratch) that
+ * every stream-ordered call reuses, so two `*_dev` calls of one context in flight on two
+ * streams race on it. Use one context per concurrent stream. `*_dev` calls are
+ * stream-ordered and asynchronous; b2f_sync() waits and returns any device-side error raised
+ * since the previous b2f_sync (errors are sticky until then). Host-pointer calls block. No
+ * call aborts; errors come back as B2F_* status codes with a message in b2f_last_error().
+ * They map onto halo2's plonk::Error at a Rust call site: B2F_ERR_ROWS ->
+ * NotEnoughRowsAvailable, the others -> Synthesis.
  */
 #ifndef B2F_H
 #define B2F_H
@@ -36,6 +40,8 @@ extern "C" {
 #define B2F_NUM_GATES 16       /* selector bits, docs/LAYOUT.md §4 */
 #define B2F_CODE_LOOKUP 16
 #define B2F_CODE_COPY 17
+#define B2F_CODE_FIXED 18   /* fixed-column cell differs from the keygen structure */
+#define B2F_CODE_LAYOUT 19  /* the row map was rejected: nothing was checked */
 #define B2F_MAX_ROUNDS (1u << 20)
 
 /* Status codes */
@@ -58,14 +64,21 @@ typedef struct {
 } b2f_input;
 
 /* MockProver-equivalent verdict (docs/LAYOUT.md §6). first_failure = min over all failures
- * of (row << 8) | code (code = selector bit 0..15, B2F_CODE_LOOKUP, B2F_CODE_COPY),
- * UINT64_MAX when every constraint holds. */
+ * of (row << 8) | code (code = selector bit 0..15, B2F_CODE_LOOKUP, B2F_CODE_COPY,
+ * B2F_CODE_FIXED), UINT64_MAX when every constraint holds.
+ * fixed_failures: rows whose fixed cell (selector mask | k_0 << 16) differs from the one the
+ * keygen structure of the row map puts there (b2f_fill_fixed_dev): halo2 fixes selectors and
+ * constants at keygen, so a trace checked under a caller-altered fixed column is rejected even
+ * when its advice is consistent with the altered selectors.
+ * A rejected row map (B2F_ERR_LAYOUT) leaves rows_checked = 0 and first_failure =
+ * B2F_CODE_LAYOUT: the report never reads clean for a batch that was not checked. */
 typedef struct {
     uint64_t gate_failures[B2F_NUM_GATES];
     uint64_t lookup_failures;
     uint64_t copy_failures;
     uint64_t first_failure;
     uint64_t rows_checked;
+    uint64_t fixed_failures;
 } b2f_eval_report;
 
 typedef struct b2f_ctx b2f_ctx;
@@ -135,10 +148,28 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
 B2F_API int b2f_debug_inject(b2f_ctx* ctx, uint64_t row, uint32_t col, uint32_t mask);
 
 /* Diagnostics: eval-kernel phase cycle totals (s_memtime deltas summed over workgroups) of
- * the B2F_DIAG_EVAL=23 (EVAL_CLOCK) variant since the previous call; out[8 * wave + phase],
- * phases: stage+lookups, barrier 1, prefetch issue, G-table build, gate pass, copies,
- * per-quad paths, barrier 2. Zeros when that variant never ran. Clears the totals. */
+ * the EVAL_CLOCK variant since the previous call; out[8 * wave + phase], phases:
+ * stage+lookups, barrier 1, prefetch issue, G-table build, gate pass, copies, per-quad paths,
+ * barrier 2. That variant exists only in the diagnostics build of this ABI (libb2f_diag.so,
+ * selected there by B2F_DIAG_EVAL=23); the product library (libb2f.so) reads no environment,
+ * launches only the full kernels and returns zeros here. Clears the totals. */
 B2F_API int b2f_debug_clock(b2f_ctx* ctx, uint64_t* out);
+
+/* Keygen structure (halo2 keygen_vk / keygen_pk over Value::unknown() witnesses,
+ * benchmarking/src/blake2f_circuit_bench.rs:54-55; SURVEY.md §8(b) "Semantics to preserve"):
+ * the fixed column of a batch from its row map alone, no witness -- selector masks and the
+ * IV constants k_0 (LAYOUT.md §4/§5), zeros past offsets[n]. Equal to the d_fixed that
+ * b2f_fill_dev writes for any witness of the same rounds. B2F_ERR_LAYOUT (at b2f_sync) for an
+ * invalid row map. d_fixed 16-byte aligned, total_rows a multiple of 4. Asynchronous. */
+B2F_API int b2f_fill_fixed_dev(b2f_ctx* ctx, const uint64_t* d_offsets, size_t n,
+                               uint64_t total_rows, uint32_t* d_fixed, void* stream);
+
+/* The copy constraints (equality pairs, `copy_advice` sites: table16.rs:431-433,
+ * compression_util.rs:398-416,548-574) of one instance of `rounds` rounds, as keygen records
+ * them: writes min(count, cap) quadruples (dst_row, dst_col, src_row, src_col), rows relative
+ * to the instance, columns a_0..a_9 (b2f_halo2_column_index maps them to halo2's order), and
+ * returns count = 24 + 576 * rounds + 96 (0 if rounds > B2F_MAX_ROUNDS). Host function. */
+B2F_API uint64_t b2f_copy_constraints(uint32_t rounds, uint32_t* out4, uint64_t cap);
 
 /* Wait for `stream` and return the first device-side error of the fill/eval calls issued
  * since the previous b2f_sync (B2F_ERR_LAYOUT / B2F_ERR_ROUNDS), then clear it. */

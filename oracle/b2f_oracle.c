@@ -113,6 +113,12 @@ typedef struct {
     uint32_t* copies;   /* structure mode: (dst_row, dst_col, src_row, src_col) */
     size_t ncopies, cap;
     int record;         /* structure mode: count (and store up to cap) copy pairs */
+    /* test-only tampering (orc_fill_tampered): 1 = the ADD block at tamper_row adds
+     * tamper_delta to its sum and leaves its selector off; 2 = the CONST block at tamper_row
+     * uses IV ^ tamper_delta (advice and k_0 alike) */
+    int tamper_kind;
+    uint32_t tamper_row;
+    uint64_t tamper_delta;
 } region_t;
 
 static inline void put(region_t* R, int col, uint32_t row, uint32_t v) {
@@ -161,6 +167,7 @@ static word_t blk_inw(region_t* R, uint32_t r0, uint64_t w) {
 }
 
 static word_t blk_const(region_t* R, uint32_t r0, uint64_t w) {
+    if (R->tamper_kind == 2 && r0 == R->tamper_row) w ^= R->tamper_delta;
     word_t o; o.val = w;
     for (unsigned k = 0; k < 4; k++) {
         lookup_row(R, r0 + k, limb(w, k));
@@ -243,6 +250,8 @@ static word_t blk_add(region_t* R, uint32_t r0, const word_t* A, const word_t* B
                       const word_t* M, int sel) {
     unsigned __int128 full = (unsigned __int128)A->val + B->val + (M ? M->val : 0);
     uint64_t s = (uint64_t)full;
+    const int tampered = R->tamper_kind == 1 && r0 == R->tamper_row;
+    if (tampered) s += R->tamper_delta;
     word_t o; o.val = s;
     for (unsigned k = 0; k < 4; k++) {
         lookup_row(R, r0 + k, limb(s, k));
@@ -252,7 +261,7 @@ static word_t blk_add(region_t* R, uint32_t r0, const word_t* A, const word_t* B
         o.d[k] = C(r0 + k, A1); o.s[k] = C(r0 + k, A2);
     }
     put(R, A9, r0, (uint32_t)(full >> 64));
-    enable(R, sel, r0);
+    if (!tampered) enable(R, sel, r0);
     return o;
 }
 
@@ -327,6 +336,33 @@ size_t orc_copies(uint32_t rounds, uint32_t* out4, size_t cap) {
     R.record = 1;
     synthesize(&R, &in, NULL);
     return R.ncopies;
+}
+
+/* Structure-mode synthesize of the fixed column of one instance (rows [0, R(rounds))). */
+static void fixed_structure(uint32_t rounds, uint32_t* fixed) {
+    orc_input in;
+    memset(&in, 0, sizeof in);
+    in.rounds = rounds;
+    memset(fixed, 0, orc_rows(rounds) * sizeof(uint32_t));
+    region_t R;
+    memset(&R, 0, sizeof R);
+    R.fixed = fixed;
+    synthesize(&R, &in, NULL);
+}
+
+static int rows_ok(uint64_t R) {
+    return R >= INIT_ROWS + FINAL_ROWS && (R - INIT_ROWS - FINAL_ROWS) % ROUND_ROWS == 0;
+}
+
+int orc_fixed(const uint64_t* offsets, size_t n, uint64_t total_rows, uint32_t* fixed) {
+    if (offsets[0] != 0 || offsets[n] > total_rows) return -1;
+    for (size_t i = 0; i < n; i++)
+        if (offsets[i + 1] < offsets[i] || !rows_ok(offsets[i + 1] - offsets[i])) return -1;
+    memset(fixed, 0, total_rows * sizeof(uint32_t));
+    for (size_t i = 0; i < n; i++)
+        fixed_structure((uint32_t)((offsets[i + 1] - offsets[i] - INIT_ROWS - FINAL_ROWS) / ROUND_ROWS),
+                        fixed + offsets[i]);
+    return 0;
 }
 
 /* ---------------------------------------------------------------- Fp export (§8(f) row 1)
@@ -430,8 +466,9 @@ int orc_max_threads(void) {
 #endif
 }
 
-int orc_fill(const orc_input* in, size_t n, const uint64_t* offsets, uint64_t total_rows,
-             uint32_t* advice, uint32_t* fixed, uint64_t* h_out, int nthreads) {
+static int fill_impl(const orc_input* in, size_t n, const uint64_t* offsets, uint64_t total_rows,
+                     uint32_t* advice, uint32_t* fixed, uint64_t* h_out, int nthreads,
+                     size_t t_inst, int t_kind, uint32_t t_row, uint64_t t_delta) {
     for (size_t i = 0; i < n; i++)
         if (offsets[i + 1] - offsets[i] != orc_rows(in[i].rounds)) return -1;
     if (offsets[n] > total_rows) return -1;
@@ -452,12 +489,26 @@ int orc_fill(const orc_input* in, size_t n, const uint64_t* offsets, uint64_t to
         region_t R;
         memset(&R, 0, sizeof R);
         R.adv = advice; R.fixed = fixed; R.stride = total_rows; R.base = offsets[i];
+        if ((size_t)i == t_inst) {
+            R.tamper_kind = t_kind; R.tamper_row = t_row; R.tamper_delta = t_delta;
+        }
         uint64_t out[8];
         synthesize(&R, &in[i], out);
         if (h_out) memcpy(h_out + 8 * i, out, sizeof out);
     }
     (void)nthreads;
     return 0;
+}
+
+int orc_fill(const orc_input* in, size_t n, const uint64_t* offsets, uint64_t total_rows,
+             uint32_t* advice, uint32_t* fixed, uint64_t* h_out, int nthreads) {
+    return fill_impl(in, n, offsets, total_rows, advice, fixed, h_out, nthreads, (size_t)-1, 0, 0, 0);
+}
+
+int orc_fill_tampered(const orc_input* in, size_t n, const uint64_t* offsets,
+                      uint64_t total_rows, uint32_t* advice, uint32_t* fixed, uint64_t* h_out,
+                      size_t inst, int kind, uint32_t row, uint64_t delta) {
+    return fill_impl(in, n, offsets, total_rows, advice, fixed, h_out, 1, inst, kind, row, delta);
 }
 
 /* ------------------------------------------------------------------ eval (LAYOUT.md §6) */
@@ -590,6 +641,7 @@ int orc_eval(const uint32_t* advice, const uint32_t* fixed, const uint64_t* offs
         size_t cap = 0;
         uint32_t cp_rounds = UINT32_MAX;
         size_t ncp = 0;
+        uint32_t* fx = NULL; /* keygen fixed column of cp_rounds */
         /* Rows and gates: chunk the global rows (independent of instance boundaries). */
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic, 4096)
@@ -626,9 +678,18 @@ int orc_eval(const uint32_t* advice, const uint32_t* fixed, const uint64_t* offs
                     cp = (uint32_t*)malloc(4 * cap * sizeof(uint32_t));
                 }
                 ncp = orc_copies(rounds, cp, cap);
+                free(fx);
+                fx = (uint32_t*)malloc(orc_rows(rounds) * sizeof(uint32_t));
+                fixed_structure(rounds, fx);
                 cp_rounds = rounds;
             }
             uint64_t base = offsets[i];
+            /* the fixed column against the keygen structure (halo2 fixes it at keygen) */
+            for (uint64_t r = 0; r < orc_rows(rounds); r++)
+                if (fixed[base + r] != fx[r]) {
+                    loc.fixed_failures++;
+                    note(&loc, base + r, ORC_CODE_FIXED);
+                }
             for (size_t q = 0; q < ncp; q++) {
                 const uint32_t* e = cp + 4 * q;
                 if (A[e[1]][base + e[0]] != A[e[3]][base + e[2]]) {
@@ -638,6 +699,16 @@ int orc_eval(const uint32_t* advice, const uint32_t* fixed, const uint64_t* offs
             }
         }
         free(cp);
+        free(fx);
+        /* rows past the last instance carry no selector or constant */
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+        for (long long rr = (long long)offsets[n]; rr < (long long)total_rows; rr++)
+            if (fixed[rr]) {
+                loc.fixed_failures++;
+                note(&loc, (uint64_t)rr, ORC_CODE_FIXED);
+            }
 #ifdef _OPENMP
 #pragma omp critical
 #endif
@@ -645,6 +716,7 @@ int orc_eval(const uint32_t* advice, const uint32_t* fixed, const uint64_t* offs
             for (int s = 0; s < ORC_NGATES; s++) rep->gate_failures[s] += loc.gate_failures[s];
             rep->lookup_failures += loc.lookup_failures;
             rep->copy_failures += loc.copy_failures;
+            rep->fixed_failures += loc.fixed_failures;
             if (loc.first_failure < rep->first_failure) rep->first_failure = loc.first_failure;
         }
     }

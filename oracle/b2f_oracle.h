@@ -35,6 +35,7 @@ typedef struct {
 #define ORC_NGATES 16
 #define ORC_CODE_LOOKUP 16
 #define ORC_CODE_COPY 17
+#define ORC_CODE_FIXED 18
 
 typedef struct {
     uint64_t gate_failures[ORC_NGATES];
@@ -42,6 +43,7 @@ typedef struct {
     uint64_t copy_failures;
     uint64_t first_failure;  /* min((row << 8) | code), UINT64_MAX if none */
     uint64_t rows_checked;
+    uint64_t fixed_failures; /* rows whose fixed cell differs from the keygen structure */
 } orc_report;
 
 /* R(rounds) = 228 + 416 * rounds (LAYOUT.md §5). */
@@ -52,6 +54,10 @@ void orc_offsets(const orc_input* in, size_t n, uint64_t* offsets);
  * quadruples (instance-relative rows); returns the count. */
 size_t orc_copies(uint32_t rounds, uint32_t* out4, size_t cap);
 
+/* Keygen structure: the fixed column of a batch from its row map alone (structure-mode
+ * synthesis of every instance, zeros past offsets[n]). Returns 0, or -1 on a bad row map. */
+int orc_fixed(const uint64_t* offsets, size_t n, uint64_t total_rows, uint32_t* fixed);
+
 /* RFC 7693 / EIP-152 compression F (README.md:1-97), any rounds. */
 void orc_compress(uint32_t rounds, const uint64_t h[8], const uint64_t m[16],
                   const uint64_t t[2], uint32_t f, uint64_t out[8]);
@@ -61,6 +67,16 @@ void orc_compress(uint32_t rounds, const uint64_t h[8], const uint64_t m[16],
  * nthreads <= 0 means OpenMP default. Returns 0, or -1 on inconsistent offsets. */
 int orc_fill(const orc_input* in, size_t n, const uint64_t* offsets, uint64_t total_rows,
              uint32_t* advice, uint32_t* fixed, uint64_t* h_out, int nthreads);
+
+/* Test-only: a trace that is consistent with an ALTERED fixed column, the case the keygen
+ * structure check exists for. Instance `inst` is synthesized with kind 1: the ADD block whose
+ * first row is `row` (instance-relative) adds `delta` to its sum, assigns the rest of the
+ * compression from that value and leaves its selector off (so no gate sees the wrong sum);
+ * kind 2: the CONST block at `row` assigns IV ^ delta in its advice AND its k_0 cells. Every
+ * gate, lookup and copy constraint holds under the trace's own fixed column. */
+int orc_fill_tampered(const orc_input* in, size_t n, const uint64_t* offsets,
+                      uint64_t total_rows, uint32_t* advice, uint32_t* fixed, uint64_t* h_out,
+                      size_t inst, int kind, uint32_t row, uint64_t delta);
 
 /* MockProver-equivalent check of a trace (LAYOUT.md §6). Returns 0, or -1 when an
  * instance's row count is not R(rounds) for any rounds. */

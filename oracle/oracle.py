@@ -17,6 +17,7 @@ NCOLS = 10
 NGATES = 16
 CODE_LOOKUP = 16
 CODE_COPY = 17
+CODE_FIXED = 18
 
 # orc_input (b2f_oracle.h) as a numpy record: 216 bytes
 INPUT_DTYPE = np.dtype([("h", "<u8", (8,)), ("m", "<u8", (16,)), ("t", "<u8", (2,)),
@@ -29,14 +30,16 @@ class Report(ctypes.Structure):
                 ("lookup_failures", ctypes.c_uint64),
                 ("copy_failures", ctypes.c_uint64),
                 ("first_failure", ctypes.c_uint64),
-                ("rows_checked", ctypes.c_uint64)]
+                ("rows_checked", ctypes.c_uint64),
+                ("fixed_failures", ctypes.c_uint64)]
 
     def as_dict(self):
         return {"gate_failures": list(self.gate_failures),
                 "lookup_failures": self.lookup_failures,
                 "copy_failures": self.copy_failures,
                 "first_failure": self.first_failure,
-                "rows_checked": self.rows_checked}
+                "rows_checked": self.rows_checked,
+                "fixed_failures": self.fixed_failures}
 
 
 _lib = None
@@ -67,6 +70,11 @@ def lib():
         L.orc_export_fp.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                     ctypes.c_uint32, P, ctypes.c_uint64]
         L.orc_fp_mont.argtypes = [ctypes.c_uint32, P]
+        L.orc_fixed.argtypes = [P, ctypes.c_size_t, ctypes.c_uint64, P]
+        L.orc_fill_tampered.argtypes = [P, ctypes.c_size_t, P, ctypes.c_uint64, P, P, P,
+                                        ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32,
+                                        ctypes.c_uint64]
+        L.orc_fixed.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -117,6 +125,24 @@ def fill(inputs, total_rows=None, nthreads=0):
     return adv, fixed, h_out, off
 
 
+TAMPER_ADD, TAMPER_CONST = 1, 2
+
+
+def fill_tampered(inputs, inst, kind, row, delta):
+    """A trace consistent with an altered fixed column (see orc_fill_tampered)."""
+    inputs = np.ascontiguousarray(inputs, dtype=INPUT_DTYPE)
+    off = offsets(inputs)
+    total = int(off[-1])
+    adv = np.empty((NCOLS, total), dtype=np.uint32)
+    fixed = np.empty(total, dtype=np.uint32)
+    h_out = np.zeros((len(inputs), 8), dtype=np.uint64)
+    rc = lib().orc_fill_tampered(_p(inputs), len(inputs), _p(off), total, _p(adv), _p(fixed),
+                                 _p(h_out), int(inst), int(kind), int(row), int(delta))
+    if rc != 0:
+        raise ValueError("orc_fill_tampered: inconsistent offsets")
+    return adv, fixed, h_out, off
+
+
 def evaluate(adv, fixed, off, nthreads=0):
     adv = np.ascontiguousarray(adv, dtype=np.uint32)
     fixed = np.ascontiguousarray(fixed, dtype=np.uint32)
@@ -127,6 +153,16 @@ def evaluate(adv, fixed, off, nthreads=0):
     if rc != 0:
         raise ValueError("orc_eval: offsets are not a LAYOUT v1 row map")
     return rep.as_dict()
+
+
+def fixed_structure(off, total_rows=None):
+    """Keygen fixed column of a row map (structure-mode synthesis, zeros past off[-1])."""
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    total = int(off[-1]) if total_rows is None else int(total_rows)
+    fx = np.empty(total, dtype=np.uint32)
+    if lib().orc_fixed(_p(off), len(off) - 1, total, _p(fx)) != 0:
+        raise ValueError("orc_fixed: offsets are not a LAYOUT v1 row map")
+    return fx
 
 
 FP_CANONICAL, FP_MONTGOMERY = 0, 1

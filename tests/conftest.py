@@ -41,6 +41,17 @@ def engine():
     eng.close()
 
 
+@pytest.fixture(scope="session")
+def diag_engine():
+    """An engine on the diagnostics build (libb2f_diag.so): fused band sizes other than the
+    product's, kernel floors. Never the product path."""
+    import b2f
+
+    eng = b2f.Engine(0, diag=True)
+    yield eng
+    eng.close()
+
+
 def random_inputs(n, rounds_choices=(12,), seed=1):
     import b2f
 

@@ -92,18 +92,46 @@ def test_null_context_calls_fail_cleanly():
     assert lib.b2f_last_error(None) == b"null context"
 
 
-def test_missing_library_fails_loudly(tmp_path):
+def test_missing_library_fails_loudly():
     """No fallback: without the HIP library every entry point raises (checked in a fresh
     interpreter so the loaded library of this session is not reused)."""
-    import os
     import subprocess
     import sys
 
     code = ("import sys; sys.path.insert(0, %r)\n"
-            "import b2f\n"
+            "import b2f\nfrom b2f import _lib\n"
+            "_lib.LIB_PATH = '/nonexistent/libb2f.so'\n"
             "try:\n    b2f.load()\nexcept OSError as e:\n    print('raised', 'not found' in str(e))\n"
             "try:\n    b2f.Engine(0)\nexcept OSError as e:\n    print('raised2')\n") % (ROOT + "/zk-odst_amd")
-    env = dict(os.environ, B2F_LIB=str(tmp_path / "absent.so"))
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
-                         timeout=120)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert "raised True" in out.stdout and "raised2" in out.stdout, out.stdout + out.stderr
+
+
+def test_product_library_reads_no_environment():
+    """the diagnostic kernel variants (selected by B2F_DIAG_* / B2F_BAND /
+    B2F_FILL_WGS) live only in libb2f_diag.so; libb2f.so does not even contain the names, so
+    no environment can swap a product kernel for a diagnostic one."""
+    from b2f import _lib
+
+    prod = open(_lib.LIB_PATH, "rb").read()
+    diag = open(_lib.DIAG_LIB_PATH, "rb").read()
+    for var in (b"B2F_DIAG_EVAL", b"B2F_DIAG_FILL", b"B2F_DIAG_FUSED", b"B2F_BAND", b"B2F_FILL_WGS"):
+        assert var not in prod, var
+        assert var in diag, var
+    lib = _lib.load(diag=True)
+    for name, _, _ in _lib.SIGNATURES:
+        assert hasattr(lib, name), name
+
+
+@pytest.mark.parametrize("rounds", [0, 1, 2, 12, 13])
+def test_copy_constraints_match_oracle_structure(orc, rounds):
+    """b2f_copy_constraints (the product's keygen copy list, host code) == the equality pairs
+    the oracle's structure-mode synthesis records, as sets; count 24 + 576 rounds + 96."""
+    import b2f
+
+    got = b2f.copy_constraints(rounds)
+    want = orc.copies(rounds)
+    assert len(got) == 24 + 576 * rounds + 96 == len(want)
+    key = lambda a: sorted(map(tuple, a.tolist()))  # noqa: E731
+    assert key(got) == key(want)
+    assert len(set(map(tuple, got[:, :2].tolist()))) == len(got)  # one copy per operand cell

@@ -33,18 +33,25 @@ def _worker(rank, world, port, inputs_bytes, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     x = np.frombuffer(inputs_bytes, dtype=INPUT_DTYPE)
     shards = bdist.plan_shards(x, world)
+    srows, sbase = bdist.shard_rows(x, shards)
+    w = bdist.trace_window(srows)
     lo, hi = shards[rank]
     ox = np.frombuffer(x[lo:hi].tobytes(), dtype=oracle.INPUT_DTYPE).copy()
-    adv, fixed, h_out, off = oracle.fill(ox)
+    adv, fixed, h_out, off = oracle.fill(ox, total_rows=w)  # the common window, zero tail
     if rank == 1:  # a corruption on one rank must show in the combined verdict
         adv[1, 5] += 1
     rep = oracle.evaluate(adv, fixed, off)
-    combined = bdist.reduce_report(rep, dist, torch, "cpu")
+    combined = bdist.reduce_report(rep, dist, torch, "cpu", row_offset=sbase[rank])
+    # the device-tensor form bench.py uses (no host round trip)
+    raw = np.array([*rep["gate_failures"], rep["lookup_failures"], rep["copy_failures"],
+                    rep["first_failure"], rep["rows_checked"], rep["fixed_failures"]],
+                   dtype=np.uint64)
+    words = bdist.all_reduce_verdict(
+        bdist.verdict_words(torch.from_numpy(raw.view(np.int64)), sbase[rank], torch), dist)
     h = bdist.gather_h_out(torch.from_numpy(h_out.view(np.int64)), shards, dist, torch)
-    srows = [int(bdist.offsets(x[a:b])[-1]) for a, b in shards]
     ga, gf = bdist.gather_trace(torch.from_numpy(adv.view(np.int32)),
                                 torch.from_numpy(fixed.view(np.int32)), srows, dist, torch)
-    q.put((rank, combined, h.numpy().view(np.uint64).tobytes(), shards,
+    q.put((rank, combined, words.tolist(), h.numpy().view(np.uint64).tobytes(), shards, sbase,
            ga.numpy().view(np.uint32).tobytes(), gf.numpy().view(np.uint32).tobytes()))
     dist.destroy_process_group()
 
@@ -62,10 +69,16 @@ def test_plan_shards_balances_rows():
         assert max(rows) - min(rows) <= 2 * 5220  # within two instances of even
 
 
-def test_gloo_world2_matches_single_process(orc):
+@pytest.mark.parametrize("n,rounds,seed", [(37, (0, 1, 4, 12), 42), (23, (1, 4, 12), 43)])
+def test_gloo_world2_matches_single_process(orc, n, rounds, seed):
+    """Unequal mixed-rounds shards: the all-gathered witness table is the single-process
+    trace (total_rows = world x window), h' is the batch's, and the combined verdict equals the
+    oracle's verdict on the reassembled table, first failure at its global row."""
     import multiprocessing as mp
 
-    x = random_inputs(37, (0, 1, 4, 12), 42)
+    from b2f import dist as bdist
+
+    x = random_inputs(n, rounds, seed)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -77,16 +90,22 @@ def test_gloo_world2_matches_single_process(orc):
         p.join(timeout=60)
         assert p.exitcode == 0
     ox = np.frombuffer(x.tobytes(), dtype=orc.INPUT_DTYPE).copy()
-    adv_ref, fixed_ref, h_ref, off_ref = orc.fill(ox)
-    adv_ref = adv_ref.copy()
-    for rank, combined, hbytes, shards, abytes, fbytes in res:
+    shards = res[0][4]
+    srows, _ = bdist.shard_rows(x, shards)
+    assert srows[0] != srows[1], "the shards must be unequal for this test"
+    total = 2 * bdist.trace_window(srows)
+    adv_ref, fixed_ref, h_ref, off_ref = orc.fill(ox, total_rows=total)
+    want = adv_ref.copy()
+    want[1, int(off_ref[shards[1][0]]) + 5] += 1  # rank 1's corrupted cell at its global row
+    want_rep = orc.evaluate(want, fixed_ref, off_ref)
+    # the INW gate of that word fails on its block row, 4 rows into rank 1's shard
+    assert want_rep["first_failure"] >> 8 == int(off_ref[shards[1][0]]) + 4
+    for rank, combined, words, hbytes, sh, sbase, abytes, fbytes in res:
         assert np.array_equal(np.frombuffer(hbytes, dtype=np.uint64).reshape(-1, 8), h_ref)
-        # the reassembled witness table is the single-process trace (with rank 1's corrupted
-        # cell at its global row)
         ga = np.frombuffer(abytes, dtype=np.uint32).reshape(10, -1)
-        want = adv_ref.copy()
-        want[1, int(off_ref[shards[1][0]]) + 5] += 1
         assert np.array_equal(ga, want)
         assert np.array_equal(np.frombuffer(fbytes, dtype=np.uint32), fixed_ref)
-        assert combined["lookup_failures"] >= 1 and combined["first_failure"] != 2**64 - 1
-        assert combined["rows_checked"] == int(orc.offsets(ox)[-1])
+        assert combined == want_rep
+        assert words[:16] == want_rep["gate_failures"]
+        assert words[16:20] == [want_rep["lookup_failures"], want_rep["copy_failures"],
+                                want_rep["fixed_failures"], want_rep["first_failure"]]

@@ -18,6 +18,11 @@ from conftest import random_inputs
 pytestmark = pytest.mark.gpu
 
 NONE = 2**64 - 1
+PRODUCT_BAND = 16  # the band libb2f.so launches; other bands run on the diagnostics build
+
+
+def _pick(engine, diag_engine, band):
+    return engine if band == PRODUCT_BAND else diag_engine
 
 
 def _as_oracle(x, orc):
@@ -31,9 +36,11 @@ def _stream():
 
 
 def _fused(engine, x, band, total_rows=None, inject=None):
-    """One b2f_fill_eval_dev call on a fresh DeviceBatch (buffers poisoned first)."""
+    """One b2f_fill_eval_dev call on a fresh DeviceBatch (buffers poisoned first). A band other
+    than the product's needs the diagnostics engine (B2F_BAND is read only there)."""
     import b2f
 
+    assert band == PRODUCT_BAND or engine.diag, "band %d needs the diagnostics build" % band
     os.environ["B2F_BAND"] = str(band)
     try:
         batch = b2f.DeviceBatch(x, total_rows=total_rows)
@@ -52,9 +59,9 @@ def _fused(engine, x, band, total_rows=None, inject=None):
 @pytest.mark.parametrize("band", [1, 2, 3, 16])
 @pytest.mark.parametrize("rounds_choices,n,seed", [((12,), 23, 31), ((0, 1, 4, 12, 13), 71, 32),
                                                    ((1,), 200, 33)])
-def test_fused_equals_oracle(engine, orc, band, rounds_choices, n, seed):
+def test_fused_equals_oracle(engine, diag_engine, orc, band, rounds_choices, n, seed):
     x = random_inputs(n, rounds_choices, seed)
-    batch = _fused(engine, x, band)
+    batch = _fused(_pick(engine, diag_engine, band), x, band)
     adv, fixed = batch.host_trace()
     oadv, ofixed, oh, ooff = orc.fill(_as_oracle(x, orc))
     for c in range(10):
@@ -67,13 +74,13 @@ def test_fused_equals_oracle(engine, orc, band, rounds_choices, n, seed):
     assert rep["first_failure"] == NONE and rep["rows_checked"] == int(ooff[-1])
 
 
-def test_fused_padded_tail(engine, orc):
+def test_fused_padded_tail(engine, diag_engine, orc):
     """total_rows past the batch (not a multiple of the 1024-row tile): zero rows, clean."""
     import b2f
 
     x = random_inputs(9, (1, 4), 34)
     total = int(b2f.offsets(x)[-1]) + 1028
-    batch = _fused(engine, x, 2, total_rows=total)
+    batch = _fused(diag_engine, x, 2, total_rows=total)
     adv, fixed = batch.host_trace()
     used = batch.used_rows
     assert not adv[:, used:].any() and not fixed[used:].any()
@@ -97,13 +104,14 @@ def _boundary_rows(total, rng, k):
 
 
 @pytest.mark.parametrize("band", [1, 3, 16])
-def test_fused_injection_matches_eval(engine, orc, band):
+def test_fused_injection_matches_eval(engine, diag_engine, orc, band):
     """Fused verdict == b2f_eval_dev verdict on the trace the fused kernel wrote, for single
     cell faults in every column (advice and fixed) at tile/band boundaries; the written trace
     differs from the clean one in exactly the injected cell; a subset is checked against the
     oracle too."""
     import torch
 
+    engine = _pick(engine, diag_engine, band)
     rng = np.random.default_rng(40 + band)
     x = random_inputs(24, (0, 1, 4, 12), 41)
     clean = _fused(engine, x, band)
@@ -137,7 +145,7 @@ def test_fused_injection_matches_eval(engine, orc, band):
     assert flagged > cases // 3
 
 
-def test_fused_injection_last_rows(engine, orc):
+def test_fused_injection_last_rows(diag_engine, orc):
     """Selector bits injected into the last rows of the trace: gates that run past the end
     read zero rows (the eval's out-of-trace rule) -- through the fused kernel's zero halo."""
     import b2f
@@ -148,7 +156,7 @@ def test_fused_injection_last_rows(engine, orc):
     for total_rows in (total, total_p):
         for r in (total_rows - 1, total_rows - 3, total_rows - 7, total_rows - 12):
             for bit in (0, 1, 4, 6, 8, 11, 13, 15):
-                batch = _fused(engine, x, 2, total_rows=total_rows, inject=(r, 10, 1 << bit))
+                batch = _fused(diag_engine, x, 2, total_rows=total_rows, inject=(r, 10, 1 << bit))
                 got = batch.report_dict()
                 adv, fixed = batch.host_trace()
                 assert got == orc.evaluate(adv, fixed, batch.offsets_host), (total_rows, r, bit)

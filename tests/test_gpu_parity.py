@@ -211,7 +211,7 @@ def test_2p18_corruptions_past_2p30_rows(engine, orc):
     engine.sync(stream)
     got = batch.report_dict()
     want = {"gate_failures": [0] * 16, "lookup_failures": 0, "copy_failures": 0,
-            "first_failure": 2**64 - 1, "rows_checked": batch.used_rows}
+            "first_failure": 2**64 - 1, "rows_checked": batch.used_rows, "fixed_failures": 0}
     for i in sorted({f[0] for f in faults}):
         r0, r1 = int(off[i]), int(off[i + 1])
         adv = batch.advice[:, r0:r1].cpu().numpy().view(np.uint32)
@@ -221,6 +221,7 @@ def test_2p18_corruptions_past_2p30_rows(engine, orc):
         want["gate_failures"] = [a + b for a, b in zip(want["gate_failures"], o["gate_failures"])]
         want["lookup_failures"] += o["lookup_failures"]
         want["copy_failures"] += o["copy_failures"]
+        want["fixed_failures"] += o["fixed_failures"]
         first = o["first_failure"] + (r0 << 8)  # (row << 8) | code, row made global
         want["first_failure"] = min(want["first_failure"], first)
     assert got == want

@@ -167,3 +167,36 @@ def test_fp_export_layout(orc):
         for r in rng.integers(0, nr, 40):
             v = int(adv[a, r0 + r])
             assert _limbs_to_int(mont[h, r]) == (v << 256) % P_PALLAS
+
+
+def test_keygen_fixed_structure_equals_fill(orc):
+    """The fixed column from the row map alone (keygen) is the fill's fixed column."""
+    x = random_inputs(9, (0, 1, 4, 12), 61)
+    ox = np.frombuffer(x.tobytes(), dtype=orc.INPUT_DTYPE).copy()
+    adv, fixed, _, off = orc.fill(ox, total_rows=int(orc.offsets(ox)[-1]) + 40)
+    assert np.array_equal(orc.fixed_structure(off, total_rows=fixed.shape[0]), fixed)
+
+
+@pytest.mark.parametrize("kind,row,delta", [
+    (1, 164 + 416 * 1 + 52 * 3 + 0, 1 << 40),       # an a1 add, round 1, G 3
+    (1, 164 + 416 * 3 + 52 * 7 + 28, 12345),        # the last a2 add of the last round
+    (1, 164 + 416 * 0 + 52 * 0 + 12, 1),            # a c1 add (ADD2)
+    (2, 108 + 4 * 5, 0x0000_0001_0000_0000),        # IV5 (feeds v13 = IV5 ^ t1)
+    (2, 108 + 4 * 0, 0xffff),                       # IV0 (v8)
+])
+def test_tampered_trace_caught_only_by_the_fixed_check(orc, kind, row, delta):
+    """a trace whose advice is consistent with an altered fixed column (a
+    cleared ADD selector with a wrong sum propagated downstream, or a wrong IV constant in both
+    the advice and k_0) passes every gate, lookup and copy constraint; only the check of the
+    fixed column against the keygen structure flags it."""
+    x = random_inputs(3, (4,), 62)
+    ox = np.frombuffer(x.tobytes(), dtype=orc.INPUT_DTYPE).copy()
+    adv, fixed, h_out, off = orc.fill_tampered(ox, 1, kind, row, delta)
+    _, good_fixed, good_h, _ = orc.fill(ox)
+    assert not np.array_equal(h_out[1], good_h[1])  # the compression output is wrong
+    rep = orc.evaluate(adv, fixed, off)
+    assert sum(rep["gate_failures"]) == rep["lookup_failures"] == rep["copy_failures"] == 0
+    bad_rows = np.nonzero(fixed != good_fixed)[0]
+    assert rep["fixed_failures"] == len(bad_rows) >= 1
+    assert rep["first_failure"] == (int(bad_rows[0]) << 8) | orc.CODE_FIXED
+    assert int(off[1]) + row <= int(bad_rows[0]) < int(off[1]) + row + 4  # the altered block

@@ -6,4 +6,4 @@ mirror of the reference's gadget API (blake2f-circuit/src/blake2f.rs) over that 
 from ._lib import FP_CANONICAL, FP_MONTGOMERY, B2FError, EvalReport, load  # noqa: F401
 from .layout import (INPUT_DTYPE, SELECTORS, as_inputs, halo2_column_index, offsets,  # noqa: F401
                      parse_eip152, rows, split_fixed)
-from .engine import DeviceBatch, Engine  # noqa: F401
+from .engine import DeviceBatch, Engine, copy_constraints  # noqa: F401

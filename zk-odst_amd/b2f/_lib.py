@@ -3,19 +3,26 @@ __graft_entry__.build() / `make -C zk-odst_amd`).
 
 There is no fallback: if the HIP library is missing or fails to load, every entry point
 raises. The product path never touches oracle/.
+
+libb2f.so is the product library: it reads no environment and launches only the full
+kernels. libb2f_diag.so is the same ABI built with -DB2F_DIAG, whose diagnostic kernel
+variants (floors, ablations, phase clocks) are selected by B2F_DIAG_* variables; it is loaded
+only on explicit request (load(diag=True) / Engine(diag=True)) by bench floors and tools/.
 """
 import ctypes
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # zk-odst_amd/
-# B2F_LIB overrides the library path (diagnostic A/B builds of the same ABI)
-LIB_PATH = os.environ.get("B2F_LIB") or os.path.join(PKG_ROOT, "libb2f.so")
+LIB_PATH = os.path.join(PKG_ROOT, "libb2f.so")
+DIAG_LIB_PATH = os.path.join(PKG_ROOT, "libb2f_diag.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "b2f.h")
 
 NUM_ADVICE = 10
 NUM_GATES = 16
 CODE_LOOKUP = 16
 CODE_COPY = 17
+CODE_FIXED = 18
+CODE_LAYOUT = 19
 MAX_ROUNDS = 1 << 20
 KERNEL_NAMES = ["record", "fill", "eval", "export", "fill_eval", "lookup"]  # B2F_KERNEL_*
 FP_CANONICAL, FP_MONTGOMERY = 0, 1  # B2F_FP_*
@@ -37,14 +44,16 @@ class EvalReport(ctypes.Structure):
                 ("lookup_failures", ctypes.c_uint64),
                 ("copy_failures", ctypes.c_uint64),
                 ("first_failure", ctypes.c_uint64),
-                ("rows_checked", ctypes.c_uint64)]
+                ("rows_checked", ctypes.c_uint64),
+                ("fixed_failures", ctypes.c_uint64)]
 
     def as_dict(self):
         return {"gate_failures": list(self.gate_failures),
                 "lookup_failures": self.lookup_failures,
                 "copy_failures": self.copy_failures,
                 "first_failure": self.first_failure,
-                "rows_checked": self.rows_checked}
+                "rows_checked": self.rows_checked,
+                "fixed_failures": self.fixed_failures}
 
 
 REPORT_BYTES = ctypes.sizeof(EvalReport)
@@ -68,6 +77,8 @@ SIGNATURES = [
     ("b2f_fill_eval_dev", I32, [P, P, SIZE, P, U64, P, P, P, P, P]),
     ("b2f_debug_inject", I32, [P, U64, ctypes.c_uint32, ctypes.c_uint32]),
     ("b2f_debug_clock", I32, [P, P]),
+    ("b2f_fill_fixed_dev", I32, [P, P, SIZE, U64, P, P]),
+    ("b2f_copy_constraints", U64, [ctypes.c_uint32, P, U64]),
     ("b2f_chain_inputs_dev", I32, [P, P, P, P, P, ctypes.c_uint32, SIZE, P, P]),
     ("b2f_export_fp_dev", I32, [P, P, U64, U64, U64, ctypes.c_uint32, P, U64, P]),
     ("b2f_lookup_columns_dev", I32, [P, P, U64, P, ctypes.c_uint32, U64, P, P, P,
@@ -79,9 +90,7 @@ SIGNATURES = [
     ("b2f_kernel_times", I32, [P, P, P]),
 ]
 
-OPTIONAL = {"b2f_debug_clock"}
-
-_lib = None
+_libs = {}
 
 
 def _share_hip_runtime_with_torch():
@@ -97,28 +106,27 @@ def _share_hip_runtime_with_torch():
         pass
 
 
-def load():
-    """Load libb2f.so (raises OSError with a build hint when it is absent)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise OSError("libb2f.so not found at %s: build it with "
+def load(diag=False, path=None):
+    """Load libb2f.so (diag=True: libb2f_diag.so; path: an explicit build of the same ABI,
+    for A/B runs in tools/). Raises OSError with a build hint when the file is absent."""
+    path = path or (DIAG_LIB_PATH if diag else LIB_PATH)
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise OSError("%s not found: build it with "
                       "`python -c 'import __graft_entry__ as g; g.build()'` or "
-                      "`make -C zk-odst_amd`" % LIB_PATH)
+                      "`make -C zk-odst_amd`" % path)
     _share_hip_runtime_with_torch()
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, res, args in SIGNATURES:
-        if name in OPTIONAL and not hasattr(lib, name):
-            continue  # diagnostics entry point absent from an older build (A/B runs)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
-def check(ctx, rc):
+def check(ctx, rc, lib=None):
     if rc != OK:
-        msg = load().b2f_last_error(ctx)
+        msg = (lib or load()).b2f_last_error(ctx)
         raise B2FError(rc, msg.decode() if msg else "")

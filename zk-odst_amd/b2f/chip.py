@@ -214,7 +214,9 @@ class MockProver:
         off = self.batch.offsets_host
         inst = int(np.searchsorted(off, row, side="right") - 1)
         what = (SELECTORS[code] if code < 16 else
-                ("lookup" if code == _lib.CODE_LOOKUP else "permutation"))
+                {_lib.CODE_LOOKUP: "lookup", _lib.CODE_COPY: "permutation",
+                 _lib.CODE_FIXED: "fixed column (differs from keygen)",
+                 _lib.CODE_LAYOUT: "row map rejected"}.get(code, "code %d" % code))
         raise VerifyFailure(rep, {"row": int(row), "instance": inst,
                                   "local_row": int(row - off[inst]), "constraint": what})
 

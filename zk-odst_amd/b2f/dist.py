@@ -1,18 +1,26 @@
 """Multi-GPU sharding of a batch of independent compressions.
 
 Instances are independent: each rank fills and evaluates a contiguous shard with no
-data-path collective. The only exchanges are the results: the verdict counters
-(all_reduce) and the 64-byte h' per instance (one all_gather). RCCL has no all_gather_v, so
-unequal shards are padded to the largest shard. Reassembling the whole witness table on every
-rank (gather_trace, one all_gather of the 11 columns) is an optional step for batches that
-fit one GPU (2^18 x 12 rounds x 8 ranks would be 480 GB).
+data-path collective. The exchanges are the results: the verdict counters (all_reduce), the
+64-byte h' per instance (one all_gather) and, when the caller wants the whole witness table on
+every rank, one all-gather per column straight into the final column-major buffers
+(gather_trace). RCCL has no all_gather_v, so unequal shards are gathered in windows padded to
+the widest shard and compacted in place afterwards.
+
+Memory at BASELINE config 4 (2^20 x 12-round compressions over 8 ranks, R = 5,220 rows,
+44 B per row): each rank's shard is 2^17 x 5,220 rows = 30.1 GB; the gathered table is
+[11][8 W] u32 with W = the widest shard's rows, 241 GB; the compaction staging buffer is
+11 x 2^24 x 4 B = 0.74 GB. Total ~272 GB of the 288 GB HBM3E per GPU.
 """
 import numpy as np
 
 from .layout import as_inputs, offsets
 
-REPORT_WORDS = 20  # 16 gates, lookup, copy, first_failure, rows_checked
+# int64 words of b2f_eval_report: 16 gates, lookup, copy, first_failure, rows_checked, fixed
+REPORT_WORDS = 21
+W_LOOKUP, W_COPY, W_FIRST, W_ROWS, W_FIXED = 16, 17, 18, 19, 20
 NONE = np.iinfo(np.int64).max
+STAGE_ROWS = 1 << 24  # compaction staging rows per pass (x 11 columns x 4 B = 0.74 GB)
 
 
 def plan_shards(inputs, world):
@@ -29,28 +37,54 @@ def plan_shards(inputs, world):
     return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
 
 
-def report_to_tensor(rep, torch, device):
-    """Verdict dict -> int64[20] with first_failure = INT64_MAX when clean (for MIN)."""
-    v = list(rep["gate_failures"]) + [rep["lookup_failures"], rep["copy_failures"]]
+def shard_rows(inputs, shards):
+    """(rows of each shard, global row offset of each shard) for plan_shards' ranges."""
+    off = offsets(as_inputs(inputs))
+    rows = [int(off[hi] - off[lo]) for lo, hi in shards]
+    return rows, [int(off[lo]) for lo, _ in shards]
+
+
+def verdict_words(report, row_offset, torch):
+    """A rank's report (int64 [21] device tensor, b2f_eval_report bit patterns) -> int64 [20]:
+    [0:16] gate, 16 lookup, 17 copy, 18 fixed counters, 19 first failure made global
+    ((row + row_offset) << 8 | code; INT64_MAX when clean) -- ready for SUM over [0:19] and MIN
+    over [19]. No host synchronisation."""
+    r = report.view(torch.int64)
+    out = torch.empty(20, dtype=torch.int64, device=r.device)
+    out[:18].copy_(r[:18])
+    out[18] = r[W_FIXED]
+    first = r[W_FIRST]
+    out[19] = torch.where(first == -1, torch.full_like(first, NONE), first + (int(row_offset) << 8))
+    return out
+
+
+def all_reduce_verdict(words, dist, group=None):
+    """Combine verdict_words over the ranks in place (counters summed, first failure min)."""
+    dist.all_reduce(words[:19], op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(words[19:20], op=dist.ReduceOp.MIN, group=group)
+    return words
+
+
+def reduce_report(rep, dist, torch, device, row_offset=0, group=None):
+    """Combine the ranks' verdict dicts: counters and rows summed, first failure = the minimum
+    over ranks of the GLOBAL row key ((rank-local row + the shard's first global row) << 8 |
+    code), so it names the failing row of the whole batch's trace."""
+    v = list(rep["gate_failures"]) + [rep["lookup_failures"], rep["copy_failures"],
+                                      rep.get("fixed_failures", 0)]
     first = rep["first_failure"]
-    v += [NONE if first == 2**64 - 1 else first, rep["rows_checked"]]
-    return torch.tensor(v, dtype=torch.int64, device=device)
-
-
-def reduce_report(rep, dist, torch, device, group=None):
-    """Combine the ranks' verdicts: counters and rows summed, first failure = min.
-    Row numbers stay rank-local (each rank owns its own trace)."""
-    t = report_to_tensor(rep, torch, device)
-    counts = t[:18].clone()
+    first = NONE if first == 2**64 - 1 else first + (int(row_offset) << 8)
+    t = torch.tensor(v + [first, rep["rows_checked"]], dtype=torch.int64, device=device)
+    counts = t[:19].clone()
     dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
-    first = t[18:19].clone()
-    dist.all_reduce(first, op=dist.ReduceOp.MIN, group=group)
-    rows = t[19:20].clone()
+    fmin = t[19:20].clone()
+    dist.all_reduce(fmin, op=dist.ReduceOp.MIN, group=group)
+    rows = t[20:21].clone()
     dist.all_reduce(rows, op=dist.ReduceOp.SUM, group=group)
-    f = int(first.item())
+    f = int(fmin.item())
     return {"gate_failures": [int(x) for x in counts[:16].tolist()],
             "lookup_failures": int(counts[16].item()), "copy_failures": int(counts[17].item()),
-            "first_failure": 2**64 - 1 if f == NONE else f, "rows_checked": int(rows.item())}
+            "first_failure": 2**64 - 1 if f == NONE else f, "rows_checked": int(rows.item()),
+            "fixed_failures": int(counts[18].item())}
 
 
 def gather_h_out(h_local, shards, dist, torch, group=None):
@@ -66,18 +100,63 @@ def gather_h_out(h_local, shards, dist, torch, group=None):
     return torch.cat(parts, dim=0)
 
 
-def gather_trace(adv_local, fixed_local, shard_rows, dist, torch, group=None):
-    """The whole batch's trace on every rank: adv_local [10, rows_r] and fixed_local
-    [rows_r] (int32 bit patterns, rows_r = shard_rows[rank]) -> (advice [10, total],
-    fixed [total]) with the ranks' rows in order, by one all_gather of the 11 columns padded
-    to the largest shard, then one device copy into the column-major layout."""
-    world = len(shard_rows)
-    width = max(shard_rows)
-    rows = adv_local.shape[1]
-    pad = torch.zeros((11, width), dtype=adv_local.dtype, device=adv_local.device)
-    pad[:10, :rows] = adv_local
-    pad[10, :rows] = fixed_local
-    out = torch.empty((world, 11, width), dtype=adv_local.dtype, device=adv_local.device)
-    dist.all_gather_into_tensor(out.view(world * 11, width), pad, group=group)
-    cols = torch.cat([out[r, :, :n] for r, n in enumerate(shard_rows)], dim=1)  # [11, total]
-    return cols[:10].contiguous(), cols[10].contiguous()
+def trace_window(rows_per_rank):
+    """W: the per-rank window every rank's trace buffers are allocated with (the widest
+    shard's rows; a multiple of 4 as every R(rounds) is)."""
+    w = max(rows_per_rank)
+    return w + (-w) % 4
+
+
+def gather_trace_bytes(rows_per_rank):
+    """HBM bytes gather_trace allocates on every rank (result + staging)."""
+    world, w = len(rows_per_rank), trace_window(rows_per_rank)
+    return 11 * 4 * (world * w + min(STAGE_ROWS, w))
+
+
+def gather_trace(adv_local, fixed_local, rows_per_rank, dist, torch, group=None, out=None):
+    """The whole batch's witness table on every rank.
+
+    adv_local [10, W] and fixed_local [W] (int32 bit patterns): this rank's trace, allocated
+    with the common window W = trace_window(rows_per_rank) rows (b2f_fill_dev writes zeros past
+    the shard's used rows). Returns (advice [10, world * W], fixed [world * W]) -- views of one
+    [11, world * W] buffer (`out`, allocated when None) -- holding every rank's used rows back
+    to back from row 0, in rank order, and zeros after: exactly the trace one process would
+    fill for the whole batch with total_rows = world * W.
+
+    One all_gather_into_tensor per column, straight into that column of the result (no
+    pad-and-cat copies; on RCCL the eleven calls are issued in one coalesced group), then an
+    in-place compaction of the padded windows through a bounded staging buffer: rank k's rows
+    move from k * W down to the prefix sum of the shards before it, in increasing row order, so
+    a staged chunk never overwrites rows that still have to move."""
+    world = len(rows_per_rank)
+    w = adv_local.shape[1]
+    if w != trace_window(rows_per_rank) or fixed_local.shape[0] != w:
+        raise ValueError("gather_trace: local trace has %d rows, window is %d"
+                         % (w, trace_window(rows_per_rank)))
+    dev = adv_local.device
+    if out is None:
+        out = torch.empty((11, world * w), dtype=adv_local.dtype, device=dev)
+    cols = [adv_local[c] for c in range(10)] + [fixed_local]
+    coalesce = getattr(dist, "_coalescing_manager", None)
+    if coalesce is not None and dist.get_backend(group) == "nccl":
+        with coalesce(group=group, device=dev):
+            for c in range(11):
+                dist.all_gather_into_tensor(out[c], cols[c], group=group)
+    else:
+        for c in range(11):
+            dist.all_gather_into_tensor(out[c], cols[c], group=group)
+    # compaction of the padded windows (no-op when every shard fills its window)
+    stage = None
+    dst = 0
+    for k, r in enumerate(rows_per_rank):
+        src = k * w
+        if src != dst and r:
+            if stage is None:
+                stage = torch.empty((11, min(STAGE_ROWS, w)), dtype=out.dtype, device=dev)
+            for o in range(0, r, stage.shape[1]):
+                t = min(stage.shape[1], r - o)
+                stage[:, :t].copy_(out[:, src + o: src + o + t])
+                out[:, dst + o: dst + o + t].copy_(stage[:, :t])
+        dst += r
+    out[:, dst:].zero_()
+    return out[:10], out[10]

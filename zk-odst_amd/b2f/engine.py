@@ -22,8 +22,11 @@ def _np_ptr(a):
 class Engine:
     """Wraps b2f_create/b2f_destroy and the fill/eval entry points."""
 
-    def __init__(self, device=0):
-        self.lib = _lib.load()
+    def __init__(self, device=0, diag=False, lib_path=None):
+        """diag=True binds the diagnostics build (libb2f_diag.so); lib_path an explicit build
+        of the same ABI (A/B runs). The default is the product library."""
+        self.lib = _lib.load(diag=diag, path=lib_path)
+        self.diag = bool(diag or lib_path)
         self.device = int(device)
         self.ctx = self.lib.b2f_create(self.device)
         if not self.ctx:
@@ -41,7 +44,7 @@ class Engine:
             pass
 
     def _check(self, rc):
-        _lib.check(self.ctx, rc)
+        _lib.check(self.ctx, rc, self.lib)
 
     # ---------------------------------------------------------------- host-pointer calls
     def fill_host(self, inputs):
@@ -83,6 +86,11 @@ class Engine:
                                                _vp(d_h_out) if d_h_out else None,
                                                _vp(d_report), _vp(stream)))
 
+    def fill_fixed_dev(self, d_off, n, total_rows, d_fixed, stream=0):
+        """Keygen structure: the fixed column from the row map alone (b2f_fill_fixed_dev)."""
+        self._check(self.lib.b2f_fill_fixed_dev(self.ctx, _vp(d_off), int(n), int(total_rows),
+                                                _vp(d_fixed), _vp(stream)))
+
     def debug_inject(self, row=None, col=0, mask=0):
         """Test hook: XOR `mask` into cell (row, col) (col 10 = fixed) as the fused path assigns
         it; row=None turns it off."""
@@ -123,6 +131,16 @@ class Engine:
         cnt = (ctypes.c_uint32 * k)()
         self._check(self.lib.b2f_kernel_times(self.ctx, tot, cnt))
         return {name: (float(tot[i]), int(cnt[i])) for i, name in enumerate(_lib.KERNEL_NAMES)}
+
+
+def copy_constraints(rounds):
+    """The copy constraints of one instance: u32 [count, 4] (dst_row, dst_col, src_row,
+    src_col), instance-relative rows (b2f_copy_constraints)."""
+    lib = _lib.load()
+    n = int(lib.b2f_copy_constraints(int(rounds), None, 0))
+    out = np.zeros((n, 4), dtype=np.uint32)
+    lib.b2f_copy_constraints(int(rounds), _np_ptr(out), n)
+    return out
 
 
 class DeviceBatch:

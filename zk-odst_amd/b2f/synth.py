@@ -11,6 +11,13 @@ from .layout import INPUT_DTYPE
 DEFAULT_SEED = 0x5962be5d
 
 
+def _mix(z):
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
 def _splitmix64(state, n):
     """n splitmix64 outputs starting from `state` (vectorised, wraps mod 2^64)."""
     with np.errstate(over="ignore"):
@@ -39,4 +46,22 @@ def batch(n, rounds=12, seed=DEFAULT_SEED, first=0, rounds_mix=None):
     else:
         mix = np.asarray(rounds_mix, dtype=np.uint32)
         out["rounds"] = mix[(z[:, 27] % np.uint64(len(mix))).astype(np.int64)]
+    return out
+
+
+def rounds_of(n, rounds=12, seed=DEFAULT_SEED, rounds_mix=None):
+    """The `rounds` field of instances [0, n) of the same stream, without generating the
+    other words (shard planning of a large batch needs only the row map): an INPUT_DTYPE
+    array whose other fields are zero."""
+    n = int(n)
+    out = np.zeros(n, dtype=INPUT_DTYPE)
+    if rounds_mix is None:
+        out["rounds"] = rounds
+        return out
+    words_per = 8 + 16 + 2 + 2
+    with np.errstate(over="ignore"):
+        k = (np.arange(n, dtype=np.uint64) + np.uint64(1)) * np.uint64(words_per)
+        z = _mix(np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15))
+    mix = np.asarray(rounds_mix, dtype=np.uint32)
+    out["rounds"] = mix[(z % np.uint64(len(mix))).astype(np.int64)]
     return out

@@ -772,6 +772,25 @@ struct EvalAcc {
               (unsigned long long)((row << 8) | (uint32_t)__builtin_ctz(mask)));
   }
 };
+static_assert(B2F_CODE_FIXED == 18, "the fixed-column counter is word 18 of the accumulator");
+
+// A workgroup's counters into the report: one global atomic per non-zero counter (call after
+// a barrier, every thread of the workgroup).
+__device__ __forceinline__ void flush_report(const EvalAcc& A, b2f_eval_report* rep, int tid) {
+  if (tid < 19) {
+    const uint32_t v = A.c[tid];
+    if (v) {
+      unsigned long long* dst = tid < 16    ? (unsigned long long*)&rep->gate_failures[tid]
+                              : tid == 16   ? (unsigned long long*)&rep->lookup_failures
+                              : tid == 17   ? (unsigned long long*)&rep->copy_failures
+                                            : (unsigned long long*)&rep->fixed_failures;
+      atomicAdd(dst, (unsigned long long)v);
+    }
+  } else if (tid == 19) {
+    const uint64_t fm = *reinterpret_cast<const uint64_t*>(A.c + 20);
+    if (fm != ~0ull) atomicMin((unsigned long long*)&rep->first_failure, (unsigned long long)fm);
+  }
+}
 
 // component j of a quad register (select chain: never an indexed access into a register array)
 __device__ __forceinline__ uint32_t comp(const uint4& v, int j) {
@@ -1262,8 +1281,8 @@ __device__ __forceinline__ void copy_check(EvalAcc& A, uint32_t dv, uint32_t sv,
 }
 
 // canonical cell of limb k of state word w as half-round hr starts (instance-local row)
-__device__ __forceinline__ uint32_t state_src(uint32_t w, uint32_t k, uint32_t spread, uint32_t hr,
-                                              uint32_t& col) {
+__host__ __device__ __forceinline__ uint32_t state_src(uint32_t w, uint32_t k, uint32_t spread,
+                                                       uint32_t hr, uint32_t& col) {
   if (hr == 0) {
     col = spread ? A2 : A1;
     if (w < 8) return 4 * w + k;

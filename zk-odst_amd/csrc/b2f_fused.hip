@@ -398,6 +398,19 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
           A.fail(row0 + j, B2F_CODE_LOOKUP);
       }
     }
+    if ((MODE & FZ_GATES) && gq < total_quads) {
+      // the fixed cells this thread assigned against the keygen structure of its quad
+      uint4 xf = make_uint4(0, 0, 0, 0);
+      if (own_rounds != ~0u) {
+        const QuadInfo d = decode_quad(own_lq, own_rounds);
+        xf = fixed_of_quad(d, d.kind == K_CONST ? IV[d.a & 7u] : 0ull);
+      }
+      if ((fx.x ^ xf.x) | (fx.y ^ xf.y) | (fx.z ^ xf.z) | (fx.w ^ xf.w)) {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (comp(fx, j) != comp(xf, j)) A.fail(row0 + j, B2F_CODE_FIXED);
+      }
+    }
     const GCarve C{F_QSEL, F_A9, F_CT, F_G, F_TS, SHIFT, U_END, true};
     const uint32_t ng = S[FS_NG];
     if (MODE & FZ_GATES) g_pass(T, A, L, S + FS_GT, ng, base0, (uint32_t)tid & 63u, (uint32_t)tid >> 6, C);
@@ -435,18 +448,7 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     for (int k = 0; k < 8; k++) atomicAdd(&clk[8 * (tid >> 6) + k], (unsigned long long)ck[k]);
   }
   // ---- flush the workgroup's counters: one global atomic per non-zero counter
-  if (tid < 18) {
-    const uint32_t v = L[F_ACC + tid];
-    if (v) {
-      unsigned long long* dst = tid < 16 ? (unsigned long long*)&rep->gate_failures[tid]
-                                         : tid == 16 ? (unsigned long long*)&rep->lookup_failures
-                                                     : (unsigned long long*)&rep->copy_failures;
-      atomicAdd(dst, (unsigned long long)v);
-    }
-  } else if (tid == 18) {
-    const uint64_t fm = *reinterpret_cast<const uint64_t*>(L + F_ACC + 20);
-    if (fm != ~0ull) atomicMin((unsigned long long*)&rep->first_failure, (unsigned long long)fm);
-  }
+  flush_report(A, rep, tid);
 }
 
 }  // namespace
@@ -470,6 +472,9 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   inj.j = (uint32_t)(inj_row & 3);
   inj.col = inj_col;
   inj.mask = inj_mask;
+#ifndef B2F_DIAG
+  mode = FZ_FULL;  // the product library launches the full kernel only
+#endif
   if (inj.quad != ~0ull) mode |= FZ_INJECT;
   switch (mode) {
 #define B2F_FUSED(M)                                                                          \
@@ -478,8 +483,10 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                        total_rows, rec, d_adv, d_fixed, reinterpret_cast<const TileInfo*>(tinfo), \
                        n_tiles, band, d_rep, d_status, inj, clk);                             \
     break;
+#ifdef B2F_DIAG
     B2F_FUSED(0) B2F_FUSED(2) B2F_FUSED(3) B2F_FUSED(10) B2F_FUSED(18) B2F_FUSED(8) B2F_FUSED(16)
     B2F_FUSED(34) B2F_FUSED(66) B2F_FUSED(98) B2F_FUSED(FZ_FULL | FZ_CLOCK)
+#endif
     B2F_FUSED(FZ_FULL | FZ_INJECT)
     default: B2F_FUSED(FZ_FULL)
 #undef B2F_FUSED

@@ -67,6 +67,18 @@ __device__ __forceinline__ uint64_t quad_dpp64(uint64_t v) {
 }
 constexpr int QROT1 = 0x39, QROT2 = 0x4E, QROT3 = 0x93;  // lane j <- lane (j + k) % 4
 
+// A device-side error: the per-call word (the call's later kernels exit early on it), the
+// sticky word (only b2f_sync clears it, so a later call cannot erase an earlier error) and,
+// for calls that produce a verdict, the report: a rejected batch never reads clean.
+__device__ __forceinline__ void raise_error(int* status, int* sticky, b2f_eval_report* rep, int code) {
+  atomicOr(status, 1 << code);
+  atomicOr(sticky, 1 << code);
+  if (rep) {
+    rep->rows_checked = 0;
+    atomicMin((unsigned long long*)&rep->first_failure, (unsigned long long)B2F_CODE_LAYOUT);
+  }
+}
+
 __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restrict__ in,
                                                       uint32_t n,
                                                       const uint64_t* __restrict__ off,
@@ -74,7 +86,9 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
                                                       uint64_t states_cap,
                                                       uint64_t* __restrict__ rec,
                                                       uint64_t* __restrict__ h_out,
-                                                      int* __restrict__ status) {
+                                                      int* __restrict__ status,
+                                                      int* __restrict__ sticky,
+                                                      b2f_eval_report* __restrict__ rep) {
   const uint32_t gt = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t i = gt >> 2, c = gt & 3u;  // the quad's four lanes share instance i
   if (i >= n) return;
@@ -82,7 +96,7 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
   uint32_t rounds = x->rounds;
   uint64_t o0 = off[i], o1 = off[i + 1];
   if (rounds > B2F_MAX_ROUNDS) {
-    if (c == 0) atomicOr(status, 1 << B2F_ERR_ROUNDS);
+    if (c == 0) raise_error(status, sticky, rep, B2F_ERR_ROUNDS);
     return;
   }
   uint64_t R = (uint64_t)FIXED_ROWS + (uint64_t)ROUND_ROWS * rounds;
@@ -91,7 +105,7 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
   uint64_t st = bad ? 0 : state_index(o0, i);
   if (!bad && st + 2ull * rounds + 1 > states_cap) bad = true;
   if (bad) {
-    if (c == 0) atomicOr(status, 1 << B2F_ERR_LAYOUT);
+    if (c == 0) raise_error(status, sticky, rep, B2F_ERR_LAYOUT);
     return;
   }
 
@@ -281,8 +295,10 @@ constexpr int GS_GT = 0, GS_QM = MAX_TILE_G * GT_WORDS, GS_NG = GS_QM + BLOCK / 
 constexpr int GSET = GS_NG + 4;
 constexpr int L_GS = L_INFO2 + 24;
 constexpr int L_ACC = L_GS + 2 * GSET;  // 16 gate + lookup + copy counters, first (u64)
-constexpr int LDS_WORDS = L_ACC + 20 + 2;
-static_assert(L_INFO % 4 == 0 && L_IC % 4 == 0 && L_G % 4 == 0 && L_CT % 4 == 0 && L_ACC % 2 == 0,
+constexpr int L_IV = L_ACC + 20 + 2;    // IV, 8 x u64 (CONST rows of the fixed-column check)
+constexpr int LDS_WORDS = L_IV + 16;
+static_assert(L_INFO % 4 == 0 && L_IC % 4 == 0 && L_G % 4 == 0 && L_CT % 4 == 0 && L_ACC % 2 == 0 &&
+                  L_IV % 2 == 0,
               "aligned carve");
 static_assert(LDS_WORDS * 4 * 3 <= 160 * 1024, "three eval workgroups per CU");
 static_assert(GT_WORDS == GT_WORDS_ && L_GS % 4 == 0 && GSET % 4 == 0, "G table entries are two aligned uint4");
@@ -409,6 +425,7 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
                                                     uint64_t n_tiles,
                                                     b2f_eval_report* __restrict__ rep,
                                                     int* __restrict__ status,
+                                                    int* __restrict__ sticky,
                                                     unsigned long long* __restrict__ clk) {
   __shared__ __attribute__((aligned(16))) uint32_t L[LDS_WORDS];
   uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
@@ -424,6 +441,8 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
     L[L_CT + i] = reinterpret_cast<const uint32_t*>(&c_checks)[i];
   if (tid < 40) L[L_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
   if (tid < 16) L[L_XS + tid] = expected_sel((uint32_t)tid);
+  if (tid < 16) L[L_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
+  const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + L_IV);
   const Tile T{L};
   const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + L_SG);  // [10][16]
 
@@ -434,7 +453,7 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
   const uint64_t total_quads = total_rows >> 2;
   const uint64_t used_rows = off[n];
   const bool layout_ok = used_rows <= total_rows && off[0] == 0;  // never read past the trace
-  if (!layout_ok && blockIdx.x == 0 && tid == 0) atomicOr(status, 1 << B2F_ERR_LAYOUT);
+  if (!layout_ok && blockIdx.x == 0 && tid == 0) raise_error(status, sticky, rep, B2F_ERR_LAYOUT);
   const uint64_t G = gridDim.x;
 
   // XCD-aware deal: workgroups are dispatched to the 8 XCDs round-robin (b % 8), so give each
@@ -559,7 +578,10 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
             }
           }
         }
-        if ((MODE & EVAL_COPIES) && !in_g && row0 < used_rows) {
+        // the fixed column against the keygen structure: canonical selectors for round quads
+        // (G table), the decoded init/final block otherwise, zero past the last instance
+        uint4 xf = make_uint4(in_g ? L[L_XS + (pq & 15u)] : 0u, 0u, 0u, 0u);
+        if (!in_g && row0 < used_rows && (MODE & (EVAL_GATES | EVAL_COPIES))) {
           // the quad's instance: scan the tile's cached offsets (a valid layout never needs
           // more; offsets_check_kernel flags any other)
           const uint32_t first = L[L_INFO];
@@ -571,11 +593,23 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
           if (first + i < n && o1 > row0 && o1 <= total_rows && R >= FIXED_ROWS &&
               R <= MAX_INSTANCE_ROWS && ((uint32_t)R - FIXED_ROWS) % ROUND_ROWS == 0) {
             const uint32_t rounds = ((uint32_t)R - FIXED_ROWS) / ROUND_ROWS;
-            const uint64_t ofirst = first < n ? Off[0] : ~0ull;
-            const Src<WSTRIDE> src{L + L_W, L + L_IC, adv, total_rows, tile0 - HIST, ofirst};
-            const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
-            copies_edge(A, dq[0], dq[1], dq[2], src, o, rounds, (uint32_t)((row0 - o) >> 2));
+            const uint32_t lq = (uint32_t)((row0 - o) >> 2);
+            if (MODE & EVAL_GATES) {
+              const QuadInfo d = decode_quad(lq, rounds);
+              xf = fixed_of_quad(d, d.kind == K_CONST ? IV[d.a & 7u] : 0ull);
+            }
+            if (MODE & EVAL_COPIES) {
+              const uint64_t ofirst = first < n ? Off[0] : ~0ull;
+              const Src<WSTRIDE> src{L + L_W, L + L_IC, adv, total_rows, tile0 - HIST, ofirst};
+              const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
+              copies_edge(A, dq[0], dq[1], dq[2], src, o, rounds, lq);
+            }
           }
+        }
+        if ((MODE & EVAL_GATES) && ((curfx.x ^ xf.x) | (curfx.y ^ xf.y) | (curfx.z ^ xf.z) | (curfx.w ^ xf.w))) {
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (comp(curfx, j) != comp(xf, j)) A.fail(row0 + j, B2F_CODE_FIXED);
         }
       }
     }
@@ -589,31 +623,21 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
   }
   // ---- flush the workgroup's counters: one global atomic per non-zero counter
   __syncthreads();
-  if (tid < 18) {
-    uint32_t v = L[L_ACC + tid];
-    if (v) {
-      unsigned long long* dst = tid < 16 ? (unsigned long long*)&rep->gate_failures[tid]
-                                         : tid == 16 ? (unsigned long long*)&rep->lookup_failures
-                                                     : (unsigned long long*)&rep->copy_failures;
-      atomicAdd(dst, (unsigned long long)v);
-    }
-  } else if (tid == 18) {
-    uint64_t fm = *reinterpret_cast<const uint64_t*>(L + L_ACC + 20);
-    if (fm != ~0ull) atomicMin((unsigned long long*)&rep->first_failure, (unsigned long long)fm);
-  }
+  flush_report(A, rep, tid);
 }
 
 // Device-side layout validation for b2f_eval_dev: every instance's rows must be R(rounds) for
 // some rounds and lie inside the trace. The eval kernel relies on it (an invalid layout is an
 // error whatever the counters say; it only has to stay in bounds).
 __global__ void offsets_check_kernel(const uint64_t* __restrict__ off, uint32_t n,
-                                     uint64_t total_rows, int* __restrict__ status) {
+                                     uint64_t total_rows, int* __restrict__ status,
+                                     int* __restrict__ sticky, b2f_eval_report* __restrict__ rep) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t o = off[i], o1 = off[i + 1], R = o1 - o;
   const bool bad = o1 < o || o1 > total_rows || (i == 0 && o != 0) || R < FIXED_ROWS ||
                    R > MAX_INSTANCE_ROWS || ((uint32_t)R - FIXED_ROWS) % ROUND_ROWS != 0;
-  if (bad) atomicOr(status, 1 << B2F_ERR_LAYOUT);
+  if (bad) raise_error(status, sticky, rep, B2F_ERR_LAYOUT);
 }
 
 // Multi-block chaining (Blake2f::update/finalize, blake2f.rs:101-168): the inputs of one block
@@ -637,12 +661,44 @@ __global__ void chain_inputs_kernel(const uint64_t* __restrict__ h_prev,
   out[i] = x;
 }
 
+// Keygen structure of the fixed column (b2f_fill_fixed_dev): the selector masks and IV
+// constants every row carries by its position in the row map alone (halo2 keygen with
+// Value::unknown() witnesses). Thread per quad, one 1024-row tile per
+// workgroup, the tile's instance context from TileInfo (scalar loads).
+__global__ void __launch_bounds__(BLOCK) fixed_kernel(const uint64_t* __restrict__ off, uint32_t n,
+                                                     uint64_t total_rows,
+                                                     const TileInfo* __restrict__ tinfo,
+                                                     uint32_t* __restrict__ fixed,
+                                                     const int* __restrict__ status) {
+  if (*status) return;  // offsets_check_kernel rejected the row map: write nothing
+  const uint64_t t = blockIdx.x;
+  const uint64_t gq = t * BLOCK + threadIdx.x;
+  if (gq >= (total_rows >> 2)) return;
+  const uint64_t row = 4 * gq;
+  const TileInfo ti = tinfo[t];
+  uint4 f = make_uint4(0, 0, 0, 0);
+  if (row < off[n] && ti.first < n) {
+    uint64_t o = ti.off[0], o1 = ti.off[1];
+    uint32_t i = 0;
+#pragma unroll
+    for (int k = 1; k + 1 < NOFF; k++)
+      if (ti.off[k] <= row) { o = ti.off[k]; o1 = ti.off[k + 1]; i = (uint32_t)k; }
+    if (row >= o && row < o1 && ti.first + i < n) {
+      const uint32_t rounds = ((uint32_t)(o1 - o) - FIXED_ROWS) / ROUND_ROWS;
+      const QuadInfo d = decode_quad((uint32_t)((row - o) >> 2), rounds);
+      f = fixed_of_quad(d, d.kind == K_CONST ? c_iv[d.a & 7u] : 0ull);
+    }
+  }
+  __builtin_nontemporal_store(u32x4{f.x, f.y, f.z, f.w}, reinterpret_cast<u32x4*>(fixed + row));
+}
+
 __global__ void report_init_kernel(b2f_eval_report* rep, uint64_t total_rows) {
   for (int s = 0; s < B2F_NUM_GATES; s++) rep->gate_failures[s] = 0;
   rep->lookup_failures = 0;
   rep->copy_failures = 0;
   rep->first_failure = ~0ull;
   rep->rows_checked = total_rows;
+  rep->fixed_failures = 0;
 }
 
 }  // namespace
@@ -652,7 +708,7 @@ __global__ void report_init_kernel(b2f_eval_report* rep, uint64_t total_rows) {
 struct b2f_ctx {
   int device;
   char err[512];
-  int* d_status;       // [0] fill, [1] eval
+  int* d_status;       // [0] fill call, [1] eval call, [2] sticky (cleared by b2f_sync only)
   uint64_t* d_rec;     // half-round states
   uint64_t rec_cap;    // in states (16 x u64 each)
   TileInfo* d_tiles;   // per-tile instance context
@@ -705,13 +761,15 @@ void timed_end(b2f_ctx* ctx, int i, hipStream_t s) {
   if (i >= 0) (void)hipEventRecord(ctx->pool[2 * i + 1], s);
 }
 
-// Diagnostic kernel variants for ablation runs (B2F_DIAG_FILL / B2F_DIAG_EVAL); unset in
-// every product run, where the full kernels launch.
+// Diagnostic kernel variants for ablation runs (B2F_DIAG_FILL / B2F_DIAG_EVAL /
+// B2F_DIAG_FUSED / B2F_FILL_WGS / B2F_BAND) exist only in the diagnostics library
+// (libb2f_diag.so, built with -DB2F_DIAG). The product library (libb2f.so) reads no environment
+// and always launches the full kernels.
+#ifdef B2F_DIAG
 int diag_mode(const char* var, int full) {
   const char* v = getenv(var);
   return v ? atoi(v) : full;
 }
-
 // B2F_DIAG_FUSED: only the product variant (27) and the diagnostic ones that skip every check
 // (0, 2, 3, 10, 18, 8, 16, 34, 66, 98) are accepted; anything else runs the product kernel.
 int fused_mode() {
@@ -720,6 +778,10 @@ int fused_mode() {
                     ((m & ~(1 | 2 | 8 | 16 | 32 | 64)) == 0 && ((m & (32 | 64)) == 0 || (m & 25) == 0));
   return safe ? m : 27;
 }
+#else
+constexpr int diag_mode(const char*, int full) { return full; }
+constexpr int fused_mode() { return 27; }
+#endif
 
 uint64_t layout_rows(uint32_t rounds) {
   if (rounds > B2F_MAX_ROUNDS) return 0;
@@ -751,11 +813,71 @@ int launch_tile_index(b2f_ctx* ctx, const uint64_t* d_offsets, size_t n, uint64_
   return B2F_OK;
 }
 
+// The copy constraints of one instance (LAYOUT.md §4/§5), in synthesis order: the init XOR
+// operands, then per round and G the operand cells of its eight blocks (the device check
+// tables' DescTable, make_desc), then the final XOR3 operands. Each is (dst_row, dst_col,
+// src_row, src_col), rows relative to the instance. Host code, no device work.
+uint64_t copy_constraints(uint32_t rounds, uint32_t* out4, uint64_t cap) {
+  uint64_t cnt = 0;
+  auto put = [&](uint32_t dr, uint32_t dc, uint32_t sr, uint32_t sc) {
+    if (out4 && cnt < cap) {
+      uint32_t* q = out4 + 4 * cnt;
+      q[0] = dr; q[1] = dc; q[2] = sr; q[3] = sc;
+    }
+    cnt++;
+  };
+  // v12 = IV4 ^ t0, v13 = IV5 ^ t1, v14 = IV6 ^ fmask (XOR blocks at 140 + 8a)
+  for (uint32_t a = 0; a < 3; a++)
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t dr = 140 + 8 * a + 2 * k;
+      put(dr, A3, 108 + 4 * (4 + a) + k, A2);
+      put(dr, A4, (a < 2 ? 96 + 4 * a : 104) + k, A2);
+    }
+  constexpr DescTable D = make_desc();
+  constexpr SigmaPairs SP = make_sigma_pairs();
+  for (uint32_t r = 0; r < rounds; r++)
+    for (uint32_t g = 0; g < 8; g++) {
+      const uint32_t gb = INIT_ROWS + ROUND_ROWS * r + G_ROWS * g;
+      const uint32_t hr = 2 * r + (g >= 4 ? 1u : 0u);
+      for (uint32_t p = 0; p < G_QUADS; p++)
+        for (uint32_t j = 0; j < 4; j++)
+          for (uint32_t c = 0; c < 3; c++) {
+            const uint32_t d = D.d[p][j][c], kind = d & 3u;
+            if (!kind) continue;
+            const uint32_t dr = gb + 4 * p + j, dc = A3 + c;
+            if (kind == 1) {
+              put(dr, dc, gb + ((d >> 2) & 63u), (d >> 8) & 15u);
+            } else if (kind == 2) {
+              uint32_t col = 0;
+              const uint32_t w = kGidx[g][(d >> 2) & 3u];
+              const uint32_t sr = state_src(w, (d >> 4) & 3u, (d >> 6) & 1u, hr, col);
+              put(dr, dc, sr, col);
+            } else {
+              const uint32_t pair = SP.v[r % 10][g];
+              const uint32_t mw = ((d >> 2) & 1u) ? pair >> 8 : pair & 0xffu;
+              put(dr, dc, 32 + 4 * mw + ((d >> 4) & 3u), A1);
+            }
+          }
+    }
+  // h'_i = h_i ^ v_i ^ v_{i+8} (XOR3 blocks at 164 + 416 rounds + 8i)
+  for (uint32_t i = 0; i < 8; i++)
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t dr = INIT_ROWS + ROUND_ROWS * rounds + 8 * i + 2 * k;
+      uint32_t cv = 0, cu = 0;
+      const uint32_t vs = state_src(i, k, 1, 2 * rounds, cv);
+      const uint32_t us = state_src(i + 8, k, 1, 2 * rounds, cu);
+      put(dr, A3, 4 * i + k, A2);
+      put(dr, A4, vs, cv);
+      put(dr, A5, us, cu);
+    }
+  return cnt;
+}
+
 }  // namespace
 
 extern "C" {
 
-B2F_API int b2f_version(void) { return 1; }
+B2F_API int b2f_version(void) { return 2; }  // 2: fixed_failures, sticky errors, keygen calls
 
 B2F_API uint64_t b2f_layout_rows(uint32_t rounds) { return layout_rows(rounds); }
 
@@ -808,6 +930,7 @@ B2F_API b2f_ctx* b2f_create(int device) {
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete ctx; return nullptr; }
   ctx->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   if (hipMalloc(&ctx->d_status, 4 * sizeof(int)) != hipSuccess) { delete ctx; return nullptr; }
+  // the sticky word must read 0 before the first call: a blocking memset on the null stream
   if (hipMemset(ctx->d_status, 0, 4 * sizeof(int)) != hipSuccess) { delete ctx; return nullptr; }
   return ctx;
 }
@@ -854,7 +977,7 @@ namespace {
 // b2f_fill_eval_dev.
 int fill_prologue(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const uint64_t* d_offsets,
                   uint64_t total_rows, uint32_t* d_advice, uint32_t* d_fixed, uint64_t* d_h_out,
-                  hipStream_t s) {
+                  b2f_eval_report* d_report, hipStream_t s) {
   if (!d_in || !d_offsets || !d_advice || !d_fixed || n == 0)
     return set_err(ctx, B2F_ERR_ARG, "fill: null buffer or empty batch");
   if (n > 0xffffffffull) return set_err(ctx, B2F_ERR_ARG, "fill: more than 2^32 instances");
@@ -876,10 +999,15 @@ int fill_prologue(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const uint64_t*
     ctx->rec_cap = states;
   }
   HIPCHK(ctx, hipMemsetAsync(ctx->d_status, 0, sizeof(int), s));
+  if (d_report) {  // before the record kernel, which marks the report of a rejected batch
+    hipLaunchKernelGGL(report_init_kernel, dim3(1), dim3(1), 0, s, d_report, total_rows);
+    HIPCHK(ctx, hipGetLastError());
+  }
   uint32_t nn = (uint32_t)n;
   int tk = timed_begin(ctx, B2F_KERNEL_RECORD, s);
   hipLaunchKernelGGL(record_kernel, dim3((uint32_t)((4ull * nn + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, d_in, nn,
-                     d_offsets, total_rows, ctx->rec_cap, ctx->d_rec, d_h_out, ctx->d_status);
+                     d_offsets, total_rows, ctx->rec_cap, ctx->d_rec, d_h_out, ctx->d_status,
+                     ctx->d_status + 2, d_report);
   HIPCHK(ctx, hipGetLastError());
   timed_end(ctx, tk, s);
   return B2F_OK;
@@ -893,7 +1021,7 @@ B2F_API int b2f_fill_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const ui
                          uint64_t* d_h_out, void* stream) {
   if (!ctx) return B2F_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  int rc = fill_prologue(ctx, d_in, n, d_offsets, total_rows, d_advice, d_fixed, d_h_out, s);
+  int rc = fill_prologue(ctx, d_in, n, d_offsets, total_rows, d_advice, d_fixed, d_h_out, nullptr, s);
   if (rc) return rc;
   const uint32_t nn = (uint32_t)n;
   uint64_t nt = n_tiles_of(total_rows);
@@ -908,7 +1036,10 @@ B2F_API int b2f_fill_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const ui
                        total_rows, ctx->d_rec, d_advice, d_fixed, ctx->d_status, ctx->d_tiles, \
                        nt);                                                                    \
     break;
-    B2F_FILL(0) B2F_FILL(1) B2F_FILL(2) default: B2F_FILL(3)
+#ifdef B2F_DIAG
+    B2F_FILL(0) B2F_FILL(1) B2F_FILL(2)
+#endif
+    default: B2F_FILL(3)
 #undef B2F_FILL
   }
   HIPCHK(ctx, hipGetLastError());
@@ -923,10 +1054,8 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
   if (!ctx) return B2F_ERR_ARG;
   if (!d_report) return set_err(ctx, B2F_ERR_ARG, "fill_eval: null report");
   hipStream_t s = (hipStream_t)stream;
-  int rc = fill_prologue(ctx, d_in, n, d_offsets, total_rows, d_advice, d_fixed, d_h_out, s);
+  int rc = fill_prologue(ctx, d_in, n, d_offsets, total_rows, d_advice, d_fixed, d_h_out, d_report, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(report_init_kernel, dim3(1), dim3(1), 0, s, d_report, total_rows);
-  HIPCHK(ctx, hipGetLastError());
   const uint64_t nt = n_tiles_of(total_rows);
   rc = launch_tile_index(ctx, d_offsets, n, nt, s, 16);
   if (rc) return rc;
@@ -982,7 +1111,8 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
   hipLaunchKernelGGL(report_init_kernel, dim3(1), dim3(1), 0, s, d_report, total_rows);
   HIPCHK(ctx, hipGetLastError());
   hipLaunchKernelGGL(offsets_check_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
-                     d_offsets, (uint32_t)n, total_rows, ctx->d_status + 1);
+                     d_offsets, (uint32_t)n, total_rows, ctx->d_status + 1, ctx->d_status + 2,
+                     d_report);
   HIPCHK(ctx, hipGetLastError());
   uint64_t nt = n_tiles_of(total_rows);
   int rc = launch_tile_index(ctx, d_offsets, n, nt, s);
@@ -999,10 +1129,12 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
   case M:                                                                                       \
     hipLaunchKernelGGL(eval_kernel<M>, dim3(wgs), dim3(BLOCK), 0, s, d_advice, d_fixed,         \
                        d_offsets, (uint32_t)n, total_rows, ctx->d_tiles, nt, d_report,          \
-                       ctx->d_status + 1, ctx->d_clock);                                        \
+                       ctx->d_status + 1, ctx->d_status + 2, ctx->d_clock);                     \
     break;
+#ifdef B2F_DIAG
     B2F_EVAL(1) B2F_EVAL(2) B2F_EVAL(3) B2F_EVAL(4) B2F_EVAL(5) B2F_EVAL(6) B2F_EVAL(8)
     B2F_EVAL(EVAL_FULL | EVAL_CLOCK)
+#endif
     default: B2F_EVAL(7)
 #undef B2F_EVAL
   }
@@ -1101,14 +1233,44 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
   return B2F_OK;
 }
 
+B2F_API int b2f_fill_fixed_dev(b2f_ctx* ctx, const uint64_t* d_offsets, size_t n,
+                               uint64_t total_rows, uint32_t* d_fixed, void* stream) {
+  if (!ctx) return B2F_ERR_ARG;
+  if (!d_offsets || !d_fixed || n == 0) return set_err(ctx, B2F_ERR_ARG, "fill_fixed: null buffer or empty batch");
+  if (n > 0xffffffffull) return set_err(ctx, B2F_ERR_ARG, "fill_fixed: more than 2^32 instances");
+  if (total_rows % 4) return set_err(ctx, B2F_ERR_ARG, "fill_fixed: total_rows %% 4 != 0");
+  if ((uintptr_t)d_fixed & 15) return set_err(ctx, B2F_ERR_ARG, "fill_fixed: d_fixed must be 16-byte aligned");
+  if (total_rows < (uint64_t)FIXED_ROWS * n)
+    return set_err(ctx, B2F_ERR_ROWS, "fill_fixed: %llu rows cannot hold %zu instances",
+                   (unsigned long long)total_rows, n);
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipMemsetAsync(ctx->d_status, 0, sizeof(int), s));
+  hipLaunchKernelGGL(offsets_check_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                     d_offsets, (uint32_t)n, total_rows, ctx->d_status, ctx->d_status + 2,
+                     (b2f_eval_report*)nullptr);
+  HIPCHK(ctx, hipGetLastError());
+  const uint64_t nt = n_tiles_of(total_rows);
+  int rc = launch_tile_index(ctx, d_offsets, n, nt, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(fixed_kernel, dim3((uint32_t)nt), dim3(BLOCK), 0, s, d_offsets, (uint32_t)n,
+                     total_rows, ctx->d_tiles, d_fixed, ctx->d_status);
+  HIPCHK(ctx, hipGetLastError());
+  return B2F_OK;
+}
+
+B2F_API uint64_t b2f_copy_constraints(uint32_t rounds, uint32_t* out4, uint64_t cap) {
+  if (rounds > B2F_MAX_ROUNDS) return 0;
+  return copy_constraints(rounds, out4, cap);
+}
+
 B2F_API int b2f_sync(b2f_ctx* ctx, void* stream) {
   if (!ctx) return B2F_ERR_ARG;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
-  int st[2] = {0, 0};
-  HIPCHK(ctx, hipMemcpy(st, ctx->d_status, sizeof st, hipMemcpyDeviceToHost));
-  HIPCHK(ctx, hipMemset(ctx->d_status, 0, sizeof st));
-  int bits = st[0] | st[1];
+  int bits = 0;  // the sticky word: every error raised since the previous b2f_sync
+  HIPCHK(ctx, hipMemcpy(&bits, ctx->d_status + 2, sizeof bits, hipMemcpyDeviceToHost));
+  HIPCHK(ctx, hipMemset(ctx->d_status + 2, 0, sizeof bits));
   if (bits & (1 << B2F_ERR_ROUNDS)) return set_err(ctx, B2F_ERR_ROUNDS, "rounds > %u", B2F_MAX_ROUNDS);
   if (bits & (1 << B2F_ERR_LAYOUT))
     return set_err(ctx, B2F_ERR_LAYOUT, "row offsets are not the LAYOUT v1 prefix sums");

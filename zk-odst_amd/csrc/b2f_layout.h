@@ -141,4 +141,27 @@ __device__ __forceinline__ QuadInfo decode_quad(uint32_t lq, uint32_t rounds) {
   return d;
 }
 
+// The keygen structure of the fixed column (LAYOUT.md §4/§5): the four fixed cells of a
+// decoded quad, from the row map alone. Selectors sit on a block's first row; CONST blocks
+// carry `s_const | IV_k << 16` on each of their four rows. `ivw` = IV[d.a] (read only for
+// CONST quads). halo2 fixes these at keygen (keygen_vk/keygen_pk,
+// benchmarking/src/blake2f_circuit_bench.rs:54-55), so a witness never changes them.
+__device__ __forceinline__ uint4 fixed_of_quad(const QuadInfo& d, uint64_t ivw) {
+  uint4 f = make_uint4(0, 0, 0, 0);
+  switch (d.kind) {
+    case K_CONST: {
+      const uint32_t s = 1u << S_CONST;
+      f = make_uint4(s | ((uint32_t)(ivw & 0xffffu) << 16), s | ((uint32_t)((ivw >> 16) & 0xffffu) << 16),
+                     s | ((uint32_t)((ivw >> 32) & 0xffffu) << 16), s | ((uint32_t)(ivw >> 48) << 16));
+      break;
+    }
+    case K_XOR24: if (d.q == 0) f.x = (1u << S_B1) | (1u << S_EFGH); break;
+    case K_XOR63: if (d.q == 0) f.x = (1u << S_B2) | (1u << S_IJKL); break;
+    case K_XOR3: if (d.q == 0) f.x = (1u << S_XOR3) | (1u << S_DIGEST); break;
+    case K_PAD: break;
+    default: if (d.q == 0) f.x = 1u << d.sel; break;  // INW, FMASK, XOR, ADD3, ADD2
+  }
+  return f;
+}
+
 }  // namespace b2f
