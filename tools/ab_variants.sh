@@ -3,5 +3,5 @@
 set -o pipefail
 ARGS=${AB_ARGS:---reps 3 --fill-modes 3 --eval-modes 7 --bands 16 --fused-modes 27}
 for v in "$@"; do
-  B2F_LIB=$GRAFT_REPO_ROOT/zk-odst_amd/variants/libb2f_$v.so timeout -k 10 150 python tools/ablate.py $ARGS > gpurun_out/ab_$v.txt 2>&1 || exit 1
+  timeout -k 10 150 python tools/ablate.py --lib $GRAFT_REPO_ROOT/zk-odst_amd/variants/libb2f_$v.so $ARGS > gpurun_out/ab_$v.txt 2>&1 || exit 1
 done

@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--eval-modes", default="7,8,2,4")
     ap.add_argument("--bands", default="", help="fused fill+eval band sizes to time (B2F_BAND)")
     ap.add_argument("--fused-modes", default="", help="fused kernel variants (B2F_DIAG_FUSED)")
+    ap.add_argument("--lib", default=None, help="an explicit build of the ABI (A/B runs); "
+                    "default: the diagnostics library libb2f_diag.so")
     args = ap.parse_args()
     import torch
 
@@ -25,7 +27,7 @@ def main():
 
     x = synth.batch(args.batch, rounds=args.rounds)
     batch = b2f.DeviceBatch(x)
-    eng = b2f.Engine(0)
+    eng = b2f.Engine(0, diag=True, lib_path=args.lib)
     s = torch.cuda.current_stream().cuda_stream
     nbytes = batch.used_rows * 44
     batch.fill(eng, s)

@@ -23,7 +23,7 @@ def main():
 
     x = synth.batch(args.batch, rounds=12)
     batch = b2f.DeviceBatch(x)
-    eng = b2f.Engine(0)
+    eng = b2f.Engine(0, diag=True)  # EVAL_CLOCK / FZ_CLOCK variants: diagnostics build only
     s = torch.cuda.current_stream().cuda_stream
     batch.fill(eng, s)
     run = batch.fill_evaluate if args.fused else batch.evaluate

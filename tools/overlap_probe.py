@@ -18,7 +18,10 @@ def main():
 
     n = int(os.environ.get("N", 1 << 17))
     reps = 6
-    eng = b2f.Engine(0)
+    # one context per concurrent stream (a context's scratch is per call, include/b2f.h);
+    # B2F_FILL_WGS is read only by the diagnostics build
+    eng = b2f.Engine(0, diag=True)
+    eng2 = b2f.Engine(0, diag=True)
     xa = synth.batch(n, rounds=12, seed=1)
     xb = synth.batch(n, rounds=12, seed=2)
     A, B = b2f.DeviceBatch(xa), b2f.DeviceBatch(xb)
@@ -45,7 +48,7 @@ def main():
     for k in range(reps):
         cur, nxt = (A, B) if k % 2 == 0 else (B, A)
         s2.wait_event(ev[k])                 # cur filled
-        cur.evaluate(eng, s2.cuda_stream)
+        cur.evaluate(eng2, s2.cuda_stream)
         done = torch.cuda.Event()
         done.record(s2)
         nxt.fill(eng, s1.cuda_stream)        # overlaps the eval above

@@ -1,0 +1,113 @@
+// store_probe.hip -- diagnostics: HBM store rate of the trace write patterns a fill kernel can
+// use, on the real 2^18 x 12-round trace shape (11 u32 columns, 5,220 rows per instance).
+//   tile  : 1024-row tiles dealt round-robin to persistent workgroups (the fill kernel's order)
+//   wave  : every wave owns whole instances (dynamic: a global counter), writing an instance's
+//           rows in steps of STEP quads (52 = one half-round of 4 G's) from row 0 to its end
+//   wavesI: the same with a static interleave (wave w takes instances w, w + W, ...)
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/store_probe tools/store_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define CHK(x)                                                                  \
+  do {                                                                          \
+    hipError_t e = (x);                                                         \
+    if (e != hipSuccess) {                                                      \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));                    \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+__global__ void __launch_bounds__(256) tile_store(uint32_t* adv, uint64_t total_rows, uint64_t n_tiles) {
+  const uint64_t total_quads = total_rows >> 2;
+  for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    const uint64_t gq = t * 256 + threadIdx.x;
+    if (gq >= total_quads) continue;
+    const u32x4 v = {(uint32_t)gq, 1u, 2u, 3u};
+#pragma unroll
+    for (int c = 0; c < 11; c++)
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(adv + (uint64_t)c * total_rows + 4 * gq));
+  }
+}
+
+template <int STEP, bool DYN>
+__global__ void __launch_bounds__(256) wave_store(uint32_t* adv, uint64_t total_rows, uint32_t n,
+                                                  uint32_t rows_per, unsigned* counter) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  const uint32_t quads = rows_per / 4;
+  for (uint32_t k = 0;; k++) {
+    uint32_t i;
+    if (DYN) {
+      uint32_t v = 0;
+      if (lane == 0) v = atomicAdd(counter, 1u);
+      i = __builtin_amdgcn_readfirstlane(v);
+    } else {
+      i = wid + k * nw;
+    }
+    if (i >= n) break;
+    const uint64_t o = (uint64_t)i * rows_per;
+    for (uint32_t q0 = 0; q0 < quads; q0 += STEP) {
+      const uint32_t q = q0 + lane;
+      if (lane < STEP && q < quads) {
+        const u32x4 v = {q, i, 2u, 3u};
+#pragma unroll
+        for (int c = 0; c < 11; c++)
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(adv + (uint64_t)c * total_rows + o + 4 * q));
+      }
+    }
+  }
+}
+
+int main(int argc, char** argv) {
+  const uint32_t n = argc > 1 ? atoi(argv[1]) : (1u << 18);
+  const uint32_t rows_per = 228 + 416 * 12;
+  const uint64_t total = (uint64_t)n * rows_per;
+  uint32_t* adv;
+  unsigned* ctr;
+  CHK(hipMalloc(&adv, total * 11 * 4));
+  CHK(hipMalloc(&ctr, 4));
+  hipDeviceProp_t prop;
+  CHK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  hipEvent_t a, b;
+  CHK(hipEventCreate(&a));
+  CHK(hipEventCreate(&b));
+  const double bytes = (double)total * 44;
+  auto run = [&](const char* name, auto launch) {
+    float best = 1e30f;
+    for (int rep = 0; rep < 4; rep++) {
+      CHK(hipMemset(ctr, 0, 4));
+      CHK(hipEventRecord(a));
+      launch();
+      CHK(hipEventRecord(b));
+      CHK(hipEventSynchronize(b));
+      float ms;
+      CHK(hipEventElapsedTime(&ms, a, b));
+      if (rep && ms < best) best = ms;
+    }
+    printf("{\"pattern\": \"%s\", \"ms\": %.3f, \"TBs\": %.3f}\n", name, best, bytes / best / 1e9);
+    fflush(stdout);
+  };
+  const uint64_t nt = (total + 1023) / 1024;
+  for (int w : {8, 4}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "tile_rr_%dwg", w);
+    run(nm, [&] { hipLaunchKernelGGL(tile_store, dim3(cus * w), dim3(256), 0, 0, adv, total, nt); });
+  }
+  for (int w : {4, 2}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "wave_dyn_step52_%dwg", w);
+    run(nm, [&] { hipLaunchKernelGGL((wave_store<52, true>), dim3(cus * w), dim3(256), 0, 0, adv, total, n, rows_per, ctr); });
+    snprintf(nm, sizeof nm, "wave_static_step52_%dwg", w);
+    run(nm, [&] { hipLaunchKernelGGL((wave_store<52, false>), dim3(cus * w), dim3(256), 0, 0, adv, total, n, rows_per, ctr); });
+    snprintf(nm, sizeof nm, "wave_dyn_step64_%dwg", w);
+    run(nm, [&] { hipLaunchKernelGGL((wave_store<64, true>), dim3(cus * w), dim3(256), 0, 0, adv, total, n, rows_per, ctr); });
+  }
+  CHK(hipFree(adv));
+  return 0;
+}
