@@ -108,14 +108,14 @@ def test_missing_library_fails_loudly():
 
 
 def test_product_library_reads_no_environment():
-    """the diagnostic kernel variants (selected by B2F_DIAG_* / B2F_BAND /
+    """the diagnostic kernel variants (selected by B2F_DIAG_* /
     B2F_FILL_WGS) live only in libb2f_diag.so; libb2f.so does not even contain the names, so
     no environment can swap a product kernel for a diagnostic one."""
     from b2f import _lib
 
     prod = open(_lib.LIB_PATH, "rb").read()
     diag = open(_lib.DIAG_LIB_PATH, "rb").read()
-    for var in (b"B2F_DIAG_EVAL", b"B2F_DIAG_FILL", b"B2F_DIAG_FUSED", b"B2F_BAND", b"B2F_FILL_WGS"):
+    for var in (b"B2F_DIAG_EVAL", b"B2F_DIAG_FILL", b"B2F_DIAG_FUSED", b"B2F_FILL_WGS"):
         assert var not in prod, var
         assert var in diag, var
     lib = _lib.load(diag=True)

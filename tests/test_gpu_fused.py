@@ -4,10 +4,11 @@ The fused kernel must produce exactly what b2f_fill_dev followed by b2f_eval_dev
 the trace, h' and the MockProver verdict -- and therefore what the CPU oracle produces. Fault
 injection (b2f_debug_inject) flips one cell as the fused kernel assigns it; the trace it writes
 then differs from the clean one in exactly that cell, and its verdict must equal the verdict
-of b2f_eval_dev and of the oracle on that written trace. Faults are placed on the places the
-fused kernel's tiling makes special: the 16 rows either side of every tile boundary (carried
-quads, deferred gates), band starts (recomputed history) and the last rows of the trace (zero
-halo). Every test here needs an MI355X (`-m gpu`)."""
+of b2f_eval_dev and of the oracle on that written trace. Faults are placed where the fused
+kernel's wave tiles make things special: both sides of every init / half-round / final tile
+boundary (copy sources recomputed from the producer side, gates whose rows run past the tile
+and are deferred to the written trace), the zero tail and the last rows of the trace. Every
+test here needs an MI355X (`-m gpu`)."""
 import os
 
 import numpy as np
@@ -18,11 +19,6 @@ from conftest import random_inputs
 pytestmark = pytest.mark.gpu
 
 NONE = 2**64 - 1
-PRODUCT_BAND = 16  # the band libb2f.so launches; other bands run on the diagnostics build
-
-
-def _pick(engine, diag_engine, band):
-    return engine if band == PRODUCT_BAND else diag_engine
 
 
 def _as_oracle(x, orc):
@@ -35,33 +31,29 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-def _fused(engine, x, band, total_rows=None, inject=None):
-    """One b2f_fill_eval_dev call on a fresh DeviceBatch (buffers poisoned first). A band other
-    than the product's needs the diagnostics engine (B2F_BAND is read only there)."""
+def _fused(engine, x, total_rows=None, inject=None):
+    """One b2f_fill_eval_dev call on a fresh DeviceBatch (buffers poisoned first)."""
     import b2f
 
-    assert band == PRODUCT_BAND or engine.diag, "band %d needs the diagnostics build" % band
-    os.environ["B2F_BAND"] = str(band)
+    batch = b2f.DeviceBatch(x, total_rows=total_rows)
+    batch.advice.fill_(-1)
+    batch.fixed.fill_(-1)
     try:
-        batch = b2f.DeviceBatch(x, total_rows=total_rows)
-        batch.advice.fill_(-1)
-        batch.fixed.fill_(-1)
         if inject is not None:
             engine.debug_inject(*inject)
         batch.fill_evaluate(engine)
         engine.sync(_stream())
     finally:
         engine.debug_inject(None)
-        os.environ.pop("B2F_BAND", None)
     return batch
 
 
-@pytest.mark.parametrize("band", [1, 2, 3, 16])
 @pytest.mark.parametrize("rounds_choices,n,seed", [((12,), 23, 31), ((0, 1, 4, 12, 13), 71, 32),
-                                                   ((1,), 200, 33)])
-def test_fused_equals_oracle(engine, diag_engine, orc, band, rounds_choices, n, seed):
+                                                   ((1,), 200, 33), ((0,), 9, 35),
+                                                   ((2, 3), 1000, 36)])
+def test_fused_equals_oracle(engine, orc, rounds_choices, n, seed):
     x = random_inputs(n, rounds_choices, seed)
-    batch = _fused(_pick(engine, diag_engine, band), x, band)
+    batch = _fused(engine, x)
     adv, fixed = batch.host_trace()
     oadv, ofixed, oh, ooff = orc.fill(_as_oracle(x, orc))
     for c in range(10):
@@ -74,13 +66,15 @@ def test_fused_equals_oracle(engine, diag_engine, orc, band, rounds_choices, n, 
     assert rep["first_failure"] == NONE and rep["rows_checked"] == int(ooff[-1])
 
 
-def test_fused_padded_tail(engine, diag_engine, orc):
-    """total_rows past the batch (not a multiple of the 1024-row tile): zero rows, clean."""
+@pytest.mark.parametrize("pad", [4, 252, 256, 1028])
+def test_fused_padded_tail(engine, orc, pad):
+    """total_rows past the batch (zero tail tiles of 64 quads, the last one partial): zero
+    rows, clean."""
     import b2f
 
     x = random_inputs(9, (1, 4), 34)
-    total = int(b2f.offsets(x)[-1]) + 1028
-    batch = _fused(diag_engine, x, 2, total_rows=total)
+    total = int(b2f.offsets(x)[-1]) + pad
+    batch = _fused(engine, x, total_rows=total)
     adv, fixed = batch.host_trace()
     used = batch.used_rows
     assert not adv[:, used:].any() and not fixed[used:].any()
@@ -88,12 +82,12 @@ def test_fused_padded_tail(engine, diag_engine, orc):
     assert rep == orc.evaluate(adv, fixed, batch.offsets_host) and rep["first_failure"] == NONE
 
 
-def _boundary_rows(total, rng, k):
-    """Rows on both sides of tile boundaries, the first/last rows, and random rows."""
+def _boundary_rows(total, starts, rng, k):
+    """Rows on both sides of the given tile starts, the first/last rows, and random rows."""
     rows = set()
-    for t in range(1, (total + 1023) // 1024):
-        for d in (-16, -13, -12, -9, -5, -4, -1, 0, 1, 3, 4, 11, 15):
-            r = 1024 * t + d
+    for t in starts:
+        for d in (-16, -13, -12, -9, -5, -4, -1, 0, 1, 3, 4, 11, 15, 29, 45, 51):
+            r = t + d
             if 0 <= r < total:
                 rows.add(r)
     rows.update([0, 1, 2, 3, total - 1, total - 2, total - 4, total - 8, total - 12])
@@ -103,27 +97,41 @@ def _boundary_rows(total, rng, k):
     return [int(r) for r in pick]
 
 
-@pytest.mark.parametrize("band", [1, 3, 16])
-def test_fused_injection_matches_eval(engine, diag_engine, orc, band):
+def _tile_rows(x):
+    """First rows of the fused kernel's tiles (init, every half-round, final) and of the zero
+    tail's 64-quad tiles."""
+    import b2f
+
+    off = b2f.offsets(x)
+    out = []
+    for i, r in enumerate(x["rounds"]):
+        o = int(off[i])
+        out += [o, o + 164] + [o + 164 + 208 * h for h in range(1, 2 * int(r))] + \
+            [o + 164 + 416 * int(r)]
+    return out
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_fused_injection_matches_eval(engine, orc, seed):
     """Fused verdict == b2f_eval_dev verdict on the trace the fused kernel wrote, for single
-    cell faults in every column (advice and fixed) at tile/band boundaries; the written trace
-    differs from the clean one in exactly the injected cell; a subset is checked against the
-    oracle too."""
+    cell faults in every column (advice and fixed) on both sides of the fused kernel's tile
+    boundaries (init / half-round / final tiles: copy sources recomputed from the producer
+    side, gates deferred past the tile end) and at random rows; the written trace differs from
+    the clean one in exactly the injected cell; a subset is checked against the oracle too."""
     import torch
 
-    engine = _pick(engine, diag_engine, band)
-    rng = np.random.default_rng(40 + band)
-    x = random_inputs(24, (0, 1, 4, 12), 41)
-    clean = _fused(engine, x, band)
+    rng = np.random.default_rng(40 + seed)
+    x = random_inputs(24, (0, 1, 4, 12), 41 + seed)
+    clean = _fused(engine, x)
     cadv, cfix = clean.advice.clone(), clean.fixed.clone()
     total = clean.total_rows
     flagged = 0
     cases = 0
-    for r in _boundary_rows(total, rng, 96):
+    for r in _boundary_rows(total, _tile_rows(x), rng, 96):
         for col in rng.choice(11, size=2, replace=False):
             col = int(col)
             bit = int(rng.integers(0, 16 if col == 10 and rng.random() < 0.7 else 32))
-            batch = _fused(engine, x, band, inject=(r, col, 1 << bit))
+            batch = _fused(engine, x, inject=(r, col, 1 << bit))
             dadv = (batch.advice != cadv).nonzero().cpu().numpy()
             dfix = (batch.fixed != cfix).nonzero().cpu().numpy()
             if col < 10:
@@ -145,7 +153,7 @@ def test_fused_injection_matches_eval(engine, diag_engine, orc, band):
     assert flagged > cases // 3
 
 
-def test_fused_injection_last_rows(diag_engine, orc):
+def test_fused_injection_last_rows(engine, orc):
     """Selector bits injected into the last rows of the trace: gates that run past the end
     read zero rows (the eval's out-of-trace rule) -- through the fused kernel's zero halo."""
     import b2f
@@ -156,7 +164,7 @@ def test_fused_injection_last_rows(diag_engine, orc):
     for total_rows in (total, total_p):
         for r in (total_rows - 1, total_rows - 3, total_rows - 7, total_rows - 12):
             for bit in (0, 1, 4, 6, 8, 11, 13, 15):
-                batch = _fused(diag_engine, x, 2, total_rows=total_rows, inject=(r, 10, 1 << bit))
+                batch = _fused(engine, x, total_rows=total_rows, inject=(r, 10, 1 << bit))
                 got = batch.report_dict()
                 adv, fixed = batch.host_trace()
                 assert got == orc.evaluate(adv, fixed, batch.offsets_host), (total_rows, r, bit)
@@ -177,7 +185,7 @@ def test_fused_2p16_equals_fill_eval(engine):
     a.evaluate(engine)
     engine.sync(_stream())
     ra = a.report_dict()
-    b = _fused(engine, x, 16)
+    b = _fused(engine, x)
     assert torch.equal(a.advice, b.advice) and torch.equal(a.fixed, b.fixed)
     assert torch.equal(a.h_out, b.h_out)
     assert b.report_dict() == ra and ra["first_failure"] == NONE
@@ -190,7 +198,7 @@ def test_fused_mixed_rounds_2p14(engine, orc):
 
     n = 1 << 14
     x = synth.batch(n, rounds_mix=[1, 4, 12])
-    batch = _fused(engine, x, 16)
+    batch = _fused(engine, x)
     rep = batch.report_dict()
     assert rep["first_failure"] == NONE and sum(rep["gate_failures"]) == 0
     off = batch.offsets_host

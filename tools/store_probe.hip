@@ -63,6 +63,25 @@ __global__ void __launch_bounds__(256) wave_store(uint32_t* adv, uint64_t total_
   }
 }
 
+// wave-granular round robin: wave w writes tiles w, w + W, ... of STEP quads each (rows 4 STEP t
+// onwards): the order a wave-per-tile fused kernel writes in
+template <int STEP>
+__global__ void __launch_bounds__(256) wave_rr_store(uint32_t* adv, uint64_t total_rows) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  const uint64_t total_quads = total_rows >> 2;
+  const uint64_t n_t = (total_quads + STEP - 1) / STEP;
+  for (uint64_t t = wid; t < n_t; t += nw) {
+    const uint64_t q = t * STEP + lane;
+    if (lane < STEP && q < total_quads) {
+      const u32x4 v = {(uint32_t)q, 1u, 2u, 3u};
+#pragma unroll
+      for (int c = 0; c < 11; c++)
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(adv + (uint64_t)c * total_rows + 4 * q));
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? atoi(argv[1]) : (1u << 18);
   const uint32_t rows_per = 228 + 416 * 12;
@@ -99,7 +118,14 @@ int main(int argc, char** argv) {
     snprintf(nm, sizeof nm, "tile_rr_%dwg", w);
     run(nm, [&] { hipLaunchKernelGGL(tile_store, dim3(cus * w), dim3(256), 0, 0, adv, total, nt); });
   }
-  for (int w : {4, 2}) {
+  for (int w : {4, 3, 2}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "wave_rr_q52_%dwg", w);
+    run(nm, [&] { hipLaunchKernelGGL(wave_rr_store<52>, dim3(cus * w), dim3(256), 0, 0, adv, total); });
+    snprintf(nm, sizeof nm, "wave_rr_q64_%dwg", w);
+    run(nm, [&] { hipLaunchKernelGGL(wave_rr_store<64>, dim3(cus * w), dim3(256), 0, 0, adv, total); });
+  }
+  for (int w : {4}) {
     char nm[64];
     snprintf(nm, sizeof nm, "wave_dyn_step52_%dwg", w);
     run(nm, [&] { hipLaunchKernelGGL((wave_store<52, true>), dim3(cus * w), dim3(256), 0, 0, adv, total, n, rows_per, ctr); });

@@ -41,12 +41,14 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
 hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
                             uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
                             int cu_count, hipStream_t s);  // b2f_export.hip
+size_t fused_scratch_bytes(uint64_t tiles);
+uint64_t fused_instance_tiles(uint64_t total_rows, uint64_t n);
 hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d_off,
                             uint64_t total_rows, const uint64_t* rec, uint32_t* d_adv,
-                            uint32_t* d_fixed, const void* tinfo, uint64_t n_tiles, uint32_t band,
+                            uint32_t* d_fixed, void* scratch, uint64_t tiles,
                             b2f_eval_report* d_rep, const int* d_status, uint64_t inj_row,
                             uint32_t inj_col, uint32_t inj_mask, int mode, int cu_count,
-                            unsigned long long* clk, hipStream_t s);  // b2f_fused.hip
+                            hipStream_t s);  // b2f_fused.hip
 }
 
 namespace {
@@ -722,6 +724,8 @@ struct b2f_ctx {
   uint32_t inj_col, inj_mask;
   void* d_lk;          // lookup-column scratch (b2f_lookup.hip carve)
   size_t lk_cap;
+  void* d_fz;          // fused-path scratch: tile descriptors + deferred rows (b2f_fused.hip)
+  size_t fz_cap;
 };
 
 namespace {
@@ -943,6 +947,7 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
   (void)hipFree(ctx->d_tiles);
   (void)hipFree(ctx->d_clock);
   (void)hipFree(ctx->d_lk);
+  (void)hipFree(ctx->d_fz);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   delete ctx;
 }
@@ -990,6 +995,9 @@ int fill_prologue(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const uint64_t*
   HIPCHK(ctx, hipSetDevice(ctx->device));
   // states = 2*sum(rounds) + n  <=  2*(total_rows - 228 n)/416 + n
   uint64_t states = 2 * ((total_rows - (uint64_t)FIXED_ROWS * n) / ROUND_ROWS) + n;
+  if (states >= (1ull << 32))
+    return set_err(ctx, B2F_ERR_ROWS, "fill: %llu rows exceed the 2^32 half-round states of one call",
+                   (unsigned long long)total_rows);
   if (states > ctx->rec_cap) {
     HIPCHK(ctx, hipStreamSynchronize(s));
     if (ctx->d_rec) HIPCHK(ctx, hipFree(ctx->d_rec));
@@ -1056,20 +1064,21 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
   hipStream_t s = (hipStream_t)stream;
   int rc = fill_prologue(ctx, d_in, n, d_offsets, total_rows, d_advice, d_fixed, d_h_out, d_report, s);
   if (rc) return rc;
-  const uint64_t nt = n_tiles_of(total_rows);
-  rc = launch_tile_index(ctx, d_offsets, n, nt, s, 16);
-  if (rc) return rc;
-  const uint32_t band = (uint32_t)diag_mode("B2F_BAND", 16);
-  const int fmode = fused_mode();
-  if ((fmode & 128) && !ctx->d_clock) {
-    HIPCHK(ctx, hipMalloc(&ctx->d_clock, 32 * sizeof(unsigned long long)));
-    HIPCHK(ctx, hipMemset(ctx->d_clock, 0, 32 * sizeof(unsigned long long)));
+  const uint64_t tiles = fused_instance_tiles(total_rows, n);
+  const size_t need = fused_scratch_bytes(tiles);
+  if (need > ctx->fz_cap) {
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    if (ctx->d_fz) HIPCHK(ctx, hipFree(ctx->d_fz));
+    ctx->d_fz = nullptr;
+    ctx->fz_cap = 0;
+    HIPCHK(ctx, hipMalloc(&ctx->d_fz, need));
+    ctx->fz_cap = need;
   }
   const int tk = timed_begin(ctx, B2F_KERNEL_FILL_EVAL, s);
   HIPCHK(ctx, launch_fill_eval(d_in, (uint32_t)n, d_offsets, total_rows, ctx->d_rec, d_advice,
-                               d_fixed, ctx->d_tiles, nt, band, d_report, ctx->d_status,
-                               ctx->inj_row, ctx->inj_col, ctx->inj_mask,
-                               fmode, ctx->cu_count, ctx->d_clock, s));
+                               d_fixed, ctx->d_fz, tiles, d_report, ctx->d_status,
+                               ctx->inj_row, ctx->inj_col, ctx->inj_mask, fused_mode(),
+                               ctx->cu_count, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
