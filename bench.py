@@ -5,9 +5,11 @@
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
     ... bench.py --gpus 8 --global-batch 1048576                 (BASELINE configs[3])
 
-One step = fill (record + fill kernels) then eval of the whole per-GPU batch (--path split, the
-headline; --path fused runs b2f_fill_eval_dev instead; the other path is timed beside it as
-"other_path"); inputs and the trace stay resident in HBM. N > 1: by default every rank runs its
+One step = witness fill + constraint eval of the whole per-GPU batch: --path fused (the
+headline) runs b2f_fill_eval_dev (record kernel + the fused kernel that checks every tile as it
+assigns it; the trace is written once and never read back), --path split runs b2f_fill_dev then
+b2f_eval_dev; the other path is timed beside it as "other_path". Inputs and the trace stay
+resident in HBM. N > 1: by default every rank runs its
 own 2^18 batch (weak scaling); --global-batch G shards G instances over the ranks with the
 row-balanced dist.plan_shards (strong scaling). Either way the step ends with one all_reduce of
 the verdict counters and one RCCL all_gather of the h' outputs. The whole witness table is
@@ -137,9 +139,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--export-rows", type=int, default=1 << 25,
                     help="rows of the Fp export timed after the headline loop (0 = skip)")
-    ap.add_argument("--path", choices=["split", "fused"], default="split",
-                    help="split: fill kernel then eval kernel (the headline); fused: "
-                         "b2f_fill_eval_dev, one kernel that checks each tile as it assigns it")
+    ap.add_argument("--path", choices=["split", "fused"], default="fused",
+                    help="fused (the headline): b2f_fill_eval_dev, one kernel that checks each "
+                         "tile as it assigns it; split: the fill kernel then the eval kernel")
     ap.add_argument("--lookup-circuits", type=int, default=64,
                     help="lookup-argument columns for this many 2^17-row circuits of the trace "
                          "(reported beside the headline; 0 skips)")

@@ -14,7 +14,8 @@ PHASES = ["stage+lookup", "barrier1", "prefetch", "gtable", "gpass", "copies", "
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1 << 18)
-    ap.add_argument("--fused", action="store_true", help="the fused kernel (B2F_DIAG_FUSED=155)")
+    ap.add_argument("--fused", type=int, default=0,
+                    help="the fused kernel's clocked variant: 155 (full), 130 (stores only), 128")
     args = ap.parse_args()
     import torch
 
@@ -27,11 +28,11 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     batch.fill(eng, s)
     run = batch.fill_evaluate if args.fused else batch.evaluate
-    os.environ["B2F_DIAG_FUSED" if args.fused else "B2F_DIAG_EVAL"] = "155" if args.fused else "23"
+    os.environ["B2F_DIAG_FUSED" if args.fused else "B2F_DIAG_EVAL"] = str(args.fused) if args.fused else "23"
     if args.fused:
         global PHASES
-        PHASES = ["loads+1", "band+ic", "assign+stage", "store", "ti+barrier1", "gtable",
-                  "lookup+gpass+copies", "perquad+barrier2"]
+        PHASES = ["ctx+loads", "producers", "assign+stage", "msgcopy", "settle", "stores",
+                  "lkp+fixed+gates", "copies/other"]
     run(eng, s)
     eng.sync(s)
     out = (ctypes.c_uint64 * 32)()

@@ -82,6 +82,112 @@ __global__ void __launch_bounds__(256) wave_rr_store(uint32_t* adv, uint64_t tot
   }
 }
 
+// the same order with per-tile work in front of the stores: `work` rounds of a dependent
+// integer hash per lane (~4 VALU each), optionally staged through LDS and read back (STAGE), and
+// stored with raw buffer stores (BUF) instead of global stores
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+__device__ void probe_buffer_store(i32x4 data, i32x4 rsrc, int voffset, int soffset,
+                                   int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
+template <int STEP, bool STAGE, bool BUF>
+__global__ void __launch_bounds__(256) wave_rr_work(uint32_t* adv, uint64_t total_rows, int work) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[4 * 11 * 256];
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t* S = L + (threadIdx.x >> 6) * 11 * 256;
+  const uint64_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  const uint64_t total_quads = total_rows >> 2;
+  const uint64_t n_t = (total_quads + STEP - 1) / STEP;
+  for (uint64_t t = wid; t < n_t; t += nw) {
+    const uint64_t q = t * STEP + lane;
+    uint32_t h = (uint32_t)q;
+    for (int k = 0; k < work; k++) h = (h ^ (h >> 7)) * 0x9E3779B1u + (uint32_t)k;
+    u32x4 v[11];
+#pragma unroll
+    for (int c = 0; c < 11; c++) v[c] = u32x4{h + c, h ^ c, h * c, h - c};
+    if (STAGE) {
+#pragma unroll
+      for (int c = 0; c < 11; c++) *reinterpret_cast<u32x4*>(S + c * 256 + 4 * lane) = v[c];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int c = 0; c < 11; c++) v[c] = *reinterpret_cast<const u32x4*>(S + c * 256 + 4 * lane);
+    }
+    const uint32_t nq = (uint32_t)(total_quads - t * STEP < STEP ? total_quads - t * STEP : STEP);
+#pragma unroll
+    for (int c = 0; c < 11; c++) {
+      uint32_t* base = adv + (uint64_t)c * total_rows + 4 * t * STEP;
+      if (BUF) {
+        const uint64_t a = reinterpret_cast<uint64_t>(base);
+        const i32x4 rsrc = {(int32_t)(uint32_t)a, (int32_t)(uint32_t)(a >> 32), (int32_t)(nq * 16u), 0x00020000};
+        probe_buffer_store(i32x4{(int32_t)v[c].x, (int32_t)v[c].y, (int32_t)v[c].z, (int32_t)v[c].w}, rsrc, (int)(16 * lane), 0, 2);
+      } else if (lane < nq) {
+        __builtin_nontemporal_store(v[c], reinterpret_cast<u32x4*>(base + 4 * lane));
+      }
+    }
+    if (STAGE) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+// interleaved: the tile's work split into 11 parts, each followed by its column's store;
+// STAGGER: wave w of a workgroup first runs (w % 4) / 4 of a tile's work, so the waves of a SIMD
+// are out of phase
+template <int STEP, bool STAGGER>
+__global__ void __launch_bounds__(256) wave_rr_inter(uint32_t* adv, uint64_t total_rows, int work) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  const uint64_t total_quads = total_rows >> 2;
+  const uint64_t n_t = (total_quads + STEP - 1) / STEP;
+  uint32_t h = lane;
+  if (STAGGER)
+    for (int k = 0; k < (int)(wid & 3) * work / 4; k++) h = (h ^ (h >> 7)) * 0x9E3779B1u + (uint32_t)k;
+  for (uint64_t t = wid; t < n_t; t += nw) {
+    const uint64_t q = t * STEP + lane;
+    h ^= (uint32_t)q;
+#pragma unroll
+    for (int c = 0; c < 11; c++) {
+      for (int k = 0; k < work / 11; k++) h = (h ^ (h >> 7)) * 0x9E3779B1u + (uint32_t)k;
+      if (lane < STEP && q < total_quads)
+        __builtin_nontemporal_store(u32x4{h, h + 1, h + 2, h + 3},
+                                    reinterpret_cast<u32x4*>(adv + (uint64_t)c * total_rows + 4 * q));
+    }
+  }
+}
+template <int STEP>
+__global__ void __launch_bounds__(256) wave_rr_stagger(uint32_t* adv, uint64_t total_rows, int work) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  const uint64_t total_quads = total_rows >> 2;
+  const uint64_t n_t = (total_quads + STEP - 1) / STEP;
+  uint32_t h = lane;
+  for (int k = 0; k < (int)(wid & 3) * work / 4; k++) h = (h ^ (h >> 7)) * 0x9E3779B1u + (uint32_t)k;
+  for (uint64_t t = wid; t < n_t; t += nw) {
+    const uint64_t q = t * STEP + lane;
+    h ^= (uint32_t)q;
+    for (int k = 0; k < work; k++) h = (h ^ (h >> 7)) * 0x9E3779B1u + (uint32_t)k;
+    if (lane < STEP && q < total_quads) {
+#pragma unroll
+      for (int c = 0; c < 11; c++)
+        __builtin_nontemporal_store(u32x4{h + c, h ^ c, h * c, h - c},
+                                    reinterpret_cast<u32x4*>(adv + (uint64_t)c * total_rows + 4 * q));
+    }
+  }
+}
+template <int STEP>
+__global__ void __launch_bounds__(256) wave_rr_nostore(uint32_t* adv, uint64_t total_rows, int work) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  const uint64_t total_quads = total_rows >> 2;
+  const uint64_t n_t = (total_quads + STEP - 1) / STEP;
+  uint32_t h = lane;
+  for (uint64_t t = wid; t < n_t; t += nw) {
+    h ^= (uint32_t)(t * STEP + lane);
+    for (int k = 0; k < work; k++) h = (h ^ (h >> 7)) * 0x9E3779B1u + (uint32_t)k;
+  }
+  if (h == 0x12345678u) adv[lane] = h;
+}
+
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? atoi(argv[1]) : (1u << 18);
   const uint32_t rows_per = 228 + 416 * 12;
@@ -118,14 +224,29 @@ int main(int argc, char** argv) {
     snprintf(nm, sizeof nm, "tile_rr_%dwg", w);
     run(nm, [&] { hipLaunchKernelGGL(tile_store, dim3(cus * w), dim3(256), 0, 0, adv, total, nt); });
   }
-  for (int w : {4, 3, 2}) {
+  for (int work : {120, 240}) {
+    char nm[96];
+    snprintf(nm, sizeof nm, "work%d_nostore", work);
+    run(nm, [&] { hipLaunchKernelGGL(wave_rr_nostore<52>, dim3(cus * 4), dim3(256), 0, 0, adv, total, work); });
+    snprintf(nm, sizeof nm, "work%d_burst", work);
+    run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<52, false, false>), dim3(cus * 4), dim3(256), 0, 0, adv, total, work); });
+    snprintf(nm, sizeof nm, "work%d_burst_stagger", work);
+    run(nm, [&] { hipLaunchKernelGGL(wave_rr_stagger<52>, dim3(cus * 4), dim3(256), 0, 0, adv, total, work); });
+    snprintf(nm, sizeof nm, "work%d_interleaved", work);
+    run(nm, [&] { hipLaunchKernelGGL((wave_rr_inter<52, false>), dim3(cus * 4), dim3(256), 0, 0, adv, total, work); });
+    snprintf(nm, sizeof nm, "work%d_interleaved_stagger", work);
+    run(nm, [&] { hipLaunchKernelGGL((wave_rr_inter<52, true>), dim3(cus * 4), dim3(256), 0, 0, adv, total, work); });
+    snprintf(nm, sizeof nm, "work%d_burst_8wg", work);
+    run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<52, false, false>), dim3(cus * 8), dim3(256), 0, 0, adv, total, work); });
+  }
+  for (int w : {4}) {
     char nm[64];
     snprintf(nm, sizeof nm, "wave_rr_q52_%dwg", w);
     run(nm, [&] { hipLaunchKernelGGL(wave_rr_store<52>, dim3(cus * w), dim3(256), 0, 0, adv, total); });
     snprintf(nm, sizeof nm, "wave_rr_q64_%dwg", w);
     run(nm, [&] { hipLaunchKernelGGL(wave_rr_store<64>, dim3(cus * w), dim3(256), 0, 0, adv, total); });
   }
-  for (int w : {4}) {
+  for (int w : {0}) {
     char nm[64];
     snprintf(nm, sizeof nm, "wave_dyn_step52_%dwg", w);
     run(nm, [&] { hipLaunchKernelGGL((wave_store<52, true>), dim3(cus * w), dim3(256), 0, 0, adv, total, n, rows_per, ctr); });

@@ -35,20 +35,26 @@
 #include "../../include/b2f.h"
 #include "b2f_common.h"
 
+typedef int32_t b2f_i32x4 __attribute__((ext_vector_type(4)));
+// the raw buffer store intrinsic (declared as CK's amd_buffer_addressing.hpp does)
+__device__ void b2f_raw_buffer_store_v4(b2f_i32x4 data, b2f_i32x4 rsrc, int voffset, int soffset,
+                                        int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
+
 namespace {
 
+using i32x4 = b2f_i32x4;
 constexpr int FW = 64;            // lanes per wave
 constexpr int WAVES = 4;          // waves per workgroup
 constexpr int STR = 208;          // staged rows per column (a half-round tile)
 constexpr uint32_t HR_Q = 52, INIT_Q = 41, FINAL_Q = 16, PAD_Q = 64;
-constexpr int NSTAGE = 9;         // staged columns a_0 .. a_8
+constexpr int NSTAGE = 11;        // staged columns a_0 .. a_9 and the fixed column
+constexpr int FXC = 10;           // staging column of the fixed cells
 
-// per-wave LDS region (words): a_0..a_8 [9][STR], per-quad canonical flag and row-0 a_9,
-// the 16 producer words (u64)
-constexpr int S_CANON = NSTAGE * STR;
-constexpr int S_A9 = S_CANON + HR_Q;
-constexpr int S_PROD = S_A9 + HR_Q;
-constexpr int WAVE_WORDS = S_PROD + 32;
+// per-wave LDS region (words): a_0..a_9, fixed [11][STR], the 16 producer words (u64), a
+// per-quad flag "the quad's selector bits are the keygen structure's" (init / final tiles)
+constexpr int S_PROD = NSTAGE * STR;
+constexpr int S_CANON = S_PROD + 32;
+constexpr int WAVE_WORDS = S_CANON + INIT_Q + 3;
 static_assert(S_PROD % 2 == 0 && WAVE_WORDS % 4 == 0 && STR % 4 == 0, "aligned wave carve");
 
 // Copy checks of a half-round tile whose source is not a message word: 64 per G, 256 per tile,
@@ -95,25 +101,6 @@ constexpr HrChecks make_hr_checks() {
 constexpr bool hr_checks_ok() { return make_hr_checks().e[0][0] != 0xffffffffu; }
 static_assert(hr_checks_ok(), "64 non-message copy checks per G");
 __constant__ HrChecks c_hr_checks = make_hr_checks();
-
-// Rows each gate reads past its selector row, minus one (LAYOUT.md §4): abcd 4, efgh 11,
-// ijkl 7, a1 4, b1 12, c1 4, d1 8, a2 4, b2 8, c2 4, d2 8, digest 7, xor 8, xor3 8, const 1,
-// fmask 4.
-constexpr uint64_t gate_span() {
-  const uint32_t rows[16] = {4, 11, 7, 4, 12, 4, 8, 4, 8, 4, 8, 7, 8, 8, 1, 4};
-  uint64_t s = 0;
-  for (int i = 0; i < 16; i++) s |= (uint64_t)(rows[i] - 1) << (4 * i);
-  return s;
-}
-constexpr uint64_t kGateSpan = gate_span();
-__device__ __forceinline__ uint32_t span_of(uint32_t sel) {  // max over the set bits
-  uint32_t m = 0;
-  for (uint32_t b = sel; b; b &= b - 1) {
-    const uint32_t s = (uint32_t)(kGateSpan >> (4 * __builtin_ctz(b))) & 15u;
-    m = s > m ? s : m;
-  }
-  return m;
-}
 
 // (a, b, c, d) word indices of G g packed in bytes (column G's g < 4, diagonal g >= 4)
 __device__ __forceinline__ uint32_t gidx_word(uint32_t g) {
@@ -170,8 +157,11 @@ __device__ __forceinline__ uint32_t inj_at(const Inject& inj, uint64_t row, uint
 
 enum : uint32_t { T_INIT = 0, T_HR, T_FINAL, T_PAD };
 
-struct TileDesc {  // 16 B, written by tile_desc_kernel
-  uint32_t inst, j, rounds, st;
+union TileDesc {  // 16 B, written by tile_desc_kernel
+  struct {
+    uint32_t inst, j, rounds, st;
+  } f;
+  uint4 v;
 };
 
 // A tile as the wave sees it (wave-uniform).
@@ -211,95 +201,298 @@ __device__ __forceinline__ Ctx make_ctx(uint64_t t, uint64_t t_inst, const uint4
   return c;
 }
 
-// Operand words of one lane for a tile (loaded one tile ahead of their use):
-//   quad lanes: the quad's operands (half-round: its G's a b c d at the half-round start and
-//   message words x y; init: the input word it decomposes; final: h_i, v_i, v_{i+8});
-//   producer lanes (the four lanes after the quads of half-round and final tiles): the G chain
-//   operands of the previous half-round, whose outputs are this tile's state-word copy
-//   sources, or for the first half-round / a 0-round final the initial work vector words;
-//   aux (half-round lanes < 32): the message word of the lane's message-copy check.
+// Operand words of one lane for a tile, loaded one tile ahead of their use. Every lane loads
+// all seven words unconditionally from a per-lane address (a harmless in-bounds word where the
+// lane has no use for one) and nothing is derived from them here: a conditional load or a use
+// right after the load would make the wave wait for its outstanding stores (vmcnt retires
+// loads and stores in order). Roles:
+//   quad lanes: half-round: its G's a b c d at the half-round start, message words x y;
+//     init: the input word the quad decomposes (h / m / t, the `rounds | f << 32` word);
+//     final: h_i, v_i, v_{i+8}
+//   producer lanes (the four lanes after the quads of half-round and final tiles): the
+//     previous half-round's G operands (its outputs are this tile's state-word copy sources),
+//     or for the first half-round / a 0-round final: h_g, h_{g+4}, -, the t / f word of v_{g+12}
+//   w[6] (half-round lanes < 32): the message word of the lane's message-copy check
 struct Ops {
-  uint64_t w[6];
-  uint64_t aux;
+  uint64_t w[7];
 };
 
 __device__ __forceinline__ Ops load_ops(const Ctx& c, uint32_t lane, const b2f_input* __restrict__ in,
-                                        const uint64_t* __restrict__ rec, const uint8_t* Sg,
-                                        const uint64_t* IV) {
-  Ops o;
-#pragma unroll
-  for (int k = 0; k < 6; k++) o.w[k] = 0;
-  o.aux = 0;
-  if (c.kind == T_PAD) return o;
-  const b2f_input* x = in + c.inst;
+                                        const uint64_t* __restrict__ rec, const uint8_t* Sg) {
+  const b2f_input* x = in + (c.kind == T_PAD ? 0u : c.inst);
   const uint64_t* fw = reinterpret_cast<const uint64_t*>(&x->rounds);  // rounds | f << 32
-  if (c.kind == T_INIT) {
-    if (lane < INIT_Q) {
-      const uint64_t* p = fw;
-      bool ld = true;
-      if (lane < 26) p = lane < 8 ? x->h + lane : (lane < 24 ? x->m + (lane - 8) : x->t + (lane - 24));
-      else if (lane < 35) ld = lane == 26;  // fmask reads the f word; CONST quads read nothing
-      else p = ((lane - 35) >> 1) < 2 ? x->t + ((lane - 35) >> 1) : fw;
-      o.w[0] = ld ? *p : 0ull;
-    }
-    return o;
-  }
+  const uint64_t* p[7] = {fw, fw, fw, fw, fw, fw, fw};
   const uint32_t npq = c.kind == T_HR ? HR_Q : FINAL_Q;
   const uint64_t* st0 = rec + 16ull * c.st;
-  if (lane < npq) {
-    if (c.kind == T_HR) {
-      const uint32_t gg = lane / G_QUADS, g = gg + 4 * (c.hr & 1u);
-      const uint64_t* s = st0 + 16ull * c.hr;
-      const uint32_t gi = gidx_word(g);
-      const uint8_t* sg = Sg + 16 * ((c.hr >> 1) % 10) + 2 * g;
-      o.w[0] = s[gi & 15u];
-      o.w[1] = s[(gi >> 8) & 15u];
-      o.w[2] = s[(gi >> 16) & 15u];
-      o.w[3] = s[(gi >> 24) & 15u];
-      o.w[4] = x->m[sg[0]];
-      o.w[5] = x->m[sg[1]];
-    } else {
-      const uint32_t a = lane >> 1;
-      const uint64_t* fin = st0 + 16ull * (2ull * c.rounds);
-      o.w[0] = x->h[a];
-      o.w[1] = fin[a];
-      o.w[2] = fin[a + 8];
-    }
-  } else if (lane < npq + 4) {
-    const uint32_t gg = lane - npq;
+  if (c.kind == T_INIT) {
+    if (lane < 26) p[0] = lane < 8 ? x->h + lane : (lane < 24 ? x->m + (lane - 8) : x->t + (lane - 24));
+    else if (lane >= 35 && ((lane - 35) >> 1) < 2) p[0] = x->t + ((lane - 35) >> 1);
+  } else if (c.kind == T_HR || c.kind == T_FINAL) {
+    const bool prodl = lane >= npq && lane < npq + 4;
+    const uint32_t gg = prodl ? lane - npq : lane / G_QUADS;
     const bool first = c.kind == T_HR ? c.hr == 0 : c.rounds == 0;
-    if (first) {  // the initial work vector words of column G gg: v_gg, v_gg+4, IV_gg, v_gg+12
-      o.w[0] = x->h[gg];
-      o.w[1] = x->h[gg + 4];
-      o.w[2] = IV[gg];
-      const uint64_t tw = gg < 2 ? x->t[gg] : (gg == 2 ? ((*fw >> 32) ? ~0ull : 0ull) : 0ull);
-      o.w[3] = IV[gg + 4] ^ tw;
-    } else {
-      const uint32_t hp = c.kind == T_HR ? c.hr - 1 : 2 * c.rounds - 1;
-      const uint32_t g = gg + 4 * (hp & 1u);
-      const uint64_t* s = st0 + 16ull * hp;
+    if (c.kind == T_FINAL && !prodl) {
+      const uint32_t a = (lane >> 1) & 7u;
+      const uint64_t* fin = st0 + 16ull * (2ull * c.rounds);
+      p[0] = x->h + a;
+      p[1] = fin + a;
+      p[2] = fin + a + 8;
+    } else if (prodl && first) {
+      p[0] = x->h + gg;
+      p[1] = x->h + gg + 4;
+      p[3] = gg < 2 ? x->t + gg : fw;
+    } else if (lane < npq + 4) {
+      const uint32_t h = prodl ? (c.kind == T_HR ? c.hr - 1 : 2 * c.rounds - 1) : c.hr;
+      const uint32_t g = (gg & 3u) + 4 * (h & 1u);
+      const uint64_t* s = st0 + 16ull * h;
       const uint32_t gi = gidx_word(g);
-      const uint8_t* sg = Sg + 16 * ((hp >> 1) % 10) + 2 * g;
-      o.w[0] = s[gi & 15u];
-      o.w[1] = s[(gi >> 8) & 15u];
-      o.w[2] = s[(gi >> 16) & 15u];
-      o.w[3] = s[(gi >> 24) & 15u];
-      o.w[4] = x->m[sg[0]];
-      o.w[5] = x->m[sg[1]];
+      const uint8_t* sg = Sg + 16 * ((h >> 1) % 10) + 2 * g;
+      p[0] = s + (gi & 15u);
+      p[1] = s + ((gi >> 8) & 15u);
+      p[2] = s + ((gi >> 16) & 15u);
+      p[3] = s + ((gi >> 24) & 15u);
+      p[4] = x->m + sg[0];
+      p[5] = x->m + sg[1];
     }
+    if (c.kind == T_HR && lane < 32)
+      p[6] = x->m + Sg[16 * ((c.hr >> 1) % 10) + 2 * ((lane >> 3) + 4 * (c.hr & 1u)) + ((lane >> 2) & 1u)];
   }
-  if (c.kind == T_HR && lane < 32) {
-    const uint32_t g = (lane >> 3) + 4 * (c.hr & 1u), which = (lane >> 2) & 1u;
-    o.aux = x->m[Sg[16 * ((c.hr >> 1) % 10) + 2 * g + which]];
-  }
+  Ops o;
+#ifdef B2F_FZ_NOLOAD  // diagnostics: operand words without memory traffic (wrong trace)
+#pragma unroll
+  for (int k = 0; k < 7; k++) o.w[k] = reinterpret_cast<uint64_t>(p[k]) * 0x9E3779B97F4A7C15ull;
+#else
+#pragma unroll
+  for (int k = 0; k < 7; k++) o.w[k] = *p[k];
+#endif
   return o;
+}
+
+// The producer lanes' outputs: the four words of G g as the previous half-round ends (its
+// chain a2 b2 c2 d2), or the initial work vector words of column G g, into the wave's prod.
+__device__ __forceinline__ void producer_words(uint64_t* prod, const Ops& P, uint32_t pg, bool first,
+                                               uint32_t hp, const uint64_t* IV) {
+  uint64_t o0, o1, o2, o3;
+  uint32_t g = pg;
+  if (first) {
+    o0 = P.w[0];
+    o1 = P.w[1];
+    o2 = IV[pg];
+    const uint64_t tw = pg < 2 ? P.w[3] : (pg == 2 ? ((P.w[3] >> 32) ? ~0ull : 0ull) : 0ull);
+    o3 = IV[pg + 4] ^ tw;
+  } else {
+    g = pg + 4 * (hp & 1u);
+    const uint64_t a1 = P.w[0] + P.w[1] + P.w[4];
+    const uint64_t d1 = rotr64(P.w[3] ^ a1, 32);
+    const uint64_t c1 = P.w[2] + d1;
+    const uint64_t b1 = rotr64(P.w[1] ^ c1, 24);
+    o0 = a1 + b1 + P.w[5];
+    o3 = rotr64(d1 ^ o0, 16);
+    o2 = c1 + o3;
+    o1 = rotr64(b1 ^ o2, 63);
+  }
+  const uint32_t gi = gidx_word(g);
+  prod[gi & 15u] = o0;
+  prod[(gi >> 8) & 15u] = o1;
+  prod[(gi >> 16) & 15u] = o2;
+  prod[(gi >> 24) & 15u] = o3;
 }
 
 // MODE (diagnostics; the product launches FZ_FULL, with FZ_INJECT only under the test hook)
 #ifndef B2F_FUSED_WAVES
-#define B2F_FUSED_WAVES 2  // waves per SIMD the fused kernel is compiled for (VGPR budget)
+#define B2F_FUSED_WAVES 4  // waves per SIMD the fused kernel is compiled for (VGPR budget)
 #endif
-enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16, FZ_FULL = 27 };
+enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16, FZ_FULL = 27,
+       FZ_CLOCK = 128 };  // per-phase s_memtime totals per wave slot (diagnostics, b2f_debug_clock)
+
+// Stores of a tile: raw buffer stores through a per-tile, per-column buffer resource whose
+// range is the tile's quads, so every lane of the wave issues the same store instructions and
+// the lanes past the tile's last quad are dropped by the range check. Straight-line stores keep
+// the compiler's vmcnt bookkeeping exact: a branch that might skip a tile's stores would make
+// every later wait for an older load wait for those stores too (vmcnt is in order).
+constexpr int BUF_NT = 2;  // gfx94x/gfx950 cache-policy bit 1: non-temporal
+__device__ __forceinline__ void tile_store(uint32_t* base, uint32_t nq, uint32_t lane, uint4 v) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const i32x4 rsrc = {(int32_t)(uint32_t)a, (int32_t)(uint32_t)(a >> 32), (int32_t)(nq * 16u), 0x00020000};
+  b2f_raw_buffer_store_v4(i32x4{(int32_t)v.x, (int32_t)v.y, (int32_t)v.z, (int32_t)v.w}, rsrc,
+                      (int)(16 * lane), 0, BUF_NT);
+}
+
+// One column of this lane's quad: the test-only injection, then staged (wave LDS) or stored
+// (16-byte non-temporal store; column 10 = the fixed column).
+template <int MODE>
+__device__ __forceinline__ void emit(uint32_t* S, int col, uint32_t lane, uint64_t qrow, uint32_t v0,
+                                     uint32_t v1, uint32_t v2, uint32_t v3, uint32_t* adv,
+                                     uint32_t* fixed, uint64_t total_rows, const Inject& inj,
+                                     bool stage) {
+  if (MODE & FZ_INJECT) {
+    if ((inj.row >> 2) == (qrow >> 2) && inj.col == (uint32_t)col) {
+      const uint32_t j = (uint32_t)inj.row & 3u;
+      v0 ^= j == 0 ? inj.mask : 0u;
+      v1 ^= j == 1 ? inj.mask : 0u;
+      v2 ^= j == 2 ? inj.mask : 0u;
+      v3 ^= j == 3 ? inj.mask : 0u;
+    }
+  }
+  *reinterpret_cast<uint4*>(S + col * STR + 4 * lane) = make_uint4(v0, v1, v2, v3);
+}
+
+// Wait for the next tile's operand words here, before this tile's stores are issued: they were
+// loaded at the top of the iteration, and the only older vector memory operations still in
+// flight are the previous tile's stores, issued a whole tile ago. Waited on later (at their
+// first use in the next iteration) they would also wait for this tile's stores (vmcnt is in
+// order, and the compiler cannot count stores across the tile kinds' branches).
+__device__ __forceinline__ void settle(const Ops& P) {
+  asm volatile("" ::"v"(P.w[0]), "v"(P.w[1]), "v"(P.w[2]), "v"(P.w[3]), "v"(P.w[4]), "v"(P.w[5]),
+               "v"(P.w[6]));
+}
+
+// The staged tile to HBM (every lane; see tile_store). Issued only after every use of the
+// loaded operand words: a use after a store would wait for the store (vmcnt is in order).
+template <int MODE>
+__device__ __forceinline__ void store_staged(const uint32_t* S, uint32_t lane, uint32_t nq, uint64_t row0,
+                                             uint32_t* adv, uint32_t* fixed, uint64_t total_rows) {
+  if (!(MODE & FZ_STORE)) return;
+  const uint32_t l = lane < nq ? lane : 0;
+#pragma unroll
+  for (int col = 0; col < NSTAGE; col++)
+    tile_store((col < 10 ? adv + (uint64_t)col * total_rows : fixed) + row0, nq, lane,
+               *reinterpret_cast<const uint4*>(S + col * STR + 4 * l));
+}
+
+// A round quad (position p of its G), column by column: the fill's quad_round (LAYOUT.md §4
+// blocks ADD3/ADD2/XOR/XOR24/XOR63 from one recipe), each column emitted as soon as it is
+// known so the quad's 44 cells are never all live at once.
+template <int MODE>
+__device__ __forceinline__ void emit_round_quad(uint32_t* S, uint32_t lane, uint64_t qrow,
+                                                uint64_t a, uint64_t b, uint64_t c, uint64_t d,
+                                                uint64_t mx, uint64_t my, uint32_t p,
+                                                const uint32_t* __restrict__ rows, uint32_t* adv,
+                                                uint32_t* fixed, uint64_t total_rows,
+                                                const Inject& inj) {
+  const uint64_t a1 = a + b + mx;
+  const uint64_t d1 = rotr64(d ^ a1, 32);
+  const uint64_t c1 = c + d1;
+  const uint64_t b1 = rotr64(b ^ c1, 24);
+  const uint64_t a2 = a1 + b1 + my;
+  const uint64_t d2 = rotr64(d1 ^ a2, 16);
+  const uint64_t c2 = c1 + d2;
+  const uint32_t st = step_of_quad(p);
+  const uint64_t X = st == 0 ? a : st == 1 ? d : st == 2 ? c : st == 3 ? b
+                   : st == 4 ? a1 : st == 5 ? d1 : st == 6 ? c1 : b1;
+  const uint64_t Y = st == 0 ? b : st == 1 ? a1 : st == 2 ? d1 : st == 3 ? c1
+                   : st == 4 ? b1 : st == 5 ? a2 : st == 6 ? d2 : c2;
+  const uint64_t M = st == 0 ? mx : st == 4 ? my : 0ull;
+  const uint64_t s1 = X + Y, Sm = s1 + M;
+  const uint32_t carry = (uint32_t)(s1 < X) + (uint32_t)(Sm < s1);
+  const uint64_t Z = X ^ Y, O = X & Y;
+  const uint64_t Wd = st == 3 ? rotr64(Z, 24) : rotr64(Z, 63);
+  const uint4 e = *reinterpret_cast<const uint4*>(rows + 4 * p);
+  const uint32_t sd = rows[4 * G_QUADS + p];
+  uint32_t v[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t ej = comp(e, j);
+    const uint32_t srcw = (ej >> 2) & 3u, mcode = (ej >> 5) & 3u;
+    const uint64_t V = srcw == 0 ? Sm : srcw == 1 ? Z : O;
+    v[j] = (uint32_t)(V >> (16 * (ej & 3u) + 8 * ((ej >> 4) & 1u))) &
+           (mcode == 0 ? 0xffffu : mcode == 1 ? 0xffu : 0x7fffu);
+  }
+  emit<MODE>(S, A0, lane, qrow, tag16(v[0]), tag16(v[1]), tag16(v[2]), tag16(v[3]), adv, fixed, total_rows, inj, true);
+  emit<MODE>(S, A1, lane, qrow, v[0], v[1], v[2], v[3], adv, fixed, total_rows, inj, true);
+  emit<MODE>(S, A2, lane, qrow, spread16(v[0]), spread16(v[1]), spread16(v[2]), spread16(v[3]), adv, fixed, total_rows, inj, true);
+  // operand slots A and B (at most two rows of a quad hold spread operand limbs)
+  const uint32_t jA = sd & 3u, shA = 16 * ((sd >> 2) & 3u), jB = (sd >> 5) & 3u, shB = 16 * ((sd >> 7) & 3u);
+  const bool vA = (sd >> 4) & 1u, vB = (sd >> 9) & 1u, has_w = (sd >> 10) & 1u, has_z = (sd >> 11) & 1u;
+  const bool dense = (sd >> 12) & 1u, has_m = (sd >> 13) & 1u;
+  auto slot = [&](uint64_t Wv, int j, uint32_t fA, uint32_t fB) -> uint32_t {
+    (void)Wv;
+    return (vA && jA == (uint32_t)j) ? fA : (vB && jB == (uint32_t)j) ? fB : 0u;
+  };
+  {
+    const uint32_t sA = spread16((uint32_t)(X >> shA) & 0xffffu), sB = spread16((uint32_t)(X >> shB) & 0xffffu);
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) o[j] = dense ? (uint32_t)(X >> (16 * j)) & 0xffffu : slot(X, j, sA, sB);
+    emit<MODE>(S, A3, lane, qrow, o[0], o[1], o[2], o[3], adv, fixed, total_rows, inj, true);
+  }
+  {
+    const uint32_t sA = spread16((uint32_t)(Y >> shA) & 0xffffu), sB = spread16((uint32_t)(Y >> shB) & 0xffffu);
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) o[j] = dense ? (uint32_t)(Y >> (16 * j)) & 0xffffu : slot(Y, j, sA, sB);
+    emit<MODE>(S, A4, lane, qrow, o[0], o[1], o[2], o[3], adv, fixed, total_rows, inj, true);
+  }
+  {
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) o[j] = has_m ? (uint32_t)(M >> (16 * j)) & 0xffffu : 0u;
+    emit<MODE>(S, A5, lane, qrow, o[0], o[1], o[2], o[3], adv, fixed, total_rows, inj, true);
+  }
+  {
+    const uint32_t zA = ((uint32_t)(Z >> shA) & 0xffffu) >> 15, zB = ((uint32_t)(Z >> shB) & 0xffffu) >> 15;
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) o[j] = has_z ? slot(Z, j, zA, zB) : 0u;
+    emit<MODE>(S, A6, lane, qrow, o[0], o[1], o[2], o[3], adv, fixed, total_rows, inj, true);
+  }
+  {
+    const uint32_t wA = (uint32_t)(Wd >> shA) & 0xffffu, wB = (uint32_t)(Wd >> shB) & 0xffffu;
+    uint32_t o[4], q[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      o[j] = has_w ? slot(Wd, j, wA, wB) : 0u;
+      q[j] = has_w ? slot(Wd, j, spread16(wA), spread16(wB)) : 0u;
+    }
+    emit<MODE>(S, A7, lane, qrow, o[0], o[1], o[2], o[3], adv, fixed, total_rows, inj, true);
+    emit<MODE>(S, A8, lane, qrow, q[0], q[1], q[2], q[3], adv, fixed, total_rows, inj, true);
+  }
+  emit<MODE>(S, A9, lane, qrow, (e.x >> 12) & 1u ? carry : 0u, (e.y >> 12) & 1u ? carry : 0u,
+             (e.z >> 12) & 1u ? carry : 0u, (e.w >> 12) & 1u ? carry : 0u, adv, fixed, total_rows, inj, true);
+  emit<MODE>(S, FXC, lane, qrow, e.x >> 16, e.y >> 16, e.z >> 16, e.w >> 16, adv, fixed, total_rows, inj, true);
+}
+
+// A built quad (init / final / zero rows): every column emitted.
+template <int MODE>
+__device__ __forceinline__ void emit_quad(uint32_t* S, uint32_t lane, uint64_t qrow, const Quad& Q,
+                                          uint32_t* adv, uint32_t* fixed, uint64_t total_rows,
+                                          const Inject& inj, bool stage) {
+#pragma unroll
+  for (int cc = 0; cc < 10; cc++)
+    emit<MODE>(S, cc, lane, qrow, Q.c[cc][0], Q.c[cc][1], Q.c[cc][2], Q.c[cc][3], adv, fixed, total_rows, inj, stage);
+  emit<MODE>(S, FXC, lane, qrow, Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3], adv, fixed, total_rows, inj, stage);
+}
+
+// Lookups on the quad's four rows.
+__device__ __forceinline__ void check_lookups(EvalAcc& A, uint4 q0, uint4 q1, uint4 q2, uint64_t qrow) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t tg = comp(q0, j), de = comp(q1, j), sp = comp(q2, j);
+    if (!(de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu))) A.fail(qrow + j, B2F_CODE_LOOKUP);
+  }
+}
+
+// The quad's fixed cells against the keygen structure.
+__device__ __forceinline__ void check_fixed(EvalAcc& A, uint4 fx, uint4 xf, uint64_t qrow) {
+  if ((fx.x ^ xf.x) | (fx.y ^ xf.y) | (fx.z ^ xf.z) | (fx.w ^ xf.w)) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (comp(fx, j) != comp(xf, j)) A.fail(qrow + j, B2F_CODE_FIXED);
+  }
+}
+
+// The selector rows of a quad whose selector bits are not the keygen structure's (only a
+// corrupted fixed column, i.e. the test hook, has one): their gates -- every selector bit of
+// the row, as the eval's per-quad path evaluates them -- go to the deferred list and are
+// evaluated on the written trace after the kernel (deferred_gates_kernel).
+__device__ __forceinline__ void defer_rows(uint4 fx, uint64_t qrow, uint64_t* defer, uint32_t defer_cap) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    if (!(comp(fx, j) & 0xffffu)) continue;
+    const uint64_t slot = atomicAdd((unsigned long long*)defer, 1ull);
+    if (slot < defer_cap) defer[1 + slot] = qrow + j;
+  }
+}
 
 template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES, B2F_FUSED_WAVES)
@@ -307,8 +500,16 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
              uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
              uint32_t* __restrict__ fixed, const TileDesc* __restrict__ desc,
              b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
-             uint64_t* __restrict__ defer, uint32_t defer_cap) {
+             uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk) {
   __shared__ __attribute__((aligned(16))) uint32_t L[L_WORDS];
+  uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
+  auto tick = [&](int k) {
+    if (MODE & FZ_CLOCK) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      if (k >= 0) ck[k] += now - tp;
+      tp = now;
+    }
+  };
   const int tid = threadIdx.x;
   const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
   if (tid < 22) L[L_ACC + tid] = 0;
@@ -331,193 +532,112 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     const uint64_t t_inst = (used_rows - (uint64_t)FIXED_ROWS * n) / 208 + 2ull * n;
     const uint64_t t_all = t_inst + ((total_rows - used_rows) / 4 + PAD_Q - 1) / PAD_Q;
     const uint64_t W = (uint64_t)gridDim.x * WAVES;
-    uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
+    // wave-uniform tile index: descriptors come in by scalar loads (lgkmcnt), never queued
+    // behind the wave's vector stores
+    uint64_t t = (uint64_t)blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(wv);
 
     auto raw_desc = [&](uint64_t tt) -> uint4 {
-      return tt < t_inst ? *reinterpret_cast<const uint4*>(desc + tt) : make_uint4(0, 0, 0, 0);
+      const uint64_t ti = tt < t_inst ? tt : 0;
+      const uint4 v = desc[ti].v;
+      return tt < t_inst ? v : make_uint4(0, 0, 0, 0);
     };
     // software pipeline: operands one tile ahead, descriptors two tiles ahead (every load of
     // an iteration is issued before its stores: vmcnt retires loads and stores in order)
     Ctx c = make_ctx(t, t_inst, raw_desc(t), used_rows, total_rows);
     Ops P{};
-    if (t < t_all) P = load_ops(c, lane, in, rec, Sg, IV);
+    if (t < t_all) P = load_ops(c, lane, in, rec, Sg);
     uint4 dn = raw_desc(t + W);
     for (; t < t_all; t += W) {
+      tick(-1);
       const Ctx cn = make_ctx(t + W, t_inst, dn, used_rows, total_rows);
-      Ops Pn{};
-      if (t + W < t_all) Pn = load_ops(cn, lane, in, rec, Sg, IV);
+      const Ops Pn = load_ops(cn, lane, in, rec, Sg);  // past the end: harmless loads
       dn = raw_desc(t + 2 * W);
-
-      // ---- assign this lane's quad
+      tick(0);  // next tile's context and loads issued
       const uint32_t nq = c.nq;
       const bool qlane = lane < nq;
       const uint64_t qrow = c.row0 + 4ull * lane;  // this lane's first row
-      Quad Q;
-      zero(Q);
-      uint32_t p = 0;  // quad position inside its G (half-round tiles)
-      if (c.kind == T_HR) {
-        p = lane - G_QUADS * (lane / G_QUADS);
-        quad_round(Q, P.w[0], P.w[1], P.w[2], P.w[3], P.w[4], P.w[5], p, rows);
-      } else if (c.kind == T_INIT) {
-        QuadOps qo;
-        qo.w[0] = P.w[0];
-#pragma unroll
-        for (int k = 1; k < 6; k++) qo.w[k] = 0;
-        qo.lq = lane < INIT_Q ? lane : 0;
-        qo.rounds = c.rounds;
-        quad_cells_ops(Q, qo, IV);
-      } else if (c.kind == T_FINAL) {
-        q_xor3(Q, P.w[0], P.w[1], P.w[2], lane & 1u);
-      }
-      if (!qlane) zero(Q);
-      if (MODE & FZ_INJECT) {
-        if (qlane && (inj.row >> 2) == (qrow >> 2)) {
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            if ((uint32_t)j != (uint32_t)(inj.row & 3)) continue;
-#pragma unroll
-            for (int cc = 0; cc < 10; cc++)
-              if ((uint32_t)cc == inj.col) Q.c[cc][j] ^= inj.mask;
-            if (inj.col == 10) Q.fx[j] ^= inj.mask;
-          }
-        }
-      }
-      // producer lanes: the outputs (a2, b2, c2, d2) of their G, or the initial words
-      const uint32_t npq = c.kind == T_HR ? HR_Q : FINAL_Q;
-      if ((c.kind == T_HR || c.kind == T_FINAL) && lane >= npq && lane < npq + 4) {
-        const uint32_t gg = lane - npq;
-        const bool first = c.kind == T_HR ? c.hr == 0 : c.rounds == 0;
-        const uint32_t hp = c.kind == T_HR ? c.hr - 1 : 2 * c.rounds - 1;
-        const uint32_t g = first ? gg : gg + 4 * (hp & 1u);
-        uint64_t o0 = P.w[0], o1 = P.w[1], o2 = P.w[2], o3 = P.w[3];
-        if (!first) {
-          const uint64_t a1 = P.w[0] + P.w[1] + P.w[4];
-          const uint64_t d1 = rotr64(P.w[3] ^ a1, 32);
-          const uint64_t c1 = P.w[2] + d1;
-          const uint64_t b1 = rotr64(P.w[1] ^ c1, 24);
-          o0 = a1 + b1 + P.w[5];
-          o3 = rotr64(d1 ^ o0, 16);
-          o2 = c1 + o3;
-          o1 = rotr64(b1 ^ o2, 63);
-        }
-        const uint32_t gi = gidx_word(g);
-        prod[gi & 15u] = o0;
-        prod[(gi >> 8) & 15u] = o1;
-        prod[(gi >> 16) & 15u] = o2;
-        prod[(gi >> 24) & 15u] = o3;
-      }
-      // ---- stage (every tile kind but the zero tail), then store
-      const bool staged = c.kind != T_PAD;
-      bool canon = false;
-      if (staged && qlane) {
-#pragma unroll
-        for (int cc = 0; cc < NSTAGE; cc++)
-          *reinterpret_cast<uint4*>(S + cc * STR + 4 * lane) = make_uint4(Q.c[cc][0], Q.c[cc][1], Q.c[cc][2], Q.c[cc][3]);
-        if (c.kind == T_HR) {
-          canon = (Q.fx[0] & 0xffffu) == expected_sel(p) && ((Q.fx[1] | Q.fx[2] | Q.fx[3]) & 0xffffu) == 0;
-          S[S_CANON + lane] = canon ? 1u : 0u;
-          S[S_A9 + lane] = Q.c[A9][0];
-        }
-      }
-      if ((MODE & FZ_STORE) && qlane) {
-#pragma unroll
-        for (int cc = 0; cc < 11; cc++) {
-          const u32x4 v = cc < 10 ? u32x4{Q.c[cc][0], Q.c[cc][1], Q.c[cc][2], Q.c[cc][3]}
-                                  : u32x4{Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]};
-          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>((cc < 10 ? adv + (uint64_t)cc * total_rows : fixed) + qrow));
-        }
-      }
-      // the wave's LDS writes are complete and ordered before its reads below
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
 
-      // ---- lookups and the fixed column of this lane's quad
-      if (qlane) {
-        uint4 q0, q1, q2;
-        if (staged) {
-          q0 = T.quad(A0, 4 * lane);
-          q1 = T.quad(A1, 4 * lane);
-          q2 = T.quad(A2, 4 * lane);
-        } else {
-          q0 = make_uint4(Q.c[A0][0], Q.c[A0][1], Q.c[A0][2], Q.c[A0][3]);
-          q1 = make_uint4(Q.c[A1][0], Q.c[A1][1], Q.c[A1][2], Q.c[A1][3]);
-          q2 = make_uint4(Q.c[A2][0], Q.c[A2][1], Q.c[A2][2], Q.c[A2][3]);
+      if (c.kind == T_HR) {
+        // ---- a half-round: 4 G's, lane = quad; lanes 52..55 the previous half-round's G's
+        const uint32_t gg = lane / G_QUADS, p = lane - G_QUADS * gg;
+        if (lane >= HR_Q && lane < HR_Q + 4) producer_words(prod, P, lane - HR_Q, c.hr == 0, c.hr - 1, IV);
+        tick(1);  // producers
+        if (qlane)
+          emit_round_quad<MODE>(S, lane, qrow, P.w[0], P.w[1], P.w[2], P.w[3], P.w[4], P.w[5], p, rows,
+                                adv, fixed, total_rows, inj);
+        tick(2);  // cells computed and staged
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staging is complete
+        __builtin_amdgcn_wave_barrier();
+        if ((MODE & FZ_COPIES) && lane < 32) {
+          // message words (the last use of the loaded operands, so before the stores): a1 (x)
+          // at +0 and a2 (y) at +28 of every G
+          const uint32_t mg = lane >> 3, which = (lane >> 2) & 1u, k = lane & 3u;
+          const uint32_t dr = 52 * mg + (which ? 28u : 0u) + k;
+          uint32_t sv = limb(P.w[6], k);
+          if (MODE & FZ_INJECT) {
+            const uint32_t g = mg + 4 * (c.hr & 1u);
+            const uint32_t mj = Sg[16 * ((c.hr >> 1) % 10) + 2 * g + which];
+            sv ^= inj_at(inj, c.off + 32 + 4 * mj + k, A1);
+          }
+          if (T.at(A5, dr) != sv) A.fail(c.row0 + dr, B2F_CODE_COPY);
         }
-        if (MODE & FZ_LOOKUP) {
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const uint32_t tg = comp(q0, j), de = comp(q1, j), sp = comp(q2, j);
-            if (!(de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu)))
-              A.fail(qrow + j, B2F_CODE_LOOKUP);
+        tick(3);  // staging visible, message copies
+        settle(Pn);
+        tick(4);  // the next tile's operands arrived
+        store_staged<MODE>(S, lane, nq, c.row0, adv, fixed, total_rows);
+        tick(5);  // stores issued
+        if (qlane) {
+          const uint4 fx = T.quad(FXC, 4 * lane);
+          const bool canon = (fx.x & 0xffffu) == expected_sel(p) && ((fx.y | fx.z | fx.w) & 0xffffu) == 0;
+          if (MODE & FZ_LOOKUP) check_lookups(A, T.quad(A0, 4 * lane), T.quad(A1, 4 * lane), T.quad(A2, 4 * lane), qrow);
+          if (MODE & FZ_GATES) {
+            check_fixed(A, fx, make_uint4(expected_sel(p), 0, 0, 0), qrow);
+            if (!canon) defer_rows(fx, qrow, defer, defer_cap);
           }
         }
         if (MODE & FZ_GATES) {
-          uint4 xf = make_uint4(0, 0, 0, 0);
-          if (c.kind == T_HR) {
-            xf.x = expected_sel(p);
-          } else if (c.kind != T_PAD) {
-            const QuadInfo d = decode_quad((uint32_t)((qrow - c.off) >> 2), c.rounds);
-            xf = fixed_of_quad(d, d.kind == K_CONST ? IV[d.a & 7u] : 0ull);
+          // canonical blocks, one kind per pass so each pass is one evaluator: the adds
+          // (lanes 0-15: a1 +0, c1 +12, a2 +28, c2 +40 of G lane / 4), the XORs (lanes 0-7:
+          // d1 +4, d2 +32 of G lane / 2), XOR24 limbs (lanes 0-15: b1 + efgh at +16, limb
+          // lane % 4, OR-combined over the DPP quad) and XOR63 limbs (b2 + ijkl at +44)
+          const uint32_t w4 = lane & 3u;
+          auto canon_block = [&](uint32_t r, uint32_t want) {
+            const uint4 bf = T.quad(FXC, r);  // the block's first quad
+            return (bf.x & 0xffffu) == want && ((bf.y | bf.z | bf.w) & 0xffffu) == 0;
+          };
+          if (lane < 16) {
+            const uint32_t r = 52 * (lane >> 2) + (w4 == 0 ? 0u : w4 == 1 ? 12u : w4 == 2 ? 28u : 40u);
+            const uint32_t want = 1u << (w4 == 0 ? S_A1 : w4 == 1 ? S_C1 : w4 == 2 ? S_A2 : S_C2);
+            if (canon_block(r, want) && !g_add(T, r, T.at(A9, r), (w4 & 1u) == 0))
+              A.fail_gates(c.row0 + r, want);
           }
-          if ((Q.fx[0] ^ xf.x) | (Q.fx[1] ^ xf.y) | (Q.fx[2] ^ xf.z) | (Q.fx[3] ^ xf.w)) {
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-              if (Q.fx[j] != comp(xf, j)) A.fail(qrow + j, B2F_CODE_FIXED);
+          __builtin_amdgcn_wave_barrier();
+          if (lane < 8) {
+            const uint32_t r = 52 * (lane >> 1) + ((lane & 1u) ? 32u : 4u);
+            const uint32_t want = 1u << ((lane & 1u) ? S_D2 : S_D1);
+            if (canon_block(r, want) && !g_xor(T, r, false)) A.fail_gates(c.row0 + r, want);
           }
-        }
-      }
-
-      // ---- gates
-      if (MODE & FZ_GATES) {
-        uint32_t bits = 0;  // XOR24 / XOR63 limb lanes (DPP quad OR below: all lanes active)
-        const uint32_t kgg = (lane < 40 ? lane - 24 : lane - 40) >> 2, kk = lane & 3u;
-        const uint32_t krow = 52 * kgg + (lane < 40 ? 16u : 44u);
-        bool ktake = false;
-        if (c.kind == T_HR) {
-          if (lane < 16) {  // adds: a1 +0, c1 +12, a2 +28, c2 +40
-            const uint32_t gg = lane >> 2, w = lane & 3u;
-            const uint32_t r = 52 * gg + (w == 0 ? 0u : w == 1 ? 12u : w == 2 ? 28u : 40u);
-            if (S[S_CANON + (r >> 2)] && !g_add(T, r, S[S_A9 + (r >> 2)], (w & 1u) == 0))
-              A.fail_gates(c.row0 + r, 1u << (w == 0 ? S_A1 : w == 1 ? S_C1 : w == 2 ? S_A2 : S_C2));
-          } else if (lane < 24) {  // XORs: d1 +4, d2 +32
-            const uint32_t gg = (lane - 16) >> 1, w = lane & 1u;
-            const uint32_t r = 52 * gg + (w ? 32u : 4u);
-            if (S[S_CANON + (r >> 2)] && !g_xor(T, r, false)) A.fail_gates(c.row0 + r, 1u << (w ? S_D2 : S_D1));
-          } else if (lane < 56) {  // XOR24 (b1 + efgh) / XOR63 (b2 + ijkl) limbs
-            ktake = S[S_CANON + (krow >> 2)] != 0;
-            if (ktake) bits = lane < 40 ? g_xor24_limb(T, krow, kk) : g_xor63_limb(T, krow, kk);
+          __builtin_amdgcn_wave_barrier();
+          {
+            const uint32_t r = 52 * ((lane >> 2) & 3u) + 16;
+            const uint32_t want = (1u << S_B1) | (1u << S_EFGH);
+            const bool take = lane < 16 && canon_block(r, want);
+            const uint32_t qb = quad_or(take ? g_xor24_limb(T, r, w4) : 0u);
+            if (take && w4 == 0 && qb)
+              A.fail_gates(c.row0 + r, ((qb & 1u) ? 1u << S_B1 : 0u) | ((qb & 2u) ? 1u << S_EFGH : 0u));
           }
-        }
-        bits = quad_or(bits);
-        if (ktake && kk == 0 && bits) {
-          const bool x24 = lane < 40;
-          A.fail_gates(c.row0 + krow, ((bits & 1u) ? 1u << (x24 ? S_B1 : S_B2) : 0u) |
-                                          ((bits & 2u) ? 1u << (x24 ? S_EFGH : S_IJKL) : 0u));
-        }
-        // every selector row the kind lanes do not take: init / final blocks, any row of a
-        // non-canonical quad (a corrupted fixed column), the zero tail
-        if (qlane && !(c.kind == T_HR && canon)) {
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const uint32_t k0 = Q.fx[j], sel = k0 & 0xffffu;
-            if (!sel) continue;
-            const uint32_t r = 4 * lane + j;
-            if (staged && r + span_of(sel) < 4 * nq) {
-              uint32_t failed;
-              if (sel == (1u << S_CONST)) failed = T.at(A1, r) == (k0 >> 16) ? 0u : sel;
-              else failed = row_gates(T, sel, r, Q.c[A9][j], k0);
-              if (failed) A.fail_gates(qrow + j, failed);
-            } else {  // the gate reads past this tile: evaluated on the written trace
-              const uint64_t slot = atomicAdd((unsigned long long*)defer, 1ull);
-              if (slot < defer_cap) defer[1 + slot] = qrow + j;
-            }
+          __builtin_amdgcn_wave_barrier();
+          {
+            const uint32_t r = 52 * ((lane >> 2) & 3u) + 44;
+            const uint32_t want = (1u << S_B2) | (1u << S_IJKL);
+            const bool take = lane < 16 && canon_block(r, want);
+            const uint32_t qb = quad_or(take ? g_xor63_limb(T, r, w4) : 0u);
+            if (take && w4 == 0 && qb)
+              A.fail_gates(c.row0 + r, ((qb & 1u) ? 1u << S_B2 : 0u) | ((qb & 2u) ? 1u << S_IJKL : 0u));
           }
         }
-      }
-
-      // ---- copies
-      if (MODE & FZ_COPIES) {
-        if (c.kind == T_HR) {
+        tick(6);  // lookups, fixed column, gates
+        if (MODE & FZ_COPIES) {
           const uint32_t* ct = L + L_CT + (c.hr & 1u) * HR_CHECKS;
 #pragma unroll
           for (int it = 0; it < HR_CHECKS / FW; it++) {
@@ -539,37 +659,41 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
             }
             if (dv != sv) A.fail(c.row0 + dr, B2F_CODE_COPY);
           }
-          if (lane < 32) {  // message words: a1 (x) at +0 and a2 (y) at +28 of every G
-            const uint32_t gg = lane >> 3, which = (lane >> 2) & 1u, k = lane & 3u;
-            const uint32_t dr = 52 * gg + (which ? 28u : 0u) + k;
-            const uint32_t dv = T.at(A5, dr);
-            uint32_t sv = limb(P.aux, k);
-            if (MODE & FZ_INJECT) {
-              const uint32_t g = gg + 4 * (c.hr & 1u);
-              const uint32_t mj = Sg[16 * ((c.hr >> 1) % 10) + 2 * g + which];
-              sv ^= inj_at(inj, c.off + 32 + 4 * mj + k, A1);
-            }
-            if (dv != sv) A.fail(c.row0 + dr, B2F_CODE_COPY);
-          }
-        } else if (c.kind == T_INIT) {
-          if (lane < 24) {  // v12 = IV4 ^ t0, v13 = IV5 ^ t1, v14 = IV6 ^ fmask
-            const uint32_t a = lane >> 3, k = (lane >> 1) & 3u, op = lane & 1u;
-            const uint32_t dr = 140 + 8 * a + 2 * k;
-            const uint32_t sr = op == 0 ? 108 + 4 * (4 + a) + k : (a < 2 ? 96 + 4 * a + k : 104 + k);
-            if (T.at(op ? A4 : A3, dr) != T.at(A2, sr)) A.fail(c.row0 + dr, B2F_CODE_COPY);
-          }
-        } else if (c.kind == T_FINAL && qlane) {  // h' = h ^ v_i ^ v_{i+8}
+        }
+      } else if (c.kind == T_INIT || c.kind == T_FINAL) {
+        // ---- the init region (h, m, t, fmask, IV, v12..v14) or the final XOR3 blocks
+        Quad Q;
+        zero(Q);
+        if (c.kind == T_INIT) {
+          QuadOps qo;
+          qo.w[0] = P.w[0];
+#pragma unroll
+          for (int k = 1; k < 6; k++) qo.w[k] = 0;
+          qo.lq = qlane ? lane : 0;
+          qo.rounds = c.rounds;
+          quad_cells_ops(Q, qo, IV);
+        } else {
+          q_xor3(Q, P.w[0], P.w[1], P.w[2], lane & 1u);
+        }
+        if (qlane) emit_quad<MODE>(S, lane, qrow, Q, adv, fixed, total_rows, inj, true);
+        if (c.kind == T_FINAL && lane >= FINAL_Q && lane < FINAL_Q + 4)  // the final state
+          producer_words(prod, P, lane - FINAL_Q, c.rounds == 0, 2 * c.rounds - 1, IV);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if ((MODE & FZ_COPIES) && c.kind == T_FINAL && qlane) {
+          // h' = h ^ v_i ^ v_{i+8}: sources h (INW, the loaded word: before the stores) and the
+          // final state words
           const uint32_t a = lane >> 1;
 #pragma unroll
           for (int kk2 = 0; kk2 < 2; kk2++) {
             const uint32_t k = 2 * (lane & 1u) + kk2, dr = 8 * a + 2 * k;
-            uint32_t cv = 0, cu = 0;
-            const uint32_t vs = state_src(a, k, 1, 2 * c.rounds, cv);
-            const uint32_t us = state_src(a + 8, k, 1, 2 * c.rounds, cu);
             uint32_t sh = spread16(limb(P.w[0], k));
             uint32_t sv = spread16(limb(prod[a], k));
             uint32_t su = spread16(limb(prod[a + 8], k));
             if (MODE & FZ_INJECT) {
+              uint32_t cv = 0, cu = 0;
+              const uint32_t vs = state_src(a, k, 1, 2 * c.rounds, cv);
+              const uint32_t us = state_src(a + 8, k, 1, 2 * c.rounds, cu);
               sh ^= inj_at(inj, c.off + 4 * a + k, A2);
               sv ^= inj_at(inj, c.off + vs, cv);
               su ^= inj_at(inj, c.off + us, cu);
@@ -579,13 +703,102 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
             if (T.at(A5, dr) != su) A.fail(c.row0 + dr, B2F_CODE_COPY);
           }
         }
+        settle(Pn);
+        store_staged<MODE>(S, lane, nq, c.row0, adv, fixed, total_rows);
+        if (qlane) {
+          const uint4 fx = T.quad(FXC, 4 * lane);
+          if (MODE & FZ_LOOKUP) check_lookups(A, T.quad(A0, 4 * lane), T.quad(A1, 4 * lane), T.quad(A2, 4 * lane), qrow);
+          if (MODE & FZ_GATES) {
+            const QuadInfo d = decode_quad((uint32_t)((qrow - c.off) >> 2), c.rounds);
+            const uint4 xf = fixed_of_quad(d, d.kind == K_CONST ? IV[d.a & 7u] : 0ull);
+            check_fixed(A, fx, xf, qrow);
+            const bool canon = ((fx.x ^ xf.x) & 0xffffu) == 0 && ((fx.y ^ xf.y) & 0xffffu) == 0 &&
+                               ((fx.z ^ xf.z) & 0xffffu) == 0 && ((fx.w ^ xf.w) & 0xffffu) == 0;
+            S[S_CANON + lane] = canon ? 1u : 0u;
+            if (!canon) defer_rows(fx, qrow, defer, defer_cap);
+          }
+        }
+        if (MODE & FZ_GATES) {
+          // the canonical init / final blocks, one kind per pass (LAYOUT.md §5 row map)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+          const uint32_t* cq = S + S_CANON;
+          if (c.kind == T_INIT) {
+            if (lane < 26 && cq[lane] && !gate_ok(T, S_ABCD, 4 * lane, 0u, 0u))  // h, m, t words
+              A.fail_gates(c.row0 + 4 * lane, 1u << S_ABCD);
+            if (lane == 26 && cq[26] && !gate_ok(T, S_FMASK, 104, 0u, 0u))
+              A.fail_gates(c.row0 + 104, 1u << S_FMASK);
+            if (lane < 32 && cq[27 + (lane >> 2)]) {  // IV limbs: a_1 = k_0 on every CONST row
+              const uint32_t r = 108 + lane;
+              if (T.at(A1, r) != (T.at(FXC, r) >> 16)) A.fail_gates(c.row0 + r, 1u << S_CONST);
+            }
+            if (lane < 3 && cq[35 + 2 * lane] && !g_xor(T, 140 + 8 * lane, false))  // v12..v14
+              A.fail_gates(c.row0 + 140 + 8 * lane, 1u << S_XOR);
+          } else if (lane < 8 && cq[2 * lane]) {  // h'_i: XOR3 + digest
+            const uint32_t r = 8 * lane;
+            const uint32_t f = (g_xor(T, r, true) ? 0u : 1u << S_XOR3) | (g_digest(T, r) ? 0u : 1u << S_DIGEST);
+            if (f) A.fail_gates(c.row0 + r, f);
+          }
+        }
+        if (MODE & FZ_COPIES) {
+          if (c.kind == T_INIT) {
+            if (lane < 24) {  // v12 = IV4 ^ t0, v13 = IV5 ^ t1, v14 = IV6 ^ fmask
+              const uint32_t a = lane >> 3, k = (lane >> 1) & 3u, op = lane & 1u;
+              const uint32_t dr = 140 + 8 * a + 2 * k;
+              const uint32_t sr = op == 0 ? 108 + 4 * (4 + a) + k : (a < 2 ? 96 + 4 * a + k : 104 + k);
+              if (T.at(op ? A4 : A3, dr) != T.at(A2, sr)) A.fail(c.row0 + dr, B2F_CODE_COPY);
+            }
+          }
+        }
+      } else {
+        // ---- the zero rows past the last instance: written and checked from registers (a
+        // selector here can only come from the test hook, and its gate is deferred)
+        Quad Q;
+        zero(Q);
+        if (MODE & FZ_INJECT) {
+          if ((inj.row >> 2) == (qrow >> 2)) {
+            const uint32_t j = (uint32_t)inj.row & 3u;
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+#pragma unroll
+              for (int cc = 0; cc < 10; cc++)
+                if ((uint32_t)cc == inj.col && (uint32_t)jj == j) Q.c[cc][jj] ^= inj.mask;
+              if (inj.col == 10 && (uint32_t)jj == j) Q.fx[jj] ^= inj.mask;
+            }
+          }
+        }
+        settle(Pn);
+        if (MODE & FZ_STORE) {
+#pragma unroll
+          for (int cc = 0; cc < 11; cc++)
+            tile_store((cc < 10 ? adv + (uint64_t)cc * total_rows : fixed) + c.row0, nq, lane,
+                       cc < 10 ? make_uint4(Q.c[cc][0], Q.c[cc][1], Q.c[cc][2], Q.c[cc][3])
+                               : make_uint4(Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]));
+        }
+        if (qlane) {
+          const uint4 fx = make_uint4(Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]);
+          if (MODE & FZ_LOOKUP)
+            check_lookups(A, make_uint4(Q.c[A0][0], Q.c[A0][1], Q.c[A0][2], Q.c[A0][3]),
+                          make_uint4(Q.c[A1][0], Q.c[A1][1], Q.c[A1][2], Q.c[A1][3]),
+                          make_uint4(Q.c[A2][0], Q.c[A2][1], Q.c[A2][2], Q.c[A2][3]), qrow);
+          if (MODE & FZ_GATES) {
+            check_fixed(A, fx, make_uint4(0, 0, 0, 0), qrow);
+            defer_rows(fx, qrow, defer, defer_cap);
+          }
+        }
       }
-      // the staging is rewritten by the next tile: its reads above must be done first
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the staging is rewritten by the next tile: keep the compiler from hoisting those writes
+      // above this tile's reads (the wave's LDS operations execute in order)
+      asm volatile("" ::: "memory");
       __builtin_amdgcn_wave_barrier();
+      tick(7);  // copies (and init / final / tail tiles, whole)
       c = cn;
       P = Pn;
     }
+  }
+  if ((MODE & FZ_CLOCK) && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) atomicAdd(&clk[8 * wv + k], (unsigned long long)ck[k]);
   }
   __syncthreads();
   flush_report(A, rep, tid);
@@ -601,12 +814,7 @@ __global__ void tile_desc_kernel(const uint64_t* __restrict__ off, const b2f_inp
   const uint64_t st = 2 * ((off[i] - (uint64_t)FIXED_ROWS * i) / ROUND_ROWS) + i;
   const uint64_t t0 = st + i;
   for (uint32_t j = 0; j <= 2 * rounds + 1; j++) {
-    TileDesc d;
-    d.inst = i;
-    d.j = j;
-    d.rounds = rounds;
-    d.st = (uint32_t)st;
-    desc[t0 + j] = d;
+    desc[t0 + j].v = make_uint4(i, j, rounds, (uint32_t)st);
   }
 }
 
@@ -654,7 +862,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                             uint32_t* d_fixed, void* scratch, uint64_t tiles,
                             b2f_eval_report* d_rep, const int* d_status, uint64_t inj_row,
                             uint32_t inj_col, uint32_t inj_mask, int mode, int cu_count,
-                            hipStream_t s) {
+                            unsigned long long* clk, hipStream_t s) {
   TileDesc* desc = reinterpret_cast<TileDesc*>(scratch);
   uint64_t* defer = reinterpret_cast<uint64_t*>(desc + tiles);
   hipError_t e = hipMemsetAsync(defer, 0, 8, s);
@@ -683,10 +891,11 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   case M:                                                                                     \
     hipLaunchKernelGGL(fused_kernel<M>, dim3(grid), dim3(FW * WAVES), 0, s, d_in, n, d_off,   \
                        total_rows, rec, d_adv, d_fixed, desc, d_rep, d_status, inj, defer,    \
-                       DEFER_CAP);                                                            \
+                       DEFER_CAP, clk);                                                       \
     break;
 #ifdef B2F_DIAG
     B2F_FUSED(0) B2F_FUSED(2) B2F_FUSED(3) B2F_FUSED(10) B2F_FUSED(18) B2F_FUSED(8) B2F_FUSED(16)
+    B2F_FUSED(FZ_FULL | FZ_CLOCK) B2F_FUSED(2 | FZ_CLOCK) B2F_FUSED(0 | FZ_CLOCK)
 #endif
     B2F_FUSED(FZ_FULL | FZ_INJECT)
     default: B2F_FUSED(FZ_FULL)

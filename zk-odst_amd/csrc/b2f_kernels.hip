@@ -48,7 +48,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                             uint32_t* d_fixed, void* scratch, uint64_t tiles,
                             b2f_eval_report* d_rep, const int* d_status, uint64_t inj_row,
                             uint32_t inj_col, uint32_t inj_mask, int mode, int cu_count,
-                            hipStream_t s);  // b2f_fused.hip
+                            unsigned long long* clk, hipStream_t s);  // b2f_fused.hip
 }
 
 namespace {
@@ -778,8 +778,8 @@ int diag_mode(const char* var, int full) {
 // (0, 2, 3, 10, 18, 8, 16, 34, 66, 98) are accepted; anything else runs the product kernel.
 int fused_mode() {
   const int m = diag_mode("B2F_DIAG_FUSED", 27);
-  const bool safe = m == 27 || m == (27 | 128) ||
-                    ((m & ~(1 | 2 | 8 | 16 | 32 | 64)) == 0 && ((m & (32 | 64)) == 0 || (m & 25) == 0));
+  const bool safe = m == 27 || m == (27 | 128) || m == 130 || m == 128 ||
+                    ((m & ~(1 | 2 | 8 | 16)) == 0);
   return safe ? m : 27;
 }
 #else
@@ -1074,11 +1074,16 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
     HIPCHK(ctx, hipMalloc(&ctx->d_fz, need));
     ctx->fz_cap = need;
   }
+  const int fmode = fused_mode();
+  if ((fmode & 128) && !ctx->d_clock) {
+    HIPCHK(ctx, hipMalloc(&ctx->d_clock, 32 * sizeof(unsigned long long)));
+    HIPCHK(ctx, hipMemset(ctx->d_clock, 0, 32 * sizeof(unsigned long long)));
+  }
   const int tk = timed_begin(ctx, B2F_KERNEL_FILL_EVAL, s);
   HIPCHK(ctx, launch_fill_eval(d_in, (uint32_t)n, d_offsets, total_rows, ctx->d_rec, d_advice,
                                d_fixed, ctx->d_fz, tiles, d_report, ctx->d_status,
-                               ctx->inj_row, ctx->inj_col, ctx->inj_mask, fused_mode(),
-                               ctx->cu_count, s));
+                               ctx->inj_row, ctx->inj_col, ctx->inj_mask, fmode,
+                               ctx->cu_count, ctx->d_clock, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
