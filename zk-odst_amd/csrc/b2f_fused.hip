@@ -494,6 +494,109 @@ __device__ __forceinline__ void defer_rows(uint4 fx, uint64_t qrow, uint64_t* de
   }
 }
 
+// An init or final tile, whole (about 4 % of the quads). The caller has settled the next
+// tile's loads, so the stores here wait for nothing.
+template <int MODE>
+__device__ __forceinline__ void edge_tile(uint32_t* S, uint32_t* accw, const uint64_t* IV, const Inject inj,
+                                       uint32_t* adv, uint32_t* fixed, uint64_t total_rows,
+                                       uint64_t* defer, uint32_t defer_cap, const Ctx c, const Ops P,
+                                       uint32_t lane) {
+  EvalAcc A{accw};
+  const WaveTile T{S};
+  uint64_t* prod = reinterpret_cast<uint64_t*>(S + S_PROD);
+  const uint32_t nq = c.nq;
+  const bool qlane = lane < nq;
+  const uint64_t qrow = c.row0 + 4ull * lane;
+    // ---- the init region (h, m, t, fmask, IV, v12..v14) or the final XOR3 blocks
+    Quad Q;
+    zero(Q);
+    if (c.kind == T_INIT) {
+      QuadOps qo;
+      qo.w[0] = P.w[0];
+#pragma unroll
+      for (int k = 1; k < 6; k++) qo.w[k] = 0;
+      qo.lq = qlane ? lane : 0;
+      qo.rounds = c.rounds;
+      quad_cells_ops(Q, qo, IV);
+    } else {
+      q_xor3(Q, P.w[0], P.w[1], P.w[2], lane & 1u);
+    }
+    if (qlane) emit_quad<MODE>(S, lane, qrow, Q, adv, fixed, total_rows, inj, true);
+    if (c.kind == T_FINAL && lane >= FINAL_Q && lane < FINAL_Q + 4)  // the final state
+      producer_words(prod, P, lane - FINAL_Q, c.rounds == 0, 2 * c.rounds - 1, IV);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if ((MODE & FZ_COPIES) && c.kind == T_FINAL && qlane) {
+      // h' = h ^ v_i ^ v_{i+8}: sources h (INW, the loaded word: before the stores) and the
+      // final state words
+      const uint32_t a = lane >> 1;
+#pragma unroll
+      for (int kk2 = 0; kk2 < 2; kk2++) {
+        const uint32_t k = 2 * (lane & 1u) + kk2, dr = 8 * a + 2 * k;
+        uint32_t sh = spread16(limb(P.w[0], k));
+        uint32_t sv = spread16(limb(prod[a], k));
+        uint32_t su = spread16(limb(prod[a + 8], k));
+        if (MODE & FZ_INJECT) {
+          uint32_t cv = 0, cu = 0;
+          const uint32_t vs = state_src(a, k, 1, 2 * c.rounds, cv);
+          const uint32_t us = state_src(a + 8, k, 1, 2 * c.rounds, cu);
+          sh ^= inj_at(inj, c.off + 4 * a + k, A2);
+          sv ^= inj_at(inj, c.off + vs, cv);
+          su ^= inj_at(inj, c.off + us, cu);
+        }
+        if (T.at(A3, dr) != sh) A.fail(c.row0 + dr, B2F_CODE_COPY);
+        if (T.at(A4, dr) != sv) A.fail(c.row0 + dr, B2F_CODE_COPY);
+        if (T.at(A5, dr) != su) A.fail(c.row0 + dr, B2F_CODE_COPY);
+      }
+    }
+    store_staged<MODE>(S, lane, nq, c.row0, adv, fixed, total_rows);
+    if (qlane) {
+      const uint4 fx = T.quad(FXC, 4 * lane);
+      if (MODE & FZ_LOOKUP) check_lookups(A, T.quad(A0, 4 * lane), T.quad(A1, 4 * lane), T.quad(A2, 4 * lane), qrow);
+      if (MODE & FZ_GATES) {
+        const QuadInfo d = decode_quad((uint32_t)((qrow - c.off) >> 2), c.rounds);
+        const uint4 xf = fixed_of_quad(d, d.kind == K_CONST ? IV[d.a & 7u] : 0ull);
+        check_fixed(A, fx, xf, qrow);
+        const bool canon = ((fx.x ^ xf.x) & 0xffffu) == 0 && ((fx.y ^ xf.y) & 0xffffu) == 0 &&
+                           ((fx.z ^ xf.z) & 0xffffu) == 0 && ((fx.w ^ xf.w) & 0xffffu) == 0;
+        S[S_CANON + lane] = canon ? 1u : 0u;
+        if (!canon) defer_rows(fx, qrow, defer, defer_cap);
+      }
+    }
+    if (MODE & FZ_GATES) {
+      // the canonical init / final blocks, one kind per pass (LAYOUT.md §5 row map)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t* cq = S + S_CANON;
+      if (c.kind == T_INIT) {
+        if (lane < 26 && cq[lane] && !gate_ok(T, S_ABCD, 4 * lane, 0u, 0u))  // h, m, t words
+          A.fail_gates(c.row0 + 4 * lane, 1u << S_ABCD);
+        if (lane == 26 && cq[26] && !gate_ok(T, S_FMASK, 104, 0u, 0u))
+          A.fail_gates(c.row0 + 104, 1u << S_FMASK);
+        if (lane < 32 && cq[27 + (lane >> 2)]) {  // IV limbs: a_1 = k_0 on every CONST row
+          const uint32_t r = 108 + lane;
+          if (T.at(A1, r) != (T.at(FXC, r) >> 16)) A.fail_gates(c.row0 + r, 1u << S_CONST);
+        }
+        if (lane < 3 && cq[35 + 2 * lane] && !g_xor(T, 140 + 8 * lane, false))  // v12..v14
+          A.fail_gates(c.row0 + 140 + 8 * lane, 1u << S_XOR);
+      } else if (lane < 8 && cq[2 * lane]) {  // h'_i: XOR3 + digest
+        const uint32_t r = 8 * lane;
+        const uint32_t f = (g_xor(T, r, true) ? 0u : 1u << S_XOR3) | (g_digest(T, r) ? 0u : 1u << S_DIGEST);
+        if (f) A.fail_gates(c.row0 + r, f);
+      }
+    }
+    if (MODE & FZ_COPIES) {
+      if (c.kind == T_INIT) {
+        if (lane < 24) {  // v12 = IV4 ^ t0, v13 = IV5 ^ t1, v14 = IV6 ^ fmask
+          const uint32_t a = lane >> 3, k = (lane >> 1) & 3u, op = lane & 1u;
+          const uint32_t dr = 140 + 8 * a + 2 * k;
+          const uint32_t sr = op == 0 ? 108 + 4 * (4 + a) + k : (a < 2 ? 96 + 4 * a + k : 104 + k);
+          if (T.at(op ? A4 : A3, dr) != T.at(A2, sr)) A.fail(c.row0 + dr, B2F_CODE_COPY);
+        }
+      }
+    }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES, B2F_FUSED_WAVES)
 fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
@@ -661,95 +764,10 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
           }
         }
       } else if (c.kind == T_INIT || c.kind == T_FINAL) {
-        // ---- the init region (h, m, t, fmask, IV, v12..v14) or the final XOR3 blocks
-        Quad Q;
-        zero(Q);
-        if (c.kind == T_INIT) {
-          QuadOps qo;
-          qo.w[0] = P.w[0];
-#pragma unroll
-          for (int k = 1; k < 6; k++) qo.w[k] = 0;
-          qo.lq = qlane ? lane : 0;
-          qo.rounds = c.rounds;
-          quad_cells_ops(Q, qo, IV);
-        } else {
-          q_xor3(Q, P.w[0], P.w[1], P.w[2], lane & 1u);
-        }
-        if (qlane) emit_quad<MODE>(S, lane, qrow, Q, adv, fixed, total_rows, inj, true);
-        if (c.kind == T_FINAL && lane >= FINAL_Q && lane < FINAL_Q + 4)  // the final state
-          producer_words(prod, P, lane - FINAL_Q, c.rounds == 0, 2 * c.rounds - 1, IV);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        if ((MODE & FZ_COPIES) && c.kind == T_FINAL && qlane) {
-          // h' = h ^ v_i ^ v_{i+8}: sources h (INW, the loaded word: before the stores) and the
-          // final state words
-          const uint32_t a = lane >> 1;
-#pragma unroll
-          for (int kk2 = 0; kk2 < 2; kk2++) {
-            const uint32_t k = 2 * (lane & 1u) + kk2, dr = 8 * a + 2 * k;
-            uint32_t sh = spread16(limb(P.w[0], k));
-            uint32_t sv = spread16(limb(prod[a], k));
-            uint32_t su = spread16(limb(prod[a + 8], k));
-            if (MODE & FZ_INJECT) {
-              uint32_t cv = 0, cu = 0;
-              const uint32_t vs = state_src(a, k, 1, 2 * c.rounds, cv);
-              const uint32_t us = state_src(a + 8, k, 1, 2 * c.rounds, cu);
-              sh ^= inj_at(inj, c.off + 4 * a + k, A2);
-              sv ^= inj_at(inj, c.off + vs, cv);
-              su ^= inj_at(inj, c.off + us, cu);
-            }
-            if (T.at(A3, dr) != sh) A.fail(c.row0 + dr, B2F_CODE_COPY);
-            if (T.at(A4, dr) != sv) A.fail(c.row0 + dr, B2F_CODE_COPY);
-            if (T.at(A5, dr) != su) A.fail(c.row0 + dr, B2F_CODE_COPY);
-          }
-        }
         settle(Pn);
-        store_staged<MODE>(S, lane, nq, c.row0, adv, fixed, total_rows);
-        if (qlane) {
-          const uint4 fx = T.quad(FXC, 4 * lane);
-          if (MODE & FZ_LOOKUP) check_lookups(A, T.quad(A0, 4 * lane), T.quad(A1, 4 * lane), T.quad(A2, 4 * lane), qrow);
-          if (MODE & FZ_GATES) {
-            const QuadInfo d = decode_quad((uint32_t)((qrow - c.off) >> 2), c.rounds);
-            const uint4 xf = fixed_of_quad(d, d.kind == K_CONST ? IV[d.a & 7u] : 0ull);
-            check_fixed(A, fx, xf, qrow);
-            const bool canon = ((fx.x ^ xf.x) & 0xffffu) == 0 && ((fx.y ^ xf.y) & 0xffffu) == 0 &&
-                               ((fx.z ^ xf.z) & 0xffffu) == 0 && ((fx.w ^ xf.w) & 0xffffu) == 0;
-            S[S_CANON + lane] = canon ? 1u : 0u;
-            if (!canon) defer_rows(fx, qrow, defer, defer_cap);
-          }
-        }
-        if (MODE & FZ_GATES) {
-          // the canonical init / final blocks, one kind per pass (LAYOUT.md §5 row map)
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_wave_barrier();
-          const uint32_t* cq = S + S_CANON;
-          if (c.kind == T_INIT) {
-            if (lane < 26 && cq[lane] && !gate_ok(T, S_ABCD, 4 * lane, 0u, 0u))  // h, m, t words
-              A.fail_gates(c.row0 + 4 * lane, 1u << S_ABCD);
-            if (lane == 26 && cq[26] && !gate_ok(T, S_FMASK, 104, 0u, 0u))
-              A.fail_gates(c.row0 + 104, 1u << S_FMASK);
-            if (lane < 32 && cq[27 + (lane >> 2)]) {  // IV limbs: a_1 = k_0 on every CONST row
-              const uint32_t r = 108 + lane;
-              if (T.at(A1, r) != (T.at(FXC, r) >> 16)) A.fail_gates(c.row0 + r, 1u << S_CONST);
-            }
-            if (lane < 3 && cq[35 + 2 * lane] && !g_xor(T, 140 + 8 * lane, false))  // v12..v14
-              A.fail_gates(c.row0 + 140 + 8 * lane, 1u << S_XOR);
-          } else if (lane < 8 && cq[2 * lane]) {  // h'_i: XOR3 + digest
-            const uint32_t r = 8 * lane;
-            const uint32_t f = (g_xor(T, r, true) ? 0u : 1u << S_XOR3) | (g_digest(T, r) ? 0u : 1u << S_DIGEST);
-            if (f) A.fail_gates(c.row0 + r, f);
-          }
-        }
-        if (MODE & FZ_COPIES) {
-          if (c.kind == T_INIT) {
-            if (lane < 24) {  // v12 = IV4 ^ t0, v13 = IV5 ^ t1, v14 = IV6 ^ fmask
-              const uint32_t a = lane >> 3, k = (lane >> 1) & 3u, op = lane & 1u;
-              const uint32_t dr = 140 + 8 * a + 2 * k;
-              const uint32_t sr = op == 0 ? 108 + 4 * (4 + a) + k : (a < 2 ? 96 + 4 * a + k : 104 + k);
-              if (T.at(op ? A4 : A3, dr) != T.at(A2, sr)) A.fail(c.row0 + dr, B2F_CODE_COPY);
-            }
-          }
-        }
+#ifndef B2F_FZ_NOEDGE  // diagnostics: the register budget of the half-round path alone
+        edge_tile<MODE>(S, L + L_ACC, IV, inj, adv, fixed, total_rows, defer, defer_cap, c, P, lane);
+#endif
       } else {
         // ---- the zero rows past the last instance: written and checked from registers (a
         // selector here can only come from the test hook, and its gate is deferred)
