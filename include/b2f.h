@@ -194,18 +194,28 @@ B2F_API int b2f_chain_inputs_dev(b2f_ctx* ctx, const uint64_t* d_h_prev, const u
                                  const uint64_t* d_t, const uint32_t* d_f, uint32_t rounds,
                                  size_t n, b2f_input* d_out, void* stream);
 
-/* Fp export: advice cells as pallas::Base elements (pasta_curves
- * 0.5.1 Fp, p = 0x40000000000000000000000000000000224698fc094cf91b992d30ed00000001), the
- * form halo2's prover keeps its advice columns in. Rows [row_begin, row_begin + nrows) of
- * the ten advice columns are written in halo2 column order (b2f_halo2_column_index):
- * element of a_i at row row_begin + r goes to d_out[(h * out_rows + r) * 4 + limb],
- * h = b2f_halo2_column_index(i), 4 little-endian u64 limbs. out_rows >= nrows is the
- * column stride (rows past nrows are not written; a prover zero-fills to 2^k).
- *   form B2F_FP_MONTGOMERY: x * 2^256 mod p (the in-memory Fp of pasta_curves)
- *   form B2F_FP_CANONICAL:  x as a 32-byte little-endian integer (PrimeField::to_repr)
- * d_out must be 16-byte aligned. Asynchronous on `stream`. */
+/* Fp export: advice cells as elements of the prover's scalar field,
+ * the form halo2's prover keeps its advice columns in. Two fields:
+ *   pallas::Base (pasta_curves 0.5.1 Fp, halo2_proofs 0.3.0's own field),
+ *     p = 0x40000000000000000000000000000000224698fc094cf91b992d30ed00000001;
+ *   BN254 Fr (halo2curves 0.3.2 bn256::Fr, the field of the reference's circuit test and KZG
+ *     bench: blake2f.rs:283,293, blake2f_circuit_bench.rs:10,34),
+ *     r = 0x30644e72e131a029b85045b68181585d2833e84879b9709143e1f593f0000001.
+ * Rows [row_begin, row_begin + nrows) of the ten advice columns are written in halo2 column
+ * order (b2f_halo2_column_index): element of a_i at row row_begin + r goes to
+ * d_out[(h * out_rows + r) * 4 + limb], h = b2f_halo2_column_index(i), 4 little-endian u64
+ * limbs. out_rows >= nrows is the column stride (rows past nrows are not written; a prover
+ * zero-fills to 2^k). `form`:
+ *   B2F_FP_MONTGOMERY        x * 2^256 mod p (the in-memory Fp of pasta_curves)
+ *   B2F_FP_CANONICAL         x as a 32-byte little-endian integer (PrimeField::to_repr)
+ *   B2F_FP_BN254_MONTGOMERY  x * 2^256 mod r (the in-memory bn256::Fr of halo2curves)
+ *   B2F_FP_BN254_CANONICAL   x as a 32-byte little-endian integer
+ * (bit 1 selects the field, bit 0 Montgomery form). d_out must be 16-byte aligned.
+ * Asynchronous on `stream`. */
 #define B2F_FP_CANONICAL 0
 #define B2F_FP_MONTGOMERY 1
+#define B2F_FP_BN254_CANONICAL 2
+#define B2F_FP_BN254_MONTGOMERY 3
 B2F_API int b2f_export_fp_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t total_rows,
                               uint64_t row_begin, uint64_t nrows, uint32_t form,
                               uint64_t* d_out, uint64_t out_rows, void* stream);
@@ -224,7 +234,8 @@ B2F_API int b2f_export_fp_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t t
  *   j = 2  A': permuted input (ascending canonical order)           (rows < usable_rows)
  *   j = 3  S': permuted table (A'[i] == S'[i] or A'[i] == A'[i-1])  (rows < usable_rows)
  *   j = 4  z:  lookup grand product, z[0] = 1                       (rows <= usable_rows)
- * in `form` (B2F_FP_MONTGOMERY / B2F_FP_CANONICAL); out_rows >= usable_rows + 1, blinding
+ * in `form` (any B2F_FP_* form: pasta Fp or BN254 Fr, Montgomery or canonical; the
+ * challenges are canonical elements of that field); out_rows >= usable_rows + 1, blinding
  * rows are the prover's. d_first_bad[c] receives the first circuit row whose (a_0, a_1, a_2)
  * is not a table row (halo2's ConstraintSystemFailure), UINT64_MAX if none; that circuit's
  * columns are then meaningless. Asynchronous on `stream`. */

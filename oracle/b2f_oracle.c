@@ -366,11 +366,15 @@ int orc_fixed(const uint64_t* offsets, size_t n, uint64_t total_rows, uint32_t* 
 }
 
 /* ---------------------------------------------------------------- Fp export (§8(f) row 1)
- * pallas::Base of pasta_curves 0.5.1 (Cargo.lock:1334-1337): p below, in-memory Montgomery
- * form with R = 2^256. Textbook restatement: R^2 mod p by 512 modular doublings of 1,
- * n0 = -p^-1 mod 2^64 by Newton iteration, mont(x) = CIOS(x, R^2). */
-static const uint64_t FP_P[4] = {0x992d30ed00000001ull, 0x224698fc094cf91bull, 0ull,
-                                 0x4000000000000000ull};
+ * Two prime fields, both in-memory Montgomery form with R = 2^256:
+ *   pallas::Base of pasta_curves 0.5.1 (Cargo.lock:1334-1337);
+ *   BN254 Fr of halo2curves 0.3.2 (Cargo.lock:859-861; the reference's circuit field,
+ *   blake2f.rs:283,293, blake2f_circuit_bench.rs:10,34).
+ * Textbook restatement: R^2 mod p by 512 modular doublings of 1, n0 = -p^-1 mod 2^64 by
+ * Newton iteration, mont(x) = CIOS(x, R^2) with the full carry word. */
+static const uint64_t FP_MODULI[2][4] = {
+    {0x992d30ed00000001ull, 0x224698fc094cf91bull, 0ull, 0x4000000000000000ull},
+    {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull, 0x30644e72e131a029ull}};
 
 static int fp_geq(const uint64_t a[4], const uint64_t b[4]) {
     for (int i = 3; i >= 0; i--) {
@@ -388,7 +392,7 @@ static void fp_sub(uint64_t a[4], const uint64_t b[4]) {
     }
 }
 
-static void fp_consts(uint64_t r2[4], uint64_t* n0) {
+static void fp_consts(const uint64_t p[4], uint64_t r2[4], uint64_t* n0) {
     uint64_t v[4] = {1, 0, 0, 0};
     for (int k = 0; k < 512; k++) { /* v = 2v mod p; v < p < 2^255 so 2v fits */
         uint64_t c = 0;
@@ -397,16 +401,17 @@ static void fp_consts(uint64_t r2[4], uint64_t* n0) {
             v[i] = (v[i] << 1) | c;
             c = nc;
         }
-        if (fp_geq(v, FP_P)) fp_sub(v, FP_P);
+        if (fp_geq(v, p)) fp_sub(v, p);
     }
     memcpy(r2, v, sizeof v);
     uint64_t inv = 1;
-    for (int i = 0; i < 6; i++) inv *= 2 - FP_P[0] * inv;
+    for (int i = 0; i < 6; i++) inv *= 2 - p[0] * inv;
     *n0 = 0 - inv;
 }
 
 /* CIOS Montgomery product a*b*2^-256 mod p */
-static void fp_mont_mul(const uint64_t a[4], const uint64_t b[4], uint64_t n0, uint64_t out[4]) {
+static void fp_mont_mul(const uint64_t p[4], const uint64_t a[4], const uint64_t b[4], uint64_t n0,
+                        uint64_t out[4]) {
     uint64_t t[6] = {0, 0, 0, 0, 0, 0};
     for (int i = 0; i < 4; i++) {
         unsigned __int128 c = 0;
@@ -419,10 +424,10 @@ static void fp_mont_mul(const uint64_t a[4], const uint64_t b[4], uint64_t n0, u
         t[4] = (uint64_t)c;
         t[5] = (uint64_t)(c >> 64);
         uint64_t m = t[0] * n0;
-        c = (unsigned __int128)m * FP_P[0] + t[0];
+        c = (unsigned __int128)m * p[0] + t[0];
         c >>= 64;
         for (int j = 1; j < 4; j++) {
-            c += (unsigned __int128)m * FP_P[j] + t[j];
+            c += (unsigned __int128)m * p[j] + t[j];
             t[j - 1] = (uint64_t)c;
             c >>= 64;
         }
@@ -431,28 +436,32 @@ static void fp_mont_mul(const uint64_t a[4], const uint64_t b[4], uint64_t n0, u
         t[4] = t[5] + (uint64_t)(c >> 64);
     }
     uint64_t r[4] = {t[0], t[1], t[2], t[3]};
-    if (t[4] || fp_geq(r, FP_P)) fp_sub(r, FP_P);
+    if (t[4] || fp_geq(r, p)) fp_sub(r, p);
     memcpy(out, r, sizeof r);
 }
 
-void orc_fp_mont(uint32_t x, uint64_t out[4]) {
+/* field 0 = pasta Fp, 1 = BN254 Fr */
+void orc_fp_mont(uint32_t field, uint32_t x, uint64_t out[4]) {
+    const uint64_t* p = FP_MODULI[field & 1];
     uint64_t r2[4], n0;
-    fp_consts(r2, &n0);
+    fp_consts(p, r2, &n0);
     uint64_t a[4] = {x, 0, 0, 0};
-    fp_mont_mul(a, r2, n0, out);
+    fp_mont_mul(p, a, r2, n0, out);
 }
 
+/* form: bit 0 = Montgomery, bit 1 = BN254 Fr (B2F_FP_*) */
 void orc_export_fp(const uint32_t* advice, uint64_t total_rows, uint64_t row_begin,
                    uint64_t nrows, uint32_t form, uint64_t* out, uint64_t out_rows) {
     static const int a_of_h[10] = {5, 3, 4, 6, 7, 8, 9, 0, 1, 2}; /* table16.rs:281-294 */
+    const uint64_t* p = FP_MODULI[(form >> 1) & 1];
     uint64_t r2[4], n0;
-    fp_consts(r2, &n0);
+    fp_consts(p, r2, &n0);
     for (int h = 0; h < 10; h++) {
         const uint32_t* src = advice + (uint64_t)a_of_h[h] * total_rows + row_begin;
         uint64_t* dst = out + (uint64_t)h * out_rows * 4;
         for (uint64_t r = 0; r < nrows; r++) {
             uint64_t a[4] = {src[r], 0, 0, 0};
-            if (form == 1) fp_mont_mul(a, r2, n0, dst + 4 * r);
+            if (form & 1) fp_mont_mul(p, a, r2, n0, dst + 4 * r);
             else memcpy(dst + 4 * r, a, sizeof a);
         }
     }

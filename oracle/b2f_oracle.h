@@ -91,7 +91,7 @@ int orc_eval(const uint32_t* advice, const uint32_t* fixed, const uint64_t* offs
 void orc_export_fp(const uint32_t* advice, uint64_t total_rows, uint64_t row_begin,
                    uint64_t nrows, uint32_t form, uint64_t* out, uint64_t out_rows);
 /* One Montgomery conversion (the same routine), for pinning against big-integer math. */
-void orc_fp_mont(uint32_t x, uint64_t out[4]);
+void orc_fp_mont(uint32_t field, uint32_t x, uint64_t out[4]);
 
 int orc_max_threads(void);
 

@@ -20,6 +20,9 @@ pasta_curves 0.5.1 (Cargo.lock:1334-1337). Restated from their published source:
   first row of each run of equal inputs put that value into the permuted table column and
   take one from its count; give the remaining table values, in ascending order, to the
   repeated-input rows, each to the LAST row still open (`repeated_input_rows.pop()`).
+* Fields: pasta Fp (halo2_proofs' own) and BN254 Fr (halo2curves 0.3.2 bn256::Fr,
+  Cargo.lock:859-861, the reference circuit's field, blake2f.rs:283,293); `Ord` on both is
+  the order of canonical integers. Every function takes the modulus `p` (default pasta).
 * `Permuted::commit_product`: z[0] = 1, z[i + 1] = z[i] (A[i] + beta)(S[i] + gamma) /
   ((A'[i] + beta)(S'[i] + gamma)) over the usable rows, so z has usable + 1 known entries
   and z[usable] = 1 for a valid lookup.
@@ -29,6 +32,7 @@ unpinned (halo2 cannot be built here); the tests pin this restatement by the arg
 defining properties and pin the GPU path to this restatement bit for bit.
 """
 P = 0x40000000000000000000000000000000224698FC094CF91B992D30ED00000001
+P_BN254 = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
 TABLE_ROWS = 1 << 16
 
 
@@ -45,41 +49,42 @@ def tag(x):
     return 0 if x < (1 << 8) else (1 if x < (1 << 15) else 2)
 
 
-def compress(theta, t, d, s):
+def compress(theta, t, d, s, p=P):
     acc = 0
     for e in (t, d, s):
-        acc = (acc * theta + e) % P
+        acc = (acc * theta + e) % p
     return acc
 
 
-def table_values(theta):
+def table_values(theta, p=P):
     """Compressed table value of every dense x < 2^16 (the table row x)."""
-    th2 = theta * theta % P
-    return [(th2 * tag(x) + theta * x + spread(x)) % P for x in range(TABLE_ROWS)]
+    th2 = theta * theta % p
+    return [(th2 * tag(x) + theta * x + spread(x)) % p for x in range(TABLE_ROWS)]
 
 
-def batch_invert(vals):
+def batch_invert(vals, p=P):
     pre = []
     acc = 1
     for v in vals:
-        acc = acc * v % P
+        acc = acc * v % p
         pre.append(acc)
-    inv = pow(acc, P - 2, P)
+    inv = pow(acc, p - 2, p)
     out = [0] * len(vals)
     for i in range(len(vals) - 1, -1, -1):
-        out[i] = inv * (pre[i - 1] if i else 1) % P
-        inv = inv * vals[i] % P
+        out[i] = inv * (pre[i - 1] if i else 1) % p
+        inv = inv * vals[i] % p
     return out
 
 
-def columns(a0, a1, a2, usable, theta, beta, gamma):
+def columns(a0, a1, a2, usable, theta, beta, gamma, p=P):
     """The five prover columns over `usable` rows whose lookup inputs are a0/a1/a2 (sequences
     of row values, length `usable`): (A, S, A', S', z) as lists of canonical integers, z with
     usable + 1 entries. Raises ValueError at the first input row not in the table."""
     if usable < TABLE_ROWS:
         raise ValueError("usable rows %d < table size" % usable)
-    A = [compress(theta, int(a0[i]), int(a1[i]), int(a2[i])) for i in range(usable)]
-    T = table_values(theta)
+    P = p  # noqa: N806 (the field of this call)
+    A = [compress(theta, int(a0[i]), int(a1[i]), int(a2[i]), P) for i in range(usable)]
+    T = table_values(theta, P)
     S = T + [T[0]] * (usable - TABLE_ROWS)
     # permute_expression_pair
     Ap = sorted(A)
@@ -102,7 +107,7 @@ def columns(a0, a1, a2, usable, theta, beta, gamma):
     assert not repeated
     # commit_product
     den = [(Ap[i] + beta) * (Sp[i] + gamma) % P for i in range(usable)]
-    inv = batch_invert(den)
+    inv = batch_invert(den, P)
     z = [1]
     for i in range(usable):
         z.append(z[-1] * inv[i] % P * ((A[i] + beta) % P) % P * ((S[i] + gamma) % P) % P)
@@ -122,5 +127,5 @@ def to_limbs(v):
     return [(v >> (64 * k)) & 0xFFFFFFFFFFFFFFFF for k in range(4)]
 
 
-def to_mont(v):
-    return v * (1 << 256) % P
+def to_mont(v, p=P):
+    return v * (1 << 256) % p

@@ -69,7 +69,7 @@ def lib():
         L.orc_max_threads.restype = ctypes.c_int
         L.orc_export_fp.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                     ctypes.c_uint32, P, ctypes.c_uint64]
-        L.orc_fp_mont.argtypes = [ctypes.c_uint32, P]
+        L.orc_fp_mont.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P]
         L.orc_fixed.argtypes = [P, ctypes.c_size_t, ctypes.c_uint64, P]
         L.orc_fill_tampered.argtypes = [P, ctypes.c_size_t, P, ctypes.c_uint64, P, P, P,
                                         ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32,
@@ -165,7 +165,10 @@ def fixed_structure(off, total_rows=None):
     return fx
 
 
-FP_CANONICAL, FP_MONTGOMERY = 0, 1
+FP_CANONICAL, FP_MONTGOMERY, FP_BN254_CANONICAL, FP_BN254_MONTGOMERY = 0, 1, 2, 3
+PALLAS, BN254 = 0, 1
+MODULI = {PALLAS: 0x40000000000000000000000000000000224698FC094CF91B992D30ED00000001,
+          BN254: 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001}
 
 
 def export_fp(adv, row_begin=0, nrows=None, form=FP_MONTGOMERY, out_rows=None):
@@ -180,9 +183,9 @@ def export_fp(adv, row_begin=0, nrows=None, form=FP_MONTGOMERY, out_rows=None):
     return out
 
 
-def fp_mont(x):
+def fp_mont(x, field=PALLAS):
     out = np.zeros(4, dtype=np.uint64)
-    lib().orc_fp_mont(int(x), _p(out))
+    lib().orc_fp_mont(int(field), int(x), _p(out))
     return out
 
 

@@ -13,11 +13,15 @@ pytestmark = pytest.mark.gpu
 R256 = 1 << 256
 
 
-def _chal(seed):
+def _mod(form):
     import lookup as lk
 
+    return lk.P_BN254 if form & 2 else lk.P
+
+
+def _chal(seed, form=1):
     r = np.random.default_rng(seed)
-    return [int.from_bytes(r.bytes(32), "little") % lk.P for _ in range(3)]
+    return [int.from_bytes(r.bytes(32), "little") % _mod(form) for _ in range(3)]
 
 
 def _col_ints(t):
@@ -45,26 +49,29 @@ def trace(engine):
     return batch
 
 
-@pytest.mark.parametrize("form", [1, 0])
+@pytest.mark.parametrize("form", [1, 0, 3, 2])
 def test_lookup_columns_equal_oracle(engine, trace, form):
+    """Forms 0/1 pasta Fp, 2/3 BN254 Fr (the reference circuit's field)."""
     import lookup as lk
     import torch
 
     usable = (1 << 17) - 7
     total = trace.total_rows
     begins = [0, total - 20000, total - 5]
-    theta, beta, gamma = _chal(7 + form)
+    p = _mod(form)
+    theta, beta, gamma = _chal(7 + form, form)
     out, bad = trace.lookup_columns(engine, begins, usable, theta, beta, gamma, form=form)
     engine.sync(torch.cuda.current_stream().cuda_stream)
     assert (bad.cpu().numpy().view(np.uint64) == np.uint64(2**64 - 1)).all()
     adv, _ = trace.host_trace()
     for c, b in enumerate(begins):
         a = _circuit_rows(adv, total, b, usable)
-        ref = lk.columns(a[0], a[1], a[2], usable, theta, beta, gamma)
+        ref = lk.columns(a[0], a[1], a[2], usable, theta, beta, gamma, p)
+        assert ref[4][-1] == 1  # a valid lookup closes
         for j, name in enumerate(["A", "S", "A'", "S'", "z"]):
             n = usable + 1 if j == 4 else usable
             got = _col_ints(out[c, j, :n])
-            want = ref[j] if form == 0 else [v * R256 % lk.P for v in ref[j]]
+            want = ref[j] if form in (0, 2) else [v * R256 % p for v in ref[j]]
             if got != want:
                 i = next(i for i in range(n) if got[i] != want[i])
                 pytest.fail("circuit %d column %s differs first at row %d" % (c, name, i))
@@ -111,13 +118,14 @@ def test_lookup_argument_errors(engine, trace):
     out = torch.empty((1, 5, u + 1, 4), dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream().cuda_stream
 
-    def call(usable=u, theta=3, form=1, out_rows=u + 1):
+    def call(usable=u, theta=3, form=1, out_rows=u + 1):  # noqa: E306
         engine.lookup_columns_dev(trace.advice.data_ptr(), trace.total_rows, rb.data_ptr(), 1,
                                   usable, theta, 5, 7, form, out.data_ptr(), out_rows,
                                   bad.data_ptr(), s)
 
     for kw, code in [({"usable": u - 1}, b2f._lib.ERR_ROWS), ({"out_rows": u}, b2f._lib.ERR_ROWS),
-                     ({"theta": lk.P}, b2f._lib.ERR_ARG), ({"form": 2}, b2f._lib.ERR_ARG)]:
+                     ({"theta": lk.P}, b2f._lib.ERR_ARG), ({"form": 4}, b2f._lib.ERR_ARG),
+                     ({"theta": lk.P_BN254, "form": 3}, b2f._lib.ERR_ARG)]:
         with pytest.raises(b2f.B2FError) as e:
             call(**kw)
         assert e.value.code == code, kw

@@ -259,16 +259,18 @@ def test_fp_export_matches_oracle(engine, orc):
     batch.fill(engine)
     engine.sync(torch.cuda.current_stream().cuda_stream)
     adv, _ = batch.host_trace()
-    for form in (b2f.FP_CANONICAL, b2f.FP_MONTGOMERY):
+    for form in (b2f.FP_CANONICAL, b2f.FP_MONTGOMERY, b2f.FP_BN254_CANONICAL,
+                 b2f.FP_BN254_MONTGOMERY):
         got = batch.export_fp(engine, form=form).cpu().numpy().view(np.uint64)
-        assert np.array_equal(got, orc.export_fp(adv, form=form))
+        assert np.array_equal(got, orc.export_fp(adv, form=form)), form
     r0, nr = 1001, 12345
-    out = torch.full((10, nr + 7, 4), -1, dtype=torch.int64, device="cuda:0")
-    batch.export_fp(engine, row_begin=r0, nrows=nr, form=b2f.FP_MONTGOMERY, out=out)
-    got = out.cpu().numpy().view(np.uint64)
-    ref = orc.export_fp(adv, row_begin=r0, nrows=nr, form=orc.FP_MONTGOMERY)
-    assert np.array_equal(got[:, :nr], ref)
-    assert (got[:, nr:] == np.uint64(2**64 - 1)).all()  # stride padding untouched
+    for form in (b2f.FP_MONTGOMERY, b2f.FP_BN254_MONTGOMERY):
+        out = torch.full((10, nr + 7, 4), -1, dtype=torch.int64, device="cuda:0")
+        batch.export_fp(engine, row_begin=r0, nrows=nr, form=form, out=out)
+        got = out.cpu().numpy().view(np.uint64)
+        ref = orc.export_fp(adv, row_begin=r0, nrows=nr, form=form)
+        assert np.array_equal(got[:, :nr], ref)
+        assert (got[:, nr:] == np.uint64(2**64 - 1)).all()  # stride padding untouched
 
 
 def test_fp_export_edge_values(engine, orc):
@@ -284,8 +286,9 @@ def test_fp_export_edge_values(engine, orc):
     adv[:, : len(vals)] = vals
     batch = b2f.DeviceBatch(random_inputs(1, (0,), 1), device="cuda:0", total_rows=rows)
     batch.advice.copy_(torch.from_numpy(adv.view(np.int32)))
-    got = batch.export_fp(engine, form=b2f.FP_MONTGOMERY).cpu().numpy().view(np.uint64)
-    assert np.array_equal(got, orc.export_fp(adv, form=orc.FP_MONTGOMERY))
+    for form in (b2f.FP_MONTGOMERY, b2f.FP_BN254_MONTGOMERY):
+        got = batch.export_fp(engine, form=form).cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, orc.export_fp(adv, form=form)), form
     with pytest.raises(b2f.B2FError):
         batch.export_fp(engine, row_begin=rows - 4, nrows=8)
     with pytest.raises(b2f.B2FError):

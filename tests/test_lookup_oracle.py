@@ -18,23 +18,24 @@ def _rows(n, zero_frac=0.3):
     return a0, x, a2
 
 
-def _chal():
-    return [int(rng.integers(0, 2**63)) * 2**190 % lk.P + int(rng.integers(1, 2**63))
+def _chal(p=lk.P):
+    return [int(rng.integers(0, 2**63)) * 2**190 % p + int(rng.integers(1, 2**63))
             for _ in range(3)]
 
 
-@pytest.mark.parametrize("usable", [1 << 16, (1 << 16) + 777])
-def test_permutation_properties(usable):
+@pytest.mark.parametrize("usable,p", [(1 << 16, lk.P), ((1 << 16) + 777, lk.P),
+                                      ((1 << 16) + 333, lk.P_BN254)])
+def test_permutation_properties(usable, p):
     a0, a1, a2 = _rows(usable)
-    theta, beta, gamma = _chal()
-    A, S, Ap, Sp, z = lk.columns(a0, a1, a2, usable, theta, beta, gamma)
+    theta, beta, gamma = _chal(p)
+    A, S, Ap, Sp, z = lk.columns(a0, a1, a2, usable, theta, beta, gamma, p)
     assert Ap == sorted(A)
     assert sorted(Sp) == sorted(S)
     assert Ap[0] == Sp[0]
     for i in range(1, usable):
         assert Ap[i] == Sp[i] or Ap[i] == Ap[i - 1], i
     assert len(z) == usable + 1 and z[0] == 1 and z[-1] == 1
-    assert A[5] == lk.compress(theta, int(a0[5]), int(a1[5]), int(a2[5]))
+    assert A[5] == lk.compress(theta, int(a0[5]), int(a1[5]), int(a2[5]), p)
     assert S[0] == 0 and all(v == 0 for v in S[1 << 16:])
     # halo2 hands leftovers out ascending, each to the last open repeated row: the leftover
     # values sit on repeated rows in descending order

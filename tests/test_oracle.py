@@ -133,6 +133,9 @@ def test_bad_offsets_rejected(orc):
 
 
 P_PALLAS = 0x40000000000000000000000000000000224698fc094cf91b992d30ed00000001  # pasta Fp modulus
+# BN254 scalar field modulus r (halo2curves 0.3.2 bn256::Fr, the reference's circuit field:
+# blake2f.rs:283,293, blake2f_circuit_bench.rs:10): the group order of alt_bn128 (EIP-196)
+R_BN254 = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 
 
 def _limbs_to_int(v):
@@ -151,6 +154,20 @@ def test_fp_montgomery_vs_bigint(orc):
     assert _limbs_to_int(orc.fp_mont(1)) == 0x3fffffffffffffffffffffffffffffff992c350be41914ad34786d38fffffffd
 
 
+def test_fp_bn254_montgomery_vs_bigint(orc):
+    """the BN254 Fr form pinned to mont(x) = x * 2^256 mod r, r the
+    alt_bn128 group order (decimal, as EIP-196 publishes it)."""
+    assert orc.MODULI[orc.BN254] == R_BN254
+    rng = np.random.default_rng(26)
+    xs = [0, 1, 2, 3, 255, 256, 0x7fff, 0xffff, 0x55555555, 0xaaaaaaaa, 0xfffffffe, 0xffffffff]
+    xs += [int(v) for v in rng.integers(0, 2**32, 2000, dtype=np.uint64)]
+    for x in xs:
+        assert _limbs_to_int(orc.fp_mont(x, orc.BN254)) == (x << 256) % R_BN254, x
+    # mont(1) = R mod r: halo2curves' bn256::Fr one() in memory
+    assert _limbs_to_int(orc.fp_mont(1, orc.BN254)) == \
+        0x0e0a77c19a07df2f666ea36f7879462e36fc76959f60cd29ac96341c4ffffffb
+
+
 def test_fp_export_layout(orc):
     x = random_inputs(3, (1, 2), 22)
     adv, fixed, h_out, off = orc.fill(_orc_inputs(x, orc))
@@ -167,6 +184,13 @@ def test_fp_export_layout(orc):
         for r in rng.integers(0, nr, 40):
             v = int(adv[a, r0 + r])
             assert _limbs_to_int(mont[h, r]) == (v << 256) % P_PALLAS
+    bn = orc.export_fp(adv, row_begin=r0, nrows=nr, form=orc.FP_BN254_MONTGOMERY)
+    bc = orc.export_fp(adv, row_begin=r0, nrows=nr, form=orc.FP_BN254_CANONICAL)
+    assert np.array_equal(bc, can[:, r0:r0 + nr])
+    for h, a in enumerate(order):
+        for r in rng.integers(0, nr, 40):
+            v = int(adv[a, r0 + r])
+            assert _limbs_to_int(bn[h, r]) == (v << 256) % R_BN254
 
 
 def test_keygen_fixed_structure_equals_fill(orc):

@@ -25,7 +25,7 @@ CODE_FIXED = 18
 CODE_LAYOUT = 19
 MAX_ROUNDS = 1 << 20
 KERNEL_NAMES = ["record", "fill", "eval", "export", "fill_eval", "lookup"]  # B2F_KERNEL_*
-FP_CANONICAL, FP_MONTGOMERY = 0, 1  # B2F_FP_*
+FP_CANONICAL, FP_MONTGOMERY, FP_BN254_CANONICAL, FP_BN254_MONTGOMERY = 0, 1, 2, 3  # B2F_FP_*
 
 OK, ERR_ARG, ERR_ROUNDS, ERR_ROWS, ERR_HIP, ERR_LAYOUT, ERR_INPUT = range(7)
 STATUS_NAMES = {OK: "OK", ERR_ARG: "B2F_ERR_ARG", ERR_ROUNDS: "B2F_ERR_ROUNDS",

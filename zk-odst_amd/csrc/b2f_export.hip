@@ -10,7 +10,11 @@
 //   mont(x) = p - 4 x d = 2^254 - (4x - 1) d        (x != 0),   mont(0) = 0.
 // That is one 34 x 126-bit product and a 256-bit negation per cell (the oracle computes the
 // same values with a generic Montgomery multiply by R^2, oracle/b2f_oracle.c).
-// Canonical form (PrimeField::to_repr, 32-byte little endian) is simply (x, 0, 0, 0).
+// Canonical form (PrimeField::to_repr, 32-byte little endian) is simply (x, 0, 0, 0), in
+// either field.
+// BN254 Fr (halo2curves 0.3.2 bn256::Fr, r < 2^254, no such short form): mont(x) is the
+// generic Montgomery product x * R^2 / R with the one-word operand's zero words folded
+// (b2f_field.h; 8 + 64 word products).
 //
 // HBM-bound: 4 B read, 32 B written per cell. A wave writes 64 x 16 B = 1 KiB contiguous per
 // store instruction (lane l stores 16-byte chunk l of a 1 KiB span, i.e. half l & 1 of cell
@@ -19,6 +23,7 @@
 #include <stdint.h>
 
 #include "../../include/b2f.h"
+#include "b2f_field.h"
 
 namespace b2f {
 
@@ -38,9 +43,16 @@ constexpr int CELLS_PER_ITER = EXPORT_BLOCK / 2;  // 128 cells = 4 KiB of output
 // limbs (2*half, 2*half+1) of the field element for cell value x
 __device__ __forceinline__ u64x2 fp_half(uint32_t x, uint32_t half, uint32_t form) {
   u64x2 r;
-  if (form == B2F_FP_CANONICAL) {
+  if (!(form & 1u)) {  // canonical, either field
     r.x = half ? 0 : x;
     r.y = 0;
+    return r;
+  }
+  if (form == B2F_FP_BN254_MONTGOMERY) {
+    const field::Fe m = field::from_u32<field::Bn254>(x);
+    const uint32_t o = 4 * half;
+    r.x = (uint64_t)m.w[o] | ((uint64_t)m.w[o + 1] << 32);
+    r.y = (uint64_t)m.w[o + 2] | ((uint64_t)m.w[o + 3] << 32);
     return r;
   }
   if (x == 0) {

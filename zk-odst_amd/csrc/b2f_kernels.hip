@@ -1179,8 +1179,7 @@ B2F_API int b2f_export_fp_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t t
                               uint64_t* d_out, uint64_t out_rows, void* stream) {
   if (!ctx) return B2F_ERR_ARG;
   if (!d_advice || !d_out) return set_err(ctx, B2F_ERR_ARG, "export: null buffer");
-  if (form != B2F_FP_CANONICAL && form != B2F_FP_MONTGOMERY)
-    return set_err(ctx, B2F_ERR_ARG, "export: unknown form %u", form);
+  if (form > B2F_FP_BN254_MONTGOMERY) return set_err(ctx, B2F_ERR_ARG, "export: unknown form %u", form);
   if ((uintptr_t)d_out & 15) return set_err(ctx, B2F_ERR_ARG, "export: d_out must be 16-byte aligned");
   if (row_begin > total_rows || nrows > total_rows - row_begin)
     return set_err(ctx, B2F_ERR_ROWS, "export: rows [%llu, +%llu) exceed total_rows %llu",
@@ -1206,16 +1205,19 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
   if (!ctx) return B2F_ERR_ARG;
   if (!d_advice || !d_row_begin || !theta || !beta || !gamma || !d_out || !d_first_bad)
     return set_err(ctx, B2F_ERR_ARG, "lookup: null buffer");
-  if (form != B2F_FP_CANONICAL && form != B2F_FP_MONTGOMERY)
-    return set_err(ctx, B2F_ERR_ARG, "lookup: unknown form %u", form);
+  if (form > B2F_FP_BN254_MONTGOMERY) return set_err(ctx, B2F_ERR_ARG, "lookup: unknown form %u", form);
   if ((uintptr_t)d_out & 15) return set_err(ctx, B2F_ERR_ARG, "lookup: d_out must be 16-byte aligned");
   if (usable_rows < (1ull << 16) || usable_rows >= (1ull << 32))
     return set_err(ctx, B2F_ERR_ROWS, "lookup: usable_rows %llu not in [2^16, 2^32)",
                    (unsigned long long)usable_rows);
   if (out_rows < usable_rows + 1)
     return set_err(ctx, B2F_ERR_ROWS, "lookup: out_rows < usable_rows + 1");
-  auto canon = [](const uint64_t* v) {  // < p = 2^254 + d
-    static const uint64_t p[4] = {0x992d30ed00000001ull, 0x224698fc094cf91bull, 0, 0x4000000000000000ull};
+  auto canon = [form](const uint64_t* v) {  // < the field's modulus
+    static const uint64_t moduli[2][4] = {
+        {0x992d30ed00000001ull, 0x224698fc094cf91bull, 0, 0x4000000000000000ull},  // pasta Fp
+        {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull,
+         0x30644e72e131a029ull}};  // BN254 Fr
+    const uint64_t* p = moduli[form >> 1];
     for (int i = 3; i >= 0; i--)
       if (v[i] != p[i]) return v[i] < p[i];
     return false;

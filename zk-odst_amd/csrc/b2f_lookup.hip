@@ -2,7 +2,7 @@
 // row 4): for circuits cut from the trace (usable rows each), halo2_proofs 0.3.0's
 // compressed input A, compressed table S, permuted input A', permuted table S' and the
 // grand product z (lookup/prover.rs: commit_permuted, permute_expression_pair,
-// commit_product; restated in oracle/lookup.py).
+// commit_product; restated in oracle/lookup.py), over pasta Fp or BN254 Fr (b2f_field.h).
 //
 // halo2 sorts the compressed inputs and walks a BTreeMap of table values. Here every input
 // is a table row, so the sort is a counting sort over the 2^16 table rows in the order of
@@ -19,16 +19,21 @@
 //            (halo2 hands leftovers out in ascending order, each to the last open repeated
 //            row), found by binary search of LP;
 //   z:       the permute pass also writes each row's factors num = (A + beta)(S + gamma) and
-//            den = (A' + beta)(S' + gamma); per 64-row chunk the products of num and of den;
-//            exclusive product scans over the chunks; then each chunk's z rows N_p / D_p
-//            with one inversion per chunk (batch inversion, N_p staged in the z column).
-// Field arithmetic: pasta Fp, 4 x 64-bit limbs, Montgomery (R = 2^256) CIOS multiply.
+//            den = (A' + beta)(S' + gamma). z[p + 1] = N_p / D_p with N_p, D_p the prefix
+//            products through row p, and D_p^-1 = D^-1 * prod_{i > p} den_i: ONE inversion
+//            per circuit (of the whole product D), the rest suffix products. Per ZC-row
+//            chunk: the products of num and den (zchunk); per circuit: the exclusive prefix
+//            of the num products and, seeded with D^-1, the suffix of the den products
+//            (zscan); per chunk: N_p forward (staged in the z column), then backward
+//            z[p + 1] = N_p D_p^-1 and D_{p-1}^-1 = D_p^-1 den_p (zwrite). 3 products per
+//            row in zwrite, 2 in zchunk, 2 in permute.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "../../include/b2f.h"
+#include "b2f_field.h"
 
 namespace b2f {
 
@@ -41,122 +46,19 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
 
 namespace {
 
-typedef unsigned __int128 u128;
+using field::Fe;
+using field::load;
+using field::store;
 constexpr int TROWS = 1 << 16;
-constexpr uint64_t FP_P0 = 0x992d30ed00000001ull, FP_P1 = 0x224698fc094cf91bull,
-                   FP_P3 = 0x4000000000000000ull;
-constexpr uint64_t FP_INV = 0x992d30ecffffffffull;  // -p^-1 mod 2^64
 
-struct Fp {
-  uint64_t v[4];
-};
 struct Chal {
   uint64_t theta[4], beta[4], gamma[4];
 };
 
-__device__ __forceinline__ Fp fp_make(uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
-  Fp r;
-  r.v[0] = a; r.v[1] = b; r.v[2] = c; r.v[3] = d;
-  return r;
-}
-__device__ __forceinline__ Fp fp_one() {  // R mod p
-  return fp_make(0x34786d38fffffffdull, 0x992c350be41914adull, 0xffffffffffffffffull,
-                 0x3fffffffffffffffull);
-}
-__device__ __forceinline__ Fp fp_r2() {  // R^2 mod p
-  return fp_make(0x8c78ecb30000000full, 0xd7d30dbd8b0de0e7ull, 0x7797a99bc3c95d18ull,
-                 0x096d41af7b9cb714ull);
-}
-
-// t (< 2p) -> t mod p
-__device__ __forceinline__ Fp fp_reduce1(uint64_t t0, uint64_t t1, uint64_t t2, uint64_t t3) {
-  u128 d = (u128)t0 - FP_P0;
-  uint64_t r0 = (uint64_t)d, b = (uint64_t)(d >> 64) & 1;
-  d = (u128)t1 - FP_P1 - b;
-  uint64_t r1 = (uint64_t)d;
-  b = (uint64_t)(d >> 64) & 1;
-  d = (u128)t2 - b;
-  uint64_t r2 = (uint64_t)d;
-  b = (uint64_t)(d >> 64) & 1;
-  d = (u128)t3 - FP_P3 - b;
-  uint64_t r3 = (uint64_t)d;
-  b = (uint64_t)(d >> 64) & 1;
-  return b ? fp_make(t0, t1, t2, t3) : fp_make(r0, r1, r2, r3);
-}
-
-// Montgomery product a * b / 2^256 mod p (CIOS; p2 = 0 and p3 = 2^62 fold into the constants)
-__device__ __forceinline__ Fp fp_mul(const Fp& a, const Fp& b) {
-  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint64_t bi = b.v[i];
-    u128 c = (u128)a.v[0] * bi + t0;
-    t0 = (uint64_t)c;
-    c = (u128)a.v[1] * bi + t1 + (uint64_t)(c >> 64);
-    t1 = (uint64_t)c;
-    c = (u128)a.v[2] * bi + t2 + (uint64_t)(c >> 64);
-    t2 = (uint64_t)c;
-    c = (u128)a.v[3] * bi + t3 + (uint64_t)(c >> 64);
-    t3 = (uint64_t)c;
-    u128 c4 = (u128)t4 + (uint64_t)(c >> 64);
-    t4 = (uint64_t)c4;
-    const uint64_t t5 = (uint64_t)(c4 >> 64);
-    const uint64_t m = t0 * FP_INV;
-    c = (u128)m * FP_P0 + t0;
-    c = (u128)m * FP_P1 + t1 + (uint64_t)(c >> 64);
-    t0 = (uint64_t)c;
-    c = (u128)t2 + (uint64_t)(c >> 64);
-    t1 = (uint64_t)c;
-    c = (u128)m * FP_P3 + t3 + (uint64_t)(c >> 64);
-    t2 = (uint64_t)c;
-    c = (u128)t4 + (uint64_t)(c >> 64);
-    t3 = (uint64_t)c;
-    t4 = t5 + (uint64_t)(c >> 64);
-  }
-  return fp_reduce1(t0, t1, t2, t3);
-}
-
-__device__ __forceinline__ Fp fp_add(const Fp& a, const Fp& b) {  // a, b < p < 2^255
-  u128 c = (u128)a.v[0] + b.v[0];
-  uint64_t s0 = (uint64_t)c;
-  c = (u128)a.v[1] + b.v[1] + (uint64_t)(c >> 64);
-  uint64_t s1 = (uint64_t)c;
-  c = (u128)a.v[2] + b.v[2] + (uint64_t)(c >> 64);
-  uint64_t s2 = (uint64_t)c;
-  uint64_t s3 = a.v[3] + b.v[3] + (uint64_t)(c >> 64);
-  return fp_reduce1(s0, s1, s2, s3);
-}
-
-__device__ __forceinline__ Fp fp_small(uint32_t x) {  // Montgomery form of a small integer
-  return fp_mul(fp_make(x, 0, 0, 0), fp_r2());
-}
-
-// a^(p-2): left-to-right square and multiply over the fixed exponent
-__device__ Fp fp_inv(const Fp& a) {
-  const uint64_t e[4] = {FP_P0 - 2, FP_P1, 0, FP_P3};
-  Fp r = a;  // bit 254 (the top bit of e)
-#pragma unroll 1
-  for (int bit = 253; bit >= 0; bit--) {
-    r = fp_mul(r, r);
-    if ((e[bit >> 6] >> (bit & 63)) & 1) r = fp_mul(r, a);
-  }
-  return r;
-}
-
-__device__ __forceinline__ Fp fp_out(const Fp& a, uint32_t form) {
-  return form == B2F_FP_CANONICAL ? fp_mul(a, fp_make(1, 0, 0, 0)) : a;
-}
-
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void fp_store(uint64_t* p, const Fp& a) {
-  u64x2* q = reinterpret_cast<u64x2*>(p);
-  q[0] = u64x2{a.v[0], a.v[1]};
-  q[1] = u64x2{a.v[2], a.v[3]};
-}
-__device__ __forceinline__ Fp fp_load(const uint64_t* p) {
-  const u64x2* q = reinterpret_cast<const u64x2*>(p);
-  u64x2 x = q[0], y = q[1];
-  return fp_make(x.x, x.y, y.x, y.y);
+// Montgomery element -> the output form (Montgomery as stored, or canonical)
+template <class F>
+__device__ __forceinline__ Fe out_form(const Fe& a, bool mont) {
+  return mont ? a : field::to_canonical<F>(a);
 }
 
 __device__ __forceinline__ uint32_t spread16(uint32_t x) {
@@ -168,21 +70,22 @@ __device__ __forceinline__ uint32_t spread16(uint32_t x) {
 }
 __device__ __forceinline__ uint32_t tag16(uint32_t x) { return x < 256u ? 0u : (x < 32768u ? 1u : 2u); }
 
-__device__ __forceinline__ Fp chal(const uint64_t* c) { return fp_make(c[0], c[1], c[2], c[3]); }
-
 // ------------------------------------------------------------------ table pass (per theta)
-__global__ __launch_bounds__(256) void lk_table_kernel(Chal ch, Fp* __restrict__ Tx,
+template <class F>
+__global__ __launch_bounds__(256) void lk_table_kernel(Chal ch, Fe* __restrict__ Tx,
                                                        uint64_t* __restrict__ key,
                                                        uint32_t* __restrict__ perm) {
   const uint32_t x = blockIdx.x * 256 + threadIdx.x;
-  const Fp th = fp_mul(chal(ch.theta), fp_r2());
-  const Fp th2 = fp_mul(th, th);
-  Fp t = fp_add(fp_add(fp_mul(th2, fp_small(tag16(x))), fp_mul(th, fp_small(x))),
-                fp_small(spread16(x)));
+  const Fe th = field::to_mont<F>(field::load_words(ch.theta));
+  const Fe th2 = field::mul<F>(th, th);
+  const Fe t = field::add<F>(field::add<F>(field::mul<F>(th2, field::from_u32<F>(tag16(x))),
+                                           field::mul<F>(th, field::from_u32<F>(x))),
+                             field::from_u32<F>(spread16(x)));
   Tx[x] = t;
-  const Fp c = fp_mul(t, fp_make(1, 0, 0, 0));
+  const Fe c = field::to_canonical<F>(t);
 #pragma unroll
-  for (int k = 0; k < 4; k++) key[(uint64_t)k * TROWS + x] = c.v[k];
+  for (int k = 0; k < 4; k++)
+    key[(uint64_t)k * TROWS + x] = (uint64_t)c.w[2 * k] | ((uint64_t)c.w[2 * k + 1] << 32);
   perm[x] = x;
 }
 
@@ -193,9 +96,9 @@ __global__ __launch_bounds__(256) void lk_gather_key_kernel(const uint64_t* __re
   out[i] = limb[perm[i]];
 }
 
-__global__ __launch_bounds__(256) void lk_rank_kernel(const Fp* __restrict__ Tx,
+__global__ __launch_bounds__(256) void lk_rank_kernel(const Fe* __restrict__ Tx,
                                                       const uint32_t* __restrict__ perm,
-                                                      Fp* __restrict__ Ts) {
+                                                      Fe* __restrict__ Ts) {
   const uint32_t r = blockIdx.x * 256 + threadIdx.x;
   Ts[r] = Tx[perm[r]];
 }
@@ -243,11 +146,13 @@ __global__ __launch_bounds__(256) void lk_count_kernel(
 }
 
 // one workgroup per circuit: 1024 threads x 64 ranks
+constexpr int SAMPLE = TROWS / 16;  // every 16th pos / lp entry, for the permute searches
 __global__ __launch_bounds__(1024) void lk_scan_kernel(const uint32_t* __restrict__ perm,
                                                        const uint32_t* __restrict__ count,
                                                        uint64_t usable, uint32_t* __restrict__ pos,
                                                        uint32_t* __restrict__ dcnt,
-                                                       uint32_t* __restrict__ lp) {
+                                                       uint32_t* __restrict__ lp,
+                                                       uint32_t* __restrict__ samp) {
   const uint32_t c = blockIdx.x, t = threadIdx.x;
   const uint32_t* cnt = count + (uint64_t)c * TROWS;
   uint32_t sc = 0, sd = 0, sl = 0;
@@ -282,159 +187,193 @@ __global__ __launch_bounds__(1024) void lk_scan_kernel(const uint32_t* __restric
     ed += n ? 1u : 0u;
     D[r] = ed;
     L[r] = el;
+    if ((r & 15u) == 0) {
+      samp[(uint64_t)c * 2 * SAMPLE + (r >> 4)] = ec;
+      samp[(uint64_t)c * 2 * SAMPLE + SAMPLE + (r >> 4)] = el;
+    }
     ec += n;
     el += mult - (n ? 1u : 0u);
   }
 }
 
-// last index r with a[r] <= v (a nondecreasing, a[0] <= v)
-__device__ __forceinline__ uint32_t last_le(const uint32_t* a, uint32_t v) {
-  uint32_t lo = 0, hi = TROWS;  // answer in [lo, hi)
+// last index r with a[r] <= v (a nondecreasing over TROWS entries, a[0] <= v): the top 12
+// levels of the search over the workgroup's LDS sample s[k] = a[16 k], then the 16 entries
+// of that block (one 64-byte line, four loads in flight at once) in registers.
+__device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, const uint32_t* s,
+                                            uint32_t v) {
+  uint32_t lo = 0, hi = SAMPLE;  // last k with s[k] <= v, in [lo, hi)
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (a[mid] <= v) lo = mid; else hi = mid;
+    if (s[mid] <= v) lo = mid; else hi = mid;
   }
-  return lo;
+  const uint4* blk = reinterpret_cast<const uint4*>(a + 16 * lo);
+  const uint4 q0 = blk[0], q1 = blk[1], q2 = blk[2], q3 = blk[3];
+  const uint32_t e[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+  uint32_t n = 0;  // entries <= v (e[0] = s[lo] <= v; nondecreasing)
+#pragma unroll
+  for (int i = 1; i < 16; i++) n += e[i] <= v ? 1u : 0u;
+  return 16 * lo + n;
 }
 
+template <class F>
 __global__ __launch_bounds__(256) void lk_permute_kernel(
     const uint32_t* __restrict__ adv, uint64_t total_rows, const uint64_t* __restrict__ row_begin,
-    uint32_t c0, uint64_t usable, const Fp* __restrict__ Tx, const Fp* __restrict__ Ts,
+    uint32_t c0, uint64_t usable, const Fe* __restrict__ Tx, const Fe* __restrict__ Ts,
     const uint32_t* __restrict__ pos, const uint32_t* __restrict__ dcnt,
-    const uint32_t* __restrict__ lp, uint32_t form, uint64_t* __restrict__ out, uint64_t out_rows,
-    Chal ch, Fp* __restrict__ num, Fp* __restrict__ den) {
+    const uint32_t* __restrict__ lp, const uint32_t* __restrict__ samp, bool mont,
+    uint64_t* __restrict__ out, uint64_t out_rows, Chal ch, Fe* __restrict__ num,
+    Fe* __restrict__ den) {
   const uint32_t c = blockIdx.y;
-  const Fp beta = fp_mul(chal(ch.beta), fp_r2()), gamma = fp_mul(chal(ch.gamma), fp_r2());
-  Fp* nm = num + (uint64_t)c * usable;
-  Fp* dn = den + (uint64_t)c * usable;
+  const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
+  const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
+  Fe* nm = num + (uint64_t)c * usable;
+  Fe* dn = den + (uint64_t)c * usable;
   const Circ k = circ(row_begin, total_rows, usable, c0 + c);
   const uint32_t* P = pos + (uint64_t)c * TROWS;
   const uint32_t* D = dcnt + (uint64_t)c * TROWS;
   const uint32_t* L = lp + (uint64_t)c * TROWS;
   const uint32_t n_left = (uint32_t)usable - D[TROWS - 1];
+  __shared__ uint32_t sP[SAMPLE], sL[SAMPLE];
+  {
+    const uint4* sa = reinterpret_cast<const uint4*>(samp + (uint64_t)c * 2 * SAMPLE);
+    uint4* sp4 = reinterpret_cast<uint4*>(sP);
+    uint4* sl4 = reinterpret_cast<uint4*>(sL);
+    for (uint32_t k = threadIdx.x; k < (uint32_t)SAMPLE / 4; k += 256) {
+      sp4[k] = sa[k];
+      sl4[k] = sa[SAMPLE / 4 + k];
+    }
+  }
+  __syncthreads();
   uint64_t* o = out + (uint64_t)(c0 + c) * 5 * out_rows * 4;
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < usable; p += stride) {
     const uint32_t x = p < k.n_in ? (adv[total_rows + k.first + p] & 0xffffu) : 0u;
-    const Fp a = Tx[x];
-    const Fp sv = Tx[p < (uint64_t)TROWS ? (uint32_t)p : 0u];
-    const uint32_t r = last_le(P, (uint32_t)p);
-    const Fp ap = Ts[r];
-    Fp sp;
+    const Fe a = Tx[x];
+    const Fe sv = Tx[p < (uint64_t)TROWS ? (uint32_t)p : 0u];
+    const uint32_t r = last_le(P, sP, (uint32_t)p);
+    const Fe ap = Ts[r];
+    Fe sp;
     if (P[r] == (uint32_t)p) {
       sp = ap;
     } else {
       const uint32_t j = (uint32_t)p - D[r];
-      sp = Ts[last_le(L, n_left - 1 - j)];
+      sp = Ts[last_le(L, sL, n_left - 1 - j)];
     }
-    fp_store(o + 4 * p, fp_out(a, form));
-    fp_store(o + (out_rows + p) * 4, fp_out(sv, form));
-    fp_store(o + (2 * out_rows + p) * 4, fp_out(ap, form));
-    fp_store(o + (3 * out_rows + p) * 4, fp_out(sp, form));
+    store(o + 4 * p, out_form<F>(a, mont));
+    store(o + (out_rows + p) * 4, out_form<F>(sv, mont));
+    store(o + (2 * out_rows + p) * 4, out_form<F>(ap, mont));
+    store(o + (3 * out_rows + p) * 4, out_form<F>(sp, mont));
     // the grand product's factors (A + beta)(S + gamma) / ((A' + beta)(S' + gamma))
-    fp_store(nm[p].v, fp_mul(fp_add(a, beta), fp_add(sv, gamma)));
-    fp_store(dn[p].v, fp_mul(fp_add(ap, beta), fp_add(sp, gamma)));
+    nm[p] = field::mul<F>(field::add<F>(a, beta), field::add<F>(sv, gamma));
+    dn[p] = field::mul<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma));
   }
 }
 
-constexpr uint32_t ZC = 64;  // rows per z chunk (one inversion per chunk)
+constexpr uint32_t ZC = 16;  // rows per z chunk (one lane walks a chunk)
 
-// per chunk: products of num and den
-__global__ __launch_bounds__(256) void lk_zchunk_kernel(uint64_t usable, const Fp* __restrict__ num,
-                                                        const Fp* __restrict__ den,
-                                                        Fp* __restrict__ zn, Fp* __restrict__ zd) {
+// per chunk q (rows b..e-1): the chunk's num prefix Nloc_p = prod_{b <= i <= p} num_i staged
+// in z[p + 1], its total in zn[q], and the den product of the chunk in zd[q]
+template <class F>
+__global__ __launch_bounds__(256) void lk_zchunk_kernel(uint32_t c0, uint64_t usable,
+                                                        uint64_t* __restrict__ out, uint64_t out_rows,
+                                                        const Fe* __restrict__ num,
+                                                        const Fe* __restrict__ den,
+                                                        Fe* __restrict__ zn, Fe* __restrict__ zd) {
   const uint32_t c = blockIdx.y;
   const uint64_t nq = (usable + ZC - 1) / ZC;
   const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (q >= nq) return;
-  const Fp* nm = num + (uint64_t)c * usable;
-  const Fp* dn = den + (uint64_t)c * usable;
-  Fp pn = fp_one(), pd = fp_one();
-  const uint64_t e = (q + 1) * ZC < usable ? (q + 1) * ZC : usable;
-  for (uint64_t p = q * ZC; p < e; p++) {
-    pn = fp_mul(pn, fp_load(nm[p].v));
-    pd = fp_mul(pd, fp_load(dn[p].v));
+  const Fe* nm = num + (uint64_t)c * usable;
+  const Fe* dn = den + (uint64_t)c * usable;
+  uint64_t* zcol = out + ((uint64_t)(c0 + c) * 5 + 4) * out_rows * 4;
+  const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
+  Fe pn = nm[b], pd = dn[b];
+  store(zcol + 4 * (b + 1), pn);
+  for (uint64_t p = b + 1; p < e; p++) {
+    pn = field::mul<F>(pn, nm[p]);
+    pd = field::mul<F>(pd, dn[p]);
+    store(zcol + 4 * (p + 1), pn);
   }
   zn[(uint64_t)c * nq + q] = pn;
   zd[(uint64_t)c * nq + q] = pd;
 }
 
-// exclusive product scans of zn and zd over a circuit's chunks (one workgroup per circuit):
-// per-thread runs of chunks, then a Hillis-Steele scan of the 1024 run products in LDS (both
-// arrays at once: two independent multiply chains)
+// per circuit (one workgroup): with N_before(q) = prod_{q' < q} zn[q'] and D_end(q) =
+// prod_{q' <= q} zd[q'], zn[q] <- K_q = N_before(q) D_end(q)^-1, where D_end(q)^-1 = D^-1
+// prod_{q' > q} zd[q'] (D the product of every den: the one inversion). Per-thread runs of
+// chunks, Hillis-Steele scans of the run products in LDS (a prefix for num, a suffix for den).
 constexpr int ZS_THREADS = 1024;
-__global__ __launch_bounds__(ZS_THREADS) void lk_zscan_kernel(uint64_t usable, Fp* __restrict__ zn,
-                                                              Fp* __restrict__ zd) {
+template <class F>
+__global__ __launch_bounds__(ZS_THREADS) void lk_zscan_kernel(uint64_t usable, Fe* __restrict__ zn,
+                                                              const Fe* __restrict__ zd) {
   const uint32_t c = blockIdx.x, t = threadIdx.x;
   const uint64_t nq = (usable + ZC - 1) / ZC;
   const uint64_t per = (nq + ZS_THREADS - 1) / ZS_THREADS;
-  __shared__ Fp sn[ZS_THREADS], sd[ZS_THREADS];
-  Fp* an = zn + (uint64_t)c * nq;
-  Fp* ad = zd + (uint64_t)c * nq;
+  __shared__ Fe sn[ZS_THREADS], sd[ZS_THREADS];
+  __shared__ Fe dinv;
+  Fe* an = zn + (uint64_t)c * nq;
+  const Fe* ad = zd + (uint64_t)c * nq;
   const uint64_t b = t * per < nq ? t * per : nq, e = b + per < nq ? b + per : nq;
-  Fp pn = fp_one(), pd = fp_one();
+  Fe pn = field::one<F>(), pd = field::one<F>();
   for (uint64_t q = b; q < e; q++) {
-    pn = fp_mul(pn, an[q]);
-    pd = fp_mul(pd, ad[q]);
+    pn = field::mul<F>(pn, an[q]);
+    pd = field::mul<F>(pd, ad[q]);
   }
   sn[t] = pn;
   sd[t] = pd;
   __syncthreads();
-  for (int off = 1; off < ZS_THREADS; off <<= 1) {  // inclusive
-    Fp xn = pn, xd = pd;
-    if (t >= (uint32_t)off) {
-      xn = fp_mul(sn[t - off], pn);
-      xd = fp_mul(sd[t - off], pd);
-    }
+  for (int off = 1; off < ZS_THREADS; off <<= 1) {  // inclusive: prefix of sn, suffix of sd
+    Fe xn = pn, xd = pd;
+    if (t >= (uint32_t)off) xn = field::mul<F>(sn[t - off], pn);
+    if (t + off < (uint32_t)ZS_THREADS) xd = field::mul<F>(pd, sd[t + off]);
     __syncthreads();
     sn[t] = pn = xn;
     sd[t] = pd = xd;
     __syncthreads();
   }
-  Fp rn = t ? sn[t - 1] : fp_one(), rd = t ? sd[t - 1] : fp_one();
-  for (uint64_t q = b; q < e; q++) {
-    const Fp vn = an[q], vd = ad[q];
+  if (t == 0) dinv = field::inv<F>(sd[0]);  // sd[0] = D
+  __syncthreads();
+  // walk the run backward: the den suffix seeds from the runs after this one; the num prefix
+  // of chunk q is the run's prefix times the chunk products before q inside the run
+  Fe rd = t + 1 < (uint32_t)ZS_THREADS ? field::mul<F>(dinv, sd[t + 1]) : dinv;
+  Fe rn = t ? sn[t - 1] : field::one<F>();
+  for (uint64_t q = b; q < e; q++) {  // forward: exclusive num prefix into an[q]
+    const Fe vn = an[q];
     an[q] = rn;
-    ad[q] = rd;
-    rn = fp_mul(rn, vn);
-    rd = fp_mul(rd, vd);
+    rn = field::mul<F>(rn, vn);
+  }
+  for (uint64_t q = e; q-- > b;) {  // backward: K_q = N_before(q) D_end(q)^-1
+    an[q] = field::mul<F>(an[q], rd);
+    rd = field::mul<F>(rd, ad[q]);
   }
 }
 
-// z rows of chunk q: with N_p, D_p the prefix products of num and den through row p,
-// z[p + 1] = N_p / D_p. Forward: N_p staged in z[p + 1], D running; one inversion of the
-// chunk's last D; backward: z[p + 1] = N_p (1 / D_p), 1 / D_{p-1} = (1 / D_p) den_p.
-__global__ __launch_bounds__(256) void lk_zwrite_kernel(uint32_t c0, uint64_t usable, uint32_t form,
+// z rows of chunk q, backward: z[p + 1] = K_q Nloc_p prod_{p < i < e} den_i (Nloc_p staged
+// in z[p + 1] by zchunk), the running factor K_q prod den_i one product per row.
+template <class F>
+__global__ __launch_bounds__(256) void lk_zwrite_kernel(uint32_t c0, uint64_t usable, bool mont,
                                                         uint64_t* __restrict__ out, uint64_t out_rows,
-                                                        const Fp* __restrict__ num,
-                                                        const Fp* __restrict__ den,
-                                                        const Fp* __restrict__ zn,
-                                                        const Fp* __restrict__ zd) {
+                                                        const Fe* __restrict__ den,
+                                                        const Fe* __restrict__ zn) {
   const uint32_t c = blockIdx.y;
   const uint64_t nq = (usable + ZC - 1) / ZC;
   const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (q >= nq) return;
-  const Fp* nm = num + (uint64_t)c * usable;
-  const Fp* dn = den + (uint64_t)c * usable;
+  const Fe* dn = den + (uint64_t)c * usable;
   uint64_t* zcol = out + ((uint64_t)(c0 + c) * 5 + 4) * out_rows * 4;
-  const uint64_t b = q * ZC, e = (q + 1) * ZC < usable ? (q + 1) * ZC : usable;
-  Fp n = zn[(uint64_t)c * nq + q], d = zd[(uint64_t)c * nq + q];
-  if (q == 0) fp_store(zcol, fp_out(fp_one(), form));
-  for (uint64_t p = b; p < e; p++) {
-    n = fp_mul(n, fp_load(nm[p].v));
-    d = fp_mul(d, fp_load(dn[p].v));
-    fp_store(zcol + 4 * (p + 1), n);
-  }
-  Fp inv = fp_inv(d);
+  const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
+  if (q == 0) store(zcol, out_form<F>(field::one<F>(), mont));
+  Fe k = zn[(uint64_t)c * nq + q];
   for (uint64_t p = e; p-- > b;) {
-    fp_store(zcol + 4 * (p + 1), fp_out(fp_mul(fp_load(zcol + 4 * (p + 1)), inv), form));
-    inv = fp_mul(inv, fp_load(dn[p].v));
+    store(zcol + 4 * (p + 1), out_form<F>(field::mul<F>(load(zcol + 4 * (p + 1)), k), mont));
+    if (p > b) k = field::mul<F>(k, dn[p]);
   }
 }
 
 struct Carve {
-  Fp* Tx;
-  Fp* Ts;
+  Fe* Tx;
+  Fe* Ts;
   uint64_t* key;   // 4 x TROWS canonical limbs
   uint64_t* kin;   // TROWS
   uint64_t* kout;  // TROWS
@@ -444,10 +383,11 @@ struct Carve {
   uint32_t* pos;
   uint32_t* dcnt;
   uint32_t* lp;
-  Fp* num;  // group x usable
-  Fp* den;
-  Fp* zn;  // group x nq
-  Fp* zd;
+  uint32_t* samp;  // group x 2 x SAMPLE
+  Fe* num;  // group x usable
+  Fe* den;
+  Fe* zn;  // group x nq
+  Fe* zd;
   void* sort_tmp;
   size_t sort_bytes;
   size_t total;
@@ -470,8 +410,8 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
     return r;
   };
   const uint64_t nq = (usable + ZC - 1) / ZC;
-  k.Tx = (Fp*)take(sizeof(Fp) * TROWS);
-  k.Ts = (Fp*)take(sizeof(Fp) * TROWS);
+  k.Tx = (Fe*)take(sizeof(Fe) * TROWS);
+  k.Ts = (Fe*)take(sizeof(Fe) * TROWS);
   k.key = (uint64_t*)take(8ull * 4 * TROWS);
   k.kin = (uint64_t*)take(8ull * TROWS);
   k.kout = (uint64_t*)take(8ull * TROWS);
@@ -481,36 +421,25 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.pos = (uint32_t*)take(4ull * TROWS * group);
   k.dcnt = (uint32_t*)take(4ull * TROWS * group);
   k.lp = (uint32_t*)take(4ull * TROWS * group);
-  k.num = (Fp*)take(sizeof(Fp) * usable * group);
-  k.den = (Fp*)take(sizeof(Fp) * usable * group);
-  k.zn = (Fp*)take(sizeof(Fp) * nq * group);
-  k.zd = (Fp*)take(sizeof(Fp) * nq * group);
+  k.samp = (uint32_t*)take(8ull * SAMPLE * group);
+  k.num = (Fe*)take(sizeof(Fe) * usable * group);
+  k.den = (Fe*)take(sizeof(Fe) * usable * group);
+  k.zn = (Fe*)take(sizeof(Fe) * nq * group);
+  k.zd = (Fe*)take(sizeof(Fe) * nq * group);
   k.sort_bytes = sort_temp_bytes();
   k.sort_tmp = take(k.sort_bytes);
   k.total = off;
   return k;
 }
 
-}  // namespace
-
-size_t lookup_scratch_bytes(uint32_t group, uint64_t usable_rows) {
-  return carve(nullptr, group, usable_rows).total;
-}
-
-hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
-                         const uint64_t* d_row_begin, uint32_t n_circuits, uint64_t usable_rows,
-                         const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
-                         uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
-                         void* scratch, uint32_t group, hipStream_t s) {
+template <class F>
+hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint64_t* d_row_begin,
+                      uint32_t n_circuits, uint64_t usable_rows, const Chal& ch, bool mont,
+                      uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad, void* scratch,
+                      uint32_t group, hipStream_t s) {
   Carve k = carve(scratch, group, usable_rows);
-  Chal ch;
-  for (int i = 0; i < 4; i++) {
-    ch.theta[i] = theta[i];
-    ch.beta[i] = beta[i];
-    ch.gamma[i] = gamma[i];
-  }
   const dim3 tb(TROWS / 256);
-  hipLaunchKernelGGL(lk_table_kernel, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm);
+  hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm);
   // stable LSD over the four 64-bit limbs of the canonical value
   uint32_t* pa = k.perm;
   uint32_t* pb = k.perm2;
@@ -537,20 +466,47 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
     hipLaunchKernelGGL(lk_count_kernel, dim3(bx, g), dim3(256), 0, s, d_advice, total_rows,
                        d_row_begin, c0, usable_rows, k.count, d_first_bad);
     hipLaunchKernelGGL(lk_scan_kernel, dim3(g), dim3(1024), 0, s, pa, k.count, usable_rows, k.pos,
-                       k.dcnt, k.lp);
-    hipLaunchKernelGGL(lk_permute_kernel, dim3(bx, g), dim3(256), 0, s, d_advice, total_rows,
-                       d_row_begin, c0, usable_rows, k.Tx, k.Ts, k.pos, k.dcnt, k.lp, form, d_out,
-                       out_rows, ch, k.num, k.den);
+                       k.dcnt, k.lp, k.samp);
+    // permute: ~4096 rows per workgroup (the LDS samples are staged once per workgroup)
+    const uint32_t px = (uint32_t)((usable_rows + 4095) / 4096);
+    hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
+                       d_row_begin, c0, usable_rows, k.Tx, k.Ts, k.pos, k.dcnt, k.lp, k.samp, mont,
+                       d_out, out_rows, ch, k.num, k.den);
     const uint32_t zq = (uint32_t)((nq + 255) / 256);
-    hipLaunchKernelGGL(lk_zchunk_kernel, dim3(zq, g), dim3(256), 0, s, usable_rows, k.num, k.den,
-                       k.zn, k.zd);
-    hipLaunchKernelGGL(lk_zscan_kernel, dim3(g), dim3(ZS_THREADS), 0, s, usable_rows, k.zn, k.zd);
-    hipLaunchKernelGGL(lk_zwrite_kernel, dim3(zq, g), dim3(256), 0, s, c0, usable_rows, form, d_out,
+    hipLaunchKernelGGL(lk_zchunk_kernel<F>, dim3(zq, g), dim3(256), 0, s, c0, usable_rows, d_out,
                        out_rows, k.num, k.den, k.zn, k.zd);
+    hipLaunchKernelGGL(lk_zscan_kernel<F>, dim3(g), dim3(ZS_THREADS), 0, s, usable_rows, k.zn, k.zd);
+    hipLaunchKernelGGL(lk_zwrite_kernel<F>, dim3(zq, g), dim3(256), 0, s, c0, usable_rows, mont, d_out,
+                       out_rows, k.den, k.zn);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+}  // namespace
+
+size_t lookup_scratch_bytes(uint32_t group, uint64_t usable_rows) {
+  return carve(nullptr, group, usable_rows).total;
+}
+
+hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
+                         const uint64_t* d_row_begin, uint32_t n_circuits, uint64_t usable_rows,
+                         const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
+                         uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
+                         void* scratch, uint32_t group, hipStream_t s) {
+  Chal ch;
+  for (int i = 0; i < 4; i++) {
+    ch.theta[i] = theta[i];
+    ch.beta[i] = beta[i];
+    ch.gamma[i] = gamma[i];
+  }
+  const bool mont = (form & 1u) != 0;
+  if (form >> 1)
+    return run_lookup<field::Bn254>(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, ch,
+                                    mont, d_out, out_rows, d_first_bad, scratch, group, s);
+  return run_lookup<field::Pallas>(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, ch,
+                                   mont, d_out, out_rows, d_first_bad, scratch, group, s);
 }
 
 }  // namespace b2f
