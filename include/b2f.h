@@ -246,6 +246,41 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
                                    uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
                                    void* stream);
 
+/* Keygen's permutation mapping of one instance of `rounds` rounds (halo2_proofs 0.3.0
+ * plonk/permutation/keygen.rs Assembly::copy replayed over b2f_copy_constraints in synthesis
+ * order, each copy as copy(destination, source)): for permutation column j (= a_{j+1}, the
+ * enable_equality order of table16.rs:312-314) and instance row i < R = b2f_layout_rows(rounds),
+ * out[j * R + i] = (c' << 29) | r' names the cell the permutation maps (j, i) to. Writes
+ * min(8 R, cap) words, returns 8 R (0 for rounds > B2F_MAX_ROUNDS). Host function. */
+B2F_API uint64_t b2f_permutation_mapping(uint32_t rounds, uint32_t* out, uint64_t cap);
+
+/* Permutation-argument prover columns (halo2_proofs 0.3.0 plonk/permutation: build_pk's
+ * permutation polynomials and prover.rs commit) of the equality columns a_1..a_8 for one
+ * circuit made of the instances with host row map h_offsets[0..n] (trace rows of the batch in
+ * d_advice; circuit row = trace row - h_offsets[0]), in a domain of 2^k rows:
+ *   d_sigma (nullable): sigma_j(w^i) = delta^c' w^r' for (c', r') the mapped cell, at
+ *     d_sigma[(j * out_rows + i) * 4 + limb], j < 8, every row i < 2^k (identity past the
+ *     instances);
+ *   d_z: for each set c of chunk_len columns (cs.degree() - 2 in halo2) the grand product
+ *     z_c[0] = z_{c-1}[usable_rows] (1 for c = 0),
+ *     z_c[i + 1] = z_c[i] prod_{j in c} (v_j(i) + beta delta^j w^i + gamma)
+ *                          / (v_j(i) + beta sigma_j(w^i) + gamma),   i < usable_rows,
+ *     at d_z[(c * out_rows + i) * 4 + limb], rows 0 ..= usable_rows (the blinding rows after
+ *     them are the prover's). v_j(i) is the cell of a_{j+1} (zero past the instances).
+ * usable_rows = 2^k - blinding_factors - 1 >= h_offsets[n] - h_offsets[0]; omega = the
+ * domain's generator (F::ROOT_OF_UNITY squared S - k times), delta = F::DELTA, beta, gamma:
+ * canonical elements of the field chosen by `form` (any B2F_FP_*; outputs in that form).
+ * out_rows >= usable_rows + 1 (and >= 2^k with d_sigma); 16-byte aligned outputs. A valid
+ * trace closes: z_last[usable_rows] = 1. Asynchronous on `stream` after a short host setup
+ * (mapping patterns cached per rounds in the context). */
+B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t total_rows,
+                                        const uint64_t* h_offsets, size_t n, uint32_t k,
+                                        uint64_t usable_rows, const uint64_t omega[4],
+                                        const uint64_t delta[4], const uint64_t beta[4],
+                                        const uint64_t gamma[4], uint32_t chunk_len, uint32_t form,
+                                        uint64_t* d_sigma, uint64_t* d_z, uint64_t out_rows,
+                                        void* stream);
+
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel the
  * fill/eval calls launch (no host synchronization while recording). b2f_set_timing(ctx, 1)
  * clears the log and starts recording; b2f_kernel_times waits for the recorded events and
@@ -257,7 +292,8 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
 #define B2F_KERNEL_EXPORT 3 /* Fp export */
 #define B2F_KERNEL_FILL_EVAL 4 /* fused trace expansion + constraint evaluation */
 #define B2F_KERNEL_LOOKUP 5 /* lookup-argument prover columns (all passes of one call) */
-#define B2F_NUM_KERNELS 6
+#define B2F_KERNEL_PERM 6   /* permutation-argument prover columns (all passes of one call) */
+#define B2F_NUM_KERNELS 7
 B2F_API int b2f_set_timing(b2f_ctx* ctx, int enable);
 B2F_API int b2f_kernel_times(b2f_ctx* ctx, double* total_ms, uint32_t* count);
 

@@ -126,12 +126,12 @@ def test_product_library_reads_no_environment():
 @pytest.mark.parametrize("rounds", [0, 1, 2, 12, 13])
 def test_copy_constraints_match_oracle_structure(orc, rounds):
     """b2f_copy_constraints (the product's keygen copy list, host code) == the equality pairs
-    the oracle's structure-mode synthesis records, as sets; count 24 + 576 rounds + 96."""
+    the oracle's structure-mode synthesis records, in the same (synthesis) order -- the
+    permutation argument's cycle order depends on it; count 24 + 576 rounds + 96."""
     import b2f
 
     got = b2f.copy_constraints(rounds)
     want = orc.copies(rounds)
     assert len(got) == 24 + 576 * rounds + 96 == len(want)
-    key = lambda a: sorted(map(tuple, a.tolist()))  # noqa: E731
-    assert key(got) == key(want)
+    assert np.array_equal(got, want)
     assert len(set(map(tuple, got[:, :2].tolist()))) == len(got)  # one copy per operand cell

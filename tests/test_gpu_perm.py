@@ -1,0 +1,130 @@
+"""GPU parity of the permutation-argument prover columns (b2f_permutation_columns_dev, VERDICT
+r1 item 9) with the CPU restatement of halo2_proofs 0.3.0's keygen + prover
+(oracle/permutation.py): sigma and every z bit-exact in all four field forms and several
+column-set sizes, for circuits made of all or part of a batch; z closes to 1 on the valid
+trace and not on a broken copy. Needs an MI355X (`-m gpu`)."""
+import numpy as np
+import pytest
+
+import permutation as pm
+
+from conftest import random_inputs
+
+pytestmark = pytest.mark.gpu
+
+R256 = 1 << 256
+
+
+def _ints(t):
+    a = t.cpu().numpy().view(np.uint64).astype(object)
+    return [int(v) for v in (a[:, 0] | (a[:, 1] << 64) | (a[:, 2] << 128) | (a[:, 3] << 192))]
+
+
+def _p(form):
+    return pm.P_BN254 if form & 2 else pm.P_PALLAS
+
+
+@pytest.fixture(scope="module")
+def batch(engine):
+    import b2f
+    import torch
+
+    x = random_inputs(5, (0, 1, 2), 91)
+    b = b2f.DeviceBatch(x)
+    b.fill(engine)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    return b
+
+
+def _check(engine, batch, orc, k, usable, form, chunk, instances):
+    import torch
+
+    p = _p(form)
+    rng = np.random.default_rng(92 + form + 10 * chunk)
+    beta = int.from_bytes(rng.bytes(32), "little") % p
+    gamma = int.from_bytes(rng.bytes(32), "little") % p
+    sig, z = batch.permutation_columns(engine, k, usable, beta, gamma, chunk_len=chunk, form=form,
+                                       instances=instances)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    i0, i1 = instances
+    off = batch.offsets_host[i0:i1 + 1].astype(np.int64)
+    adv, _ = batch.host_trace()
+    cadv = adv[:, int(off[0]):int(off[-1])]
+    rel = off - off[0]
+    sigma, zs = pm.columns(cadv, rel, k, usable, beta, gamma, chunk, p, orc.copies)
+    conv = (lambda v: v) if form in (0, 2) else (lambda v: v * R256 % p)
+    for j in range(8):
+        got = _ints(sig[j])
+        want = [conv(v) for v in sigma[j]]
+        if got != want:
+            i = next(i for i in range(len(got)) if got[i] != want[i])
+            pytest.fail("sigma column %d differs first at row %d" % (j, i))
+    assert z.shape[0] == len(zs)
+    for c, zc in enumerate(zs):
+        got = _ints(z[c, :usable + 1])
+        want = [conv(v) for v in zc]
+        if got != want:
+            i = next(i for i in range(len(got)) if got[i] != want[i])
+            pytest.fail("z set %d differs first at row %d" % (c, i))
+    return zs
+
+
+@pytest.mark.parametrize("form,chunk", [(1, 3), (0, 3), (3, 1), (2, 8), (1, 8), (3, 5)])
+def test_permutation_columns_equal_oracle(engine, batch, orc, form, chunk):
+    k = 12
+    zs = _check(engine, batch, orc, k, (1 << k) - 7, form, chunk, (0, batch.n))
+    assert zs[-1][-1] == 1  # a valid trace closes
+
+
+def test_permutation_circuit_inside_batch(engine, batch, orc):
+    """A circuit of instances 1..3 (its first trace row is not 0), a looser usable count."""
+    _check(engine, batch, orc, 12, 4000, 1, 3, (1, 4))
+
+
+def test_permutation_closes_and_broken_copy(engine, orc):
+    import b2f
+    import torch
+
+    x = random_inputs(6, (1, 4), 93)
+    b = b2f.DeviceBatch(x)
+    b.fill(engine)
+    s = torch.cuda.current_stream().cuda_stream
+    k, usable = 14, (1 << 14) - 9
+    one = (1 << 256) % pm.P_PALLAS
+    _, z = b.permutation_columns(engine, k, usable, 12345, 67890, chunk_len=3)
+    engine.sync(s)
+    assert _ints(z[-1, usable:usable + 1]) == [one]
+    dr, dc, sr, sc = (int(v) for v in orc.copies(4)[100])
+    row = int(b.offsets_host[1]) + dr
+    b.advice[dc, row] ^= 1 << 3
+    _, z = b.permutation_columns(engine, k, usable, 12345, 67890, chunk_len=3)
+    engine.sync(s)
+    assert _ints(z[-1, usable:usable + 1]) != [one]
+
+
+def test_permutation_argument_errors(engine, batch):
+    import b2f
+    import torch
+
+    s = torch.cuda.current_stream().cuda_stream
+    dev = batch.advice.device
+    z = torch.empty((8, 1 << 12, 4), dtype=torch.int64, device=dev)
+    off = batch.offsets_host
+    w, d = pm.domain(pm.P_PALLAS, 12)
+
+    def call(k=12, usable=4089, beta=3, chunk=3, form=1, offs=off, out_rows=1 << 12):
+        engine.permutation_columns_dev(batch.advice.data_ptr(), batch.total_rows, offs, k, usable,
+                                       w, d, beta, 5, chunk, form, 0, z.data_ptr(), out_rows, s)
+
+    bad_off = off.copy()
+    bad_off[2] += 4
+    for kw, code in [({"k": 9}, b2f._lib.ERR_ARG), ({"chunk": 0}, b2f._lib.ERR_ARG),
+                     ({"chunk": 9}, b2f._lib.ERR_ARG), ({"beta": pm.P_PALLAS}, b2f._lib.ERR_ARG),
+                     ({"form": 4}, b2f._lib.ERR_ARG), ({"usable": 100}, b2f._lib.ERR_ROWS),
+                     ({"usable": 4096}, b2f._lib.ERR_ROWS), ({"out_rows": 100}, b2f._lib.ERR_ROWS),
+                     ({"offs": bad_off}, b2f._lib.ERR_LAYOUT)]:
+        with pytest.raises(b2f.B2FError) as e:
+            call(**kw)
+        assert e.value.code == code, kw
+    call()
+    engine.sync(s)

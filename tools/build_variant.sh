@@ -9,5 +9,5 @@ H="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fvisibility=hidden --offload-arch=g
 $H -mllvm -amdgpu-atomic-optimizer-strategy=None -c -o $D/k.o csrc/b2f_kernels.hip &
 $H -mllvm -amdgpu-atomic-optimizer-strategy=None -c -o $D/f.o csrc/b2f_fused.hip &
 wait
-$H -shared -o variants/libb2f_$N.so $D/k.o $D/f.o build/b2f_export.o build/b2f_lookup.o
+$H -shared -o variants/libb2f_$N.so $D/k.o $D/f.o build/b2f_export.o build/b2f_lookup.o build/b2f_perm.o
 echo built variants/libb2f_$N.so

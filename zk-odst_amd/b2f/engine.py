@@ -118,6 +118,18 @@ class Engine:
             int(usable_rows), lim[0], lim[1], lim[2], int(form), _vp(d_out), int(out_rows),
             _vp(d_first_bad), _vp(stream)))
 
+    def permutation_columns_dev(self, d_adv, total_rows, h_offsets, k, usable_rows, omega, delta,
+                                beta, gamma, chunk_len, form, d_sigma, d_z, out_rows, stream=0):
+        """b2f_permutation_columns_dev; h_offsets: host u64 row map of the circuit's instances,
+        omega/delta/beta/gamma Python ints (canonical)."""
+        off = np.ascontiguousarray(h_offsets, dtype=np.uint64)
+        lim = [(ctypes.c_uint64 * 4)(*[(int(v) >> (64 * i)) & (2**64 - 1) for i in range(4)])
+               for v in (omega, delta, beta, gamma)]
+        self._check(self.lib.b2f_permutation_columns_dev(
+            self.ctx, _vp(d_adv), int(total_rows), _np_ptr(off), len(off) - 1, int(k),
+            int(usable_rows), lim[0], lim[1], lim[2], lim[3], int(chunk_len), int(form),
+            _vp(d_sigma) if d_sigma else None, _vp(d_z), int(out_rows), _vp(stream)))
+
     def sync(self, stream=0):
         self._check(self.lib.b2f_sync(self.ctx, _vp(stream)))
 
@@ -131,6 +143,16 @@ class Engine:
         cnt = (ctypes.c_uint32 * k)()
         self._check(self.lib.b2f_kernel_times(self.ctx, tot, cnt))
         return {name: (float(tot[i]), int(cnt[i])) for i, name in enumerate(_lib.KERNEL_NAMES)}
+
+
+def permutation_mapping(rounds):
+    """Keygen's permutation mapping of one instance: u32 [8, R] entries (c' << 29) | r'
+    (b2f_permutation_mapping)."""
+    lib = _lib.load()
+    n = int(lib.b2f_permutation_mapping(int(rounds), None, 0))
+    out = np.zeros(n, dtype=np.uint32)
+    lib.b2f_permutation_mapping(int(rounds), _np_ptr(out), n)
+    return out.reshape(8, -1)
 
 
 def copy_constraints(rounds):
@@ -220,6 +242,30 @@ class DeviceBatch:
                                usable_rows, theta, beta, gamma, form, out.data_ptr(),
                                usable_rows + 1, bad.data_ptr(), s)
         return out, bad
+
+    def permutation_columns(self, eng, k, usable_rows, beta, gamma, chunk_len=3,
+                            form=_lib.FP_MONTGOMERY, instances=None, sigma=True, stream=None):
+        """Permutation-argument prover columns of the circuit holding instances
+        [i0, i1) = `instances` (default: all) in a 2^k-row domain: (sigma int64 [8, 2^k, 4] or
+        None, z int64 [sets, 2^k, 4] with rows 0..usable_rows written) -- see
+        b2f_permutation_columns_dev. omega and delta come from the field of `form`."""
+        from . import field
+
+        torch = self.torch
+        dev = self.advice.device
+        i0, i1 = (0, self.n) if instances is None else instances
+        off = self.offsets_host[i0:i1 + 1]
+        f = field.of_form(form)
+        n_rows = 1 << int(k)
+        sets = (8 + chunk_len - 1) // chunk_len
+        sig = torch.empty((8, n_rows, 4), dtype=torch.int64, device=dev) if sigma else None
+        z = torch.empty((sets, n_rows, 4), dtype=torch.int64, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        eng.permutation_columns_dev(self.advice.data_ptr(), self.total_rows, off, k, usable_rows,
+                                    field.omega(f, int(k)), field.delta(f), beta, gamma,
+                                    chunk_len, form, sig.data_ptr() if sigma else 0,
+                                    z.data_ptr(), n_rows, s)
+        return sig, z
 
     def report_dict(self):
         raw = self.report.cpu().numpy().view(np.uint64)

@@ -1,0 +1,151 @@
+// b2f_gprod.h -- the grand product z[0] = seed, z[p + 1] = z[p] num_p / den_p over `usable`
+// rows, shared by the lookup argument (halo2_proofs 0.3.0 lookup/prover.rs commit_product,
+// seed 1) and the permutation argument (permutation/prover.rs commit, seed = the previous
+// column set's last z).
+//
+// z[p + 1] = seed N_p / D_p with N_p, D_p the prefix products through row p, and
+// D_p^-1 = D^-1 prod_{i > p} den_i: ONE inversion per product (of the whole den product D),
+// the rest prefix and suffix products. Three passes over ZC-row chunks (one lane walks one
+// chunk):
+//   gp_chunk:  the chunk's num prefix Nloc_p staged in z[p + 1], the chunk totals of num and
+//              den (2 products per row);
+//   gp_scan:   per product (one workgroup): K_q = seed N_before(q) D_end(q)^-1 per chunk, the
+//              inversion, and the closing value seed N / D (= z[usable]) for a next product;
+//   gp_write:  backward over the chunk: z[p + 1] = K_q Nloc_p prod_{p < i < e} den_i
+//              (2 products per row), converted to the output form.
+// Products are independent along blockIdx.y: product y reads num/den + y * usable and writes
+// z column z_base + y * z_stride (u64 units, 4 per element).
+#pragma once
+#include "b2f_field.h"
+
+namespace b2f {
+namespace gp {
+namespace {
+
+using field::Fe;
+
+constexpr uint32_t ZC = 16;           // rows per chunk
+constexpr int SCAN_THREADS = 1024;    // one workgroup per product
+
+__host__ __device__ inline uint64_t n_chunks(uint64_t usable) { return (usable + ZC - 1) / ZC; }
+
+template <class F>
+__device__ __forceinline__ Fe out_form(const Fe& a, bool mont) {
+  return mont ? a : field::to_canonical<F>(a);
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void gp_chunk(uint64_t usable, uint64_t* __restrict__ z_base,
+                                                uint64_t z_stride, const Fe* __restrict__ num,
+                                                const Fe* __restrict__ den, Fe* __restrict__ zn,
+                                                Fe* __restrict__ zd) {
+  const uint32_t c = blockIdx.y;
+  const uint64_t nq = n_chunks(usable);
+  const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  const Fe* nm = num + (uint64_t)c * usable;
+  const Fe* dn = den + (uint64_t)c * usable;
+  uint64_t* zcol = z_base + (uint64_t)c * z_stride;
+  const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
+  Fe pn = nm[b], pd = dn[b];
+  field::store(zcol + 4 * (b + 1), pn);
+  for (uint64_t p = b + 1; p < e; p++) {
+    pn = field::mul<F>(pn, nm[p]);
+    pd = field::mul<F>(pd, dn[p]);
+    field::store(zcol + 4 * (p + 1), pn);
+  }
+  zn[(uint64_t)c * nq + q] = pn;
+  zd[(uint64_t)c * nq + q] = pd;
+}
+
+// zn[q] <- K_q = seed N_before(q) D_end(q)^-1 with N_before(q) = prod_{q' < q} zn[q'],
+// D_end(q)^-1 = D^-1 prod_{q' > q} zd[q']. Per-thread runs of chunks, Hillis-Steele scans
+// of the run products in LDS (a prefix for num, a suffix for den), one inversion.
+// seed: Montgomery elements per product (nullptr: 1); closing (nullable) <- seed N / D.
+template <class F>
+__global__ __launch_bounds__(SCAN_THREADS) void gp_scan(uint64_t usable, Fe* __restrict__ zn,
+                                                        const Fe* __restrict__ zd,
+                                                        const Fe* __restrict__ seed,
+                                                        Fe* __restrict__ closing) {
+  const uint32_t c = blockIdx.x, t = threadIdx.x;
+  const uint64_t nq = n_chunks(usable);
+  const uint64_t per = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
+  __shared__ Fe sn[SCAN_THREADS], sd[SCAN_THREADS];
+  __shared__ Fe dinv;
+  Fe* an = zn + (uint64_t)c * nq;
+  const Fe* ad = zd + (uint64_t)c * nq;
+  const uint64_t b = t * per < nq ? t * per : nq, e = b + per < nq ? b + per : nq;
+  Fe pn = field::one<F>(), pd = field::one<F>();
+  for (uint64_t q = b; q < e; q++) {
+    pn = field::mul<F>(pn, an[q]);
+    pd = field::mul<F>(pd, ad[q]);
+  }
+  sn[t] = pn;
+  sd[t] = pd;
+  __syncthreads();
+  for (int off = 1; off < SCAN_THREADS; off <<= 1) {  // inclusive: prefix of sn, suffix of sd
+    Fe xn = pn, xd = pd;
+    if (t >= (uint32_t)off) xn = field::mul<F>(sn[t - off], pn);
+    if (t + off < (uint32_t)SCAN_THREADS) xd = field::mul<F>(pd, sd[t + off]);
+    __syncthreads();
+    sn[t] = pn = xn;
+    sd[t] = pd = xd;
+    __syncthreads();
+  }
+  const Fe s = seed ? seed[c] : field::one<F>();
+  if (t == 0) {
+    dinv = field::inv<F>(sd[0]);  // sd[0] = D
+    if (closing) closing[c] = field::mul<F>(field::mul<F>(s, sn[SCAN_THREADS - 1]), dinv);
+  }
+  __syncthreads();
+  Fe rd = t + 1 < (uint32_t)SCAN_THREADS ? field::mul<F>(dinv, sd[t + 1]) : dinv;
+  Fe rn = t ? field::mul<F>(s, sn[t - 1]) : s;
+  for (uint64_t q = b; q < e; q++) {  // forward: seed times the exclusive num prefix
+    const Fe vn = an[q];
+    an[q] = rn;
+    rn = field::mul<F>(rn, vn);
+  }
+  for (uint64_t q = e; q-- > b;) {  // backward: K_q
+    an[q] = field::mul<F>(an[q], rd);
+    rd = field::mul<F>(rd, ad[q]);
+  }
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint64_t* __restrict__ z_base,
+                                                uint64_t z_stride, const Fe* __restrict__ den,
+                                                const Fe* __restrict__ zn,
+                                                const Fe* __restrict__ seed) {
+  const uint32_t c = blockIdx.y;
+  const uint64_t nq = n_chunks(usable);
+  const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  const Fe* dn = den + (uint64_t)c * usable;
+  uint64_t* zcol = z_base + (uint64_t)c * z_stride;
+  const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
+  if (q == 0) field::store(zcol, out_form<F>(seed ? seed[c] : field::one<F>(), mont));
+  Fe k = zn[(uint64_t)c * nq + q];
+  for (uint64_t p = e; p-- > b;) {
+    field::store(zcol + 4 * (p + 1), out_form<F>(field::mul<F>(field::load(zcol + 4 * (p + 1)), k), mont));
+    if (p > b) k = field::mul<F>(k, dn[p]);
+  }
+}
+
+// The three passes for `g` independent products on `s`. zn, zd: scratch of g * n_chunks
+// elements each.
+template <class F>
+hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_t z_stride,
+               const Fe* num, const Fe* den, Fe* zn, Fe* zd, const Fe* seed, Fe* closing,
+               hipStream_t s) {
+  const uint32_t zq = (uint32_t)((n_chunks(usable) + 255) / 256);
+  hipLaunchKernelGGL(gp_chunk<F>, dim3(zq, g), dim3(256), 0, s, usable, z_base, z_stride, num, den,
+                     zn, zd);
+  hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, usable, zn, zd, seed, closing);
+  hipLaunchKernelGGL(gp_write<F>, dim3(zq, g), dim3(256), 0, s, usable, mont, z_base, z_stride, den,
+                     zn, seed);
+  return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace gp
+}  // namespace b2f

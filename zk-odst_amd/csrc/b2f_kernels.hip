@@ -24,6 +24,7 @@
 #include <string.h>
 
 #include <new>
+#include <map>
 #include <vector>
 
 #include "../../include/b2f.h"
@@ -38,6 +39,13 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
                          void* scratch, uint32_t group, hipStream_t s);
+size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst);
+hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0,
+                              const uint64_t* d_inst, size_t n_inst, const uint32_t* d_pool,
+                              uint32_t k, uint64_t usable_rows, const uint64_t* omega,
+                              const uint64_t* delta, const uint64_t* beta, const uint64_t* gamma,
+                              uint32_t chunk_len, uint32_t form, uint64_t* d_sigma, uint64_t* d_z,
+                              uint64_t out_rows, void* scratch, hipStream_t s);
 hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
                             uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
                             int cu_count, hipStream_t s);  // b2f_export.hip
@@ -726,6 +734,16 @@ struct b2f_ctx {
   size_t lk_cap;
   void* d_fz;          // fused-path scratch: tile descriptors + deferred rows (b2f_fused.hip)
   size_t fz_cap;
+  // permutation columns (b2f_perm.hip): keygen mapping patterns per rounds (host cache and
+  // the device pool holding them), the per-call instance table, scratch
+  std::map<uint32_t, std::vector<uint32_t>> pm_pat;
+  std::map<uint32_t, uint64_t> pm_pool_off;  // rounds -> offset in d_pm_pool (u32 units)
+  uint32_t* d_pm_pool;
+  std::vector<uint64_t> pm_inst_host;
+  uint64_t* d_pm_inst;
+  size_t pm_inst_cap;
+  void* d_pm;
+  size_t pm_cap;
 };
 
 namespace {
@@ -877,6 +895,45 @@ uint64_t copy_constraints(uint32_t rounds, uint32_t* out4, uint64_t cap) {
   return cnt;
 }
 
+// Keygen's permutation mapping of one instance (halo2_proofs 0.3.0 plonk/permutation/keygen.rs
+// Assembly::copy): the instance's copy constraints replayed in synthesis order, each as
+// copy(left = the copy's destination cell, right = its source) -- AssignedCell::copy_advice
+// assigns the new cell, then constrain_equal(new, self). Cycles merge smaller-into-larger:
+// every cell of the right cycle is re-pointed to the left cycle's representative and the two
+// cells' mapping entries are swapped. Permutation column j is a_{j+1} (enable_equality order,
+// table16.rs:312-314). Output: out[j * R + i] = (c' << 29) | r', the cell (c', r') that cell
+// (j, i) maps to.
+constexpr int PM_COLS = 8;
+bool perm_mapping(uint32_t rounds, std::vector<uint32_t>& out) {
+  const uint64_t R = layout_rows(rounds);
+  if (!R) return false;
+  const uint64_t ncp = copy_constraints(rounds, nullptr, 0);
+  std::vector<uint32_t> cp(4 * ncp);
+  copy_constraints(rounds, cp.data(), ncp);
+  const uint64_t cells = PM_COLS * R;
+  std::vector<uint32_t> mapping(cells), aux(cells), sizes(cells, 1);
+  for (uint64_t x = 0; x < cells; x++) mapping[x] = aux[x] = (uint32_t)x;  // x = j * R + i
+  for (uint64_t q = 0; q < ncp; q++) {
+    const uint32_t dr = cp[4 * q], dc = cp[4 * q + 1], sr = cp[4 * q + 2], sc = cp[4 * q + 3];
+    if (dc < 1 || dc > 8 || sc < 1 || sc > 8) return false;  // only a_1..a_8 take part
+    const uint32_t left = (dc - 1) * (uint32_t)R + dr, right = (sc - 1) * (uint32_t)R + sr;
+    uint32_t lc = aux[left], rc = aux[right];
+    if (lc == rc) continue;
+    if (sizes[lc] < sizes[rc]) std::swap(lc, rc);
+    sizes[lc] += sizes[rc];
+    uint32_t i = rc;
+    do {
+      aux[i] = lc;
+      i = mapping[i];
+    } while (i != rc);
+    std::swap(mapping[left], mapping[right]);
+  }
+  out.resize(cells);
+  for (uint64_t x = 0; x < cells; x++)
+    out[x] = ((mapping[x] / (uint32_t)R) << 29) | (mapping[x] % (uint32_t)R);
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -948,6 +1005,9 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
   (void)hipFree(ctx->d_clock);
   (void)hipFree(ctx->d_lk);
   (void)hipFree(ctx->d_fz);
+  (void)hipFree(ctx->d_pm_pool);
+  (void)hipFree(ctx->d_pm_inst);
+  (void)hipFree(ctx->d_pm);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   delete ctx;
 }
@@ -1245,6 +1305,116 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
   int tk = timed_begin(ctx, B2F_KERNEL_LOOKUP, s);
   HIPCHK(ctx, launch_lookup(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, theta, beta,
                             gamma, form, d_out, out_rows, d_first_bad, ctx->d_lk, group, s));
+  timed_end(ctx, tk, s);
+  return B2F_OK;
+}
+
+B2F_API uint64_t b2f_permutation_mapping(uint32_t rounds, uint32_t* out, uint64_t cap) {
+  std::vector<uint32_t> m;
+  if (!perm_mapping(rounds, m)) return 0;
+  if (out) memcpy(out, m.data(), 4 * (m.size() < cap ? m.size() : cap));
+  return m.size();
+}
+
+B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t total_rows,
+                                        const uint64_t* h_offsets, size_t n, uint32_t k,
+                                        uint64_t usable_rows, const uint64_t omega[4],
+                                        const uint64_t delta[4], const uint64_t beta[4],
+                                        const uint64_t gamma[4], uint32_t chunk_len, uint32_t form,
+                                        uint64_t* d_sigma, uint64_t* d_z, uint64_t out_rows,
+                                        void* stream) {
+  if (!ctx) return B2F_ERR_ARG;
+  if (!d_advice || !h_offsets || !omega || !delta || !beta || !gamma || !d_z || n == 0)
+    return set_err(ctx, B2F_ERR_ARG, "permutation: null buffer or no instances");
+  if (form > B2F_FP_BN254_MONTGOMERY) return set_err(ctx, B2F_ERR_ARG, "permutation: unknown form %u", form);
+  if (chunk_len < 1 || chunk_len > PM_COLS)
+    return set_err(ctx, B2F_ERR_ARG, "permutation: chunk_len %u not in [1, 8]", chunk_len);
+  if (k < 10 || k > 30) return set_err(ctx, B2F_ERR_ARG, "permutation: k %u not in [10, 30]", k);
+  if (((uintptr_t)d_z & 15) || ((uintptr_t)d_sigma & 15))
+    return set_err(ctx, B2F_ERR_ARG, "permutation: outputs must be 16-byte aligned");
+  static const uint64_t moduli[2][4] = {
+      {0x992d30ed00000001ull, 0x224698fc094cf91bull, 0, 0x4000000000000000ull},
+      {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull, 0x30644e72e131a029ull}};
+  auto canon = [&](const uint64_t* v) {
+    const uint64_t* p = moduli[form >> 1];
+    for (int i = 3; i >= 0; i--)
+      if (v[i] != p[i]) return v[i] < p[i];
+    return false;
+  };
+  if (!canon(omega) || !canon(delta) || !canon(beta) || !canon(gamma))
+    return set_err(ctx, B2F_ERR_ARG, "permutation: omega/delta/beta/gamma not canonical field elements");
+  const uint64_t n_rows = 1ull << k;
+  const uint64_t row0 = h_offsets[0];
+  std::vector<uint32_t> need;
+  for (size_t i = 0; i < n; i++) {
+    const uint64_t R = h_offsets[i + 1] - h_offsets[i];
+    if (h_offsets[i + 1] < h_offsets[i] || R < FIXED_ROWS || (R - FIXED_ROWS) % ROUND_ROWS ||
+        (R - FIXED_ROWS) / ROUND_ROWS > B2F_MAX_ROUNDS)
+      return set_err(ctx, B2F_ERR_LAYOUT, "permutation: offsets[%zu..%zu] is not an instance", i, i + 1);
+    need.push_back((uint32_t)((R - FIXED_ROWS) / ROUND_ROWS));
+  }
+  const uint64_t used = h_offsets[n] - row0;
+  if (h_offsets[n] > total_rows) return set_err(ctx, B2F_ERR_ROWS, "permutation: instances past total_rows");
+  if (used > usable_rows || usable_rows >= n_rows)
+    return set_err(ctx, B2F_ERR_ROWS, "permutation: need used rows %llu <= usable_rows %llu < 2^k",
+                   (unsigned long long)used, (unsigned long long)usable_rows);
+  if (out_rows < usable_rows + 1 || (d_sigma && out_rows < n_rows))
+    return set_err(ctx, B2F_ERR_ROWS, "permutation: out_rows too small");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  // mapping patterns: build the missing ones, rebuild the device pool if it lacks any
+  bool rebuild = false;
+  for (uint32_t r : need) {
+    if (!ctx->pm_pat.count(r)) {
+      std::vector<uint32_t> m;
+      if (!perm_mapping(r, m)) return set_err(ctx, B2F_ERR_ROUNDS, "permutation: rounds %u", r);
+      ctx->pm_pat[r] = std::move(m);
+    }
+    if (!ctx->pm_pool_off.count(r)) rebuild = true;
+  }
+  if (rebuild) {
+    std::vector<uint32_t> pool;
+    ctx->pm_pool_off.clear();
+    for (auto& kv : ctx->pm_pat) {
+      ctx->pm_pool_off[kv.first] = pool.size();
+      pool.insert(pool.end(), kv.second.begin(), kv.second.end());
+    }
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    if (ctx->d_pm_pool) HIPCHK(ctx, hipFree(ctx->d_pm_pool));
+    ctx->d_pm_pool = nullptr;
+    HIPCHK(ctx, hipMalloc(&ctx->d_pm_pool, 4 * pool.size()));
+    HIPCHK(ctx, hipMemcpy(ctx->d_pm_pool, pool.data(), 4 * pool.size(), hipMemcpyHostToDevice));
+  }
+  // instance table: n + 1 circuit start rows, then n pool offsets
+  std::vector<uint64_t>& it = ctx->pm_inst_host;
+  it.assign(2 * n + 1, 0);
+  for (size_t i = 0; i <= n; i++) it[i] = h_offsets[i] - row0;
+  for (size_t i = 0; i < n; i++) it[n + 1 + i] = ctx->pm_pool_off[need[i]];
+  const size_t need_scr = perm_scratch_bytes(k, usable_rows, n);
+  if (it.size() > ctx->pm_inst_cap || need_scr > ctx->pm_cap) {
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    if (it.size() > ctx->pm_inst_cap) {
+      if (ctx->d_pm_inst) HIPCHK(ctx, hipFree(ctx->d_pm_inst));
+      ctx->d_pm_inst = nullptr;
+      ctx->pm_inst_cap = 0;
+      HIPCHK(ctx, hipMalloc(&ctx->d_pm_inst, 8 * it.size()));
+      ctx->pm_inst_cap = it.size();
+    }
+    if (need_scr > ctx->pm_cap) {
+      if (ctx->d_pm) HIPCHK(ctx, hipFree(ctx->d_pm));
+      ctx->d_pm = nullptr;
+      ctx->pm_cap = 0;
+      HIPCHK(ctx, hipMalloc(&ctx->d_pm, need_scr));
+      ctx->pm_cap = need_scr;
+    }
+  }
+  // the table is small; a blocking upload keeps the host vector reusable by the next call
+  HIPCHK(ctx, hipStreamSynchronize(s));
+  HIPCHK(ctx, hipMemcpy(ctx->d_pm_inst, it.data(), 8 * it.size(), hipMemcpyHostToDevice));
+  int tk = timed_begin(ctx, B2F_KERNEL_PERM, s);
+  HIPCHK(ctx, launch_permutation(d_advice, total_rows, row0, ctx->d_pm_inst, n, ctx->d_pm_pool, k,
+                                 usable_rows, omega, delta, beta, gamma, chunk_len, form, d_sigma,
+                                 d_z, out_rows, ctx->d_pm, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }

@@ -19,14 +19,8 @@
 //            (halo2 hands leftovers out in ascending order, each to the last open repeated
 //            row), found by binary search of LP;
 //   z:       the permute pass also writes each row's factors num = (A + beta)(S + gamma) and
-//            den = (A' + beta)(S' + gamma). z[p + 1] = N_p / D_p with N_p, D_p the prefix
-//            products through row p, and D_p^-1 = D^-1 * prod_{i > p} den_i: ONE inversion
-//            per circuit (of the whole product D), the rest suffix products. Per ZC-row
-//            chunk: the products of num and den (zchunk); per circuit: the exclusive prefix
-//            of the num products and, seeded with D^-1, the suffix of the den products
-//            (zscan); per chunk: N_p forward (staged in the z column), then backward
-//            z[p + 1] = N_p D_p^-1 and D_{p-1}^-1 = D_p^-1 den_p (zwrite). 3 products per
-//            row in zwrite, 2 in zchunk, 2 in permute.
+//            den = (A' + beta)(S' + gamma); the grand product over them (b2f_gprod.h: one
+//            inversion per circuit, 4 products per row) writes the z column.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -34,6 +28,7 @@
 
 #include "../../include/b2f.h"
 #include "b2f_field.h"
+#include "b2f_gprod.h"
 
 namespace b2f {
 
@@ -55,11 +50,7 @@ struct Chal {
   uint64_t theta[4], beta[4], gamma[4];
 };
 
-// Montgomery element -> the output form (Montgomery as stored, or canonical)
-template <class F>
-__device__ __forceinline__ Fe out_form(const Fe& a, bool mont) {
-  return mont ? a : field::to_canonical<F>(a);
-}
+using gp::out_form;
 
 __device__ __forceinline__ uint32_t spread16(uint32_t x) {
   x = (x | (x << 8)) & 0x00FF00FFu;
@@ -270,106 +261,7 @@ __global__ __launch_bounds__(256) void lk_permute_kernel(
   }
 }
 
-constexpr uint32_t ZC = 16;  // rows per z chunk (one lane walks a chunk)
-
-// per chunk q (rows b..e-1): the chunk's num prefix Nloc_p = prod_{b <= i <= p} num_i staged
-// in z[p + 1], its total in zn[q], and the den product of the chunk in zd[q]
-template <class F>
-__global__ __launch_bounds__(256) void lk_zchunk_kernel(uint32_t c0, uint64_t usable,
-                                                        uint64_t* __restrict__ out, uint64_t out_rows,
-                                                        const Fe* __restrict__ num,
-                                                        const Fe* __restrict__ den,
-                                                        Fe* __restrict__ zn, Fe* __restrict__ zd) {
-  const uint32_t c = blockIdx.y;
-  const uint64_t nq = (usable + ZC - 1) / ZC;
-  const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (q >= nq) return;
-  const Fe* nm = num + (uint64_t)c * usable;
-  const Fe* dn = den + (uint64_t)c * usable;
-  uint64_t* zcol = out + ((uint64_t)(c0 + c) * 5 + 4) * out_rows * 4;
-  const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
-  Fe pn = nm[b], pd = dn[b];
-  store(zcol + 4 * (b + 1), pn);
-  for (uint64_t p = b + 1; p < e; p++) {
-    pn = field::mul<F>(pn, nm[p]);
-    pd = field::mul<F>(pd, dn[p]);
-    store(zcol + 4 * (p + 1), pn);
-  }
-  zn[(uint64_t)c * nq + q] = pn;
-  zd[(uint64_t)c * nq + q] = pd;
-}
-
-// per circuit (one workgroup): with N_before(q) = prod_{q' < q} zn[q'] and D_end(q) =
-// prod_{q' <= q} zd[q'], zn[q] <- K_q = N_before(q) D_end(q)^-1, where D_end(q)^-1 = D^-1
-// prod_{q' > q} zd[q'] (D the product of every den: the one inversion). Per-thread runs of
-// chunks, Hillis-Steele scans of the run products in LDS (a prefix for num, a suffix for den).
-constexpr int ZS_THREADS = 1024;
-template <class F>
-__global__ __launch_bounds__(ZS_THREADS) void lk_zscan_kernel(uint64_t usable, Fe* __restrict__ zn,
-                                                              const Fe* __restrict__ zd) {
-  const uint32_t c = blockIdx.x, t = threadIdx.x;
-  const uint64_t nq = (usable + ZC - 1) / ZC;
-  const uint64_t per = (nq + ZS_THREADS - 1) / ZS_THREADS;
-  __shared__ Fe sn[ZS_THREADS], sd[ZS_THREADS];
-  __shared__ Fe dinv;
-  Fe* an = zn + (uint64_t)c * nq;
-  const Fe* ad = zd + (uint64_t)c * nq;
-  const uint64_t b = t * per < nq ? t * per : nq, e = b + per < nq ? b + per : nq;
-  Fe pn = field::one<F>(), pd = field::one<F>();
-  for (uint64_t q = b; q < e; q++) {
-    pn = field::mul<F>(pn, an[q]);
-    pd = field::mul<F>(pd, ad[q]);
-  }
-  sn[t] = pn;
-  sd[t] = pd;
-  __syncthreads();
-  for (int off = 1; off < ZS_THREADS; off <<= 1) {  // inclusive: prefix of sn, suffix of sd
-    Fe xn = pn, xd = pd;
-    if (t >= (uint32_t)off) xn = field::mul<F>(sn[t - off], pn);
-    if (t + off < (uint32_t)ZS_THREADS) xd = field::mul<F>(pd, sd[t + off]);
-    __syncthreads();
-    sn[t] = pn = xn;
-    sd[t] = pd = xd;
-    __syncthreads();
-  }
-  if (t == 0) dinv = field::inv<F>(sd[0]);  // sd[0] = D
-  __syncthreads();
-  // walk the run backward: the den suffix seeds from the runs after this one; the num prefix
-  // of chunk q is the run's prefix times the chunk products before q inside the run
-  Fe rd = t + 1 < (uint32_t)ZS_THREADS ? field::mul<F>(dinv, sd[t + 1]) : dinv;
-  Fe rn = t ? sn[t - 1] : field::one<F>();
-  for (uint64_t q = b; q < e; q++) {  // forward: exclusive num prefix into an[q]
-    const Fe vn = an[q];
-    an[q] = rn;
-    rn = field::mul<F>(rn, vn);
-  }
-  for (uint64_t q = e; q-- > b;) {  // backward: K_q = N_before(q) D_end(q)^-1
-    an[q] = field::mul<F>(an[q], rd);
-    rd = field::mul<F>(rd, ad[q]);
-  }
-}
-
-// z rows of chunk q, backward: z[p + 1] = K_q Nloc_p prod_{p < i < e} den_i (Nloc_p staged
-// in z[p + 1] by zchunk), the running factor K_q prod den_i one product per row.
-template <class F>
-__global__ __launch_bounds__(256) void lk_zwrite_kernel(uint32_t c0, uint64_t usable, bool mont,
-                                                        uint64_t* __restrict__ out, uint64_t out_rows,
-                                                        const Fe* __restrict__ den,
-                                                        const Fe* __restrict__ zn) {
-  const uint32_t c = blockIdx.y;
-  const uint64_t nq = (usable + ZC - 1) / ZC;
-  const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (q >= nq) return;
-  const Fe* dn = den + (uint64_t)c * usable;
-  uint64_t* zcol = out + ((uint64_t)(c0 + c) * 5 + 4) * out_rows * 4;
-  const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
-  if (q == 0) store(zcol, out_form<F>(field::one<F>(), mont));
-  Fe k = zn[(uint64_t)c * nq + q];
-  for (uint64_t p = e; p-- > b;) {
-    store(zcol + 4 * (p + 1), out_form<F>(field::mul<F>(load(zcol + 4 * (p + 1)), k), mont));
-    if (p > b) k = field::mul<F>(k, dn[p]);
-  }
-}
+using gp::ZC;
 
 struct Carve {
   Fe* Tx;
@@ -457,7 +349,6 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   hipLaunchKernelGGL(lk_rank_kernel, tb, dim3(256), 0, s, k.Tx, pa, k.Ts);
   hipError_t e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s);
   if (e != hipSuccess) return e;
-  const uint64_t nq = (usable_rows + ZC - 1) / ZC;
   for (uint32_t c0 = 0; c0 < n_circuits; c0 += group) {
     const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
     e = hipMemsetAsync(k.count, 0, 4ull * TROWS * g, s);
@@ -472,13 +363,8 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
     hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
                        d_row_begin, c0, usable_rows, k.Tx, k.Ts, k.pos, k.dcnt, k.lp, k.samp, mont,
                        d_out, out_rows, ch, k.num, k.den);
-    const uint32_t zq = (uint32_t)((nq + 255) / 256);
-    hipLaunchKernelGGL(lk_zchunk_kernel<F>, dim3(zq, g), dim3(256), 0, s, c0, usable_rows, d_out,
-                       out_rows, k.num, k.den, k.zn, k.zd);
-    hipLaunchKernelGGL(lk_zscan_kernel<F>, dim3(g), dim3(ZS_THREADS), 0, s, usable_rows, k.zn, k.zd);
-    hipLaunchKernelGGL(lk_zwrite_kernel<F>, dim3(zq, g), dim3(256), 0, s, c0, usable_rows, mont, d_out,
-                       out_rows, k.den, k.zn);
-    e = hipGetLastError();
+    e = gp::run<F>(g, usable_rows, mont, d_out + ((uint64_t)c0 * 5 + 4) * out_rows * 4,
+                   5 * out_rows * 4, k.num, k.den, k.zn, k.zd, nullptr, nullptr, s);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

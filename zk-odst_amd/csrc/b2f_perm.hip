@@ -1,0 +1,254 @@
+// b2f_perm.hip -- permutation-argument prover columns of the equality columns a_1..a_8
+// (table16.rs:312-314; halo2_proofs 0.3.0 plonk/permutation: keygen.rs Assembly::copy +
+// build_pk's permutation polynomials, prover.rs commit; restated in oracle/permutation.py).
+//
+// One circuit = whole instances of a batch, circuit row = trace row - the first instance's
+// offset. Keygen's cycle structure comes from the structure alone and is the same for every
+// instance of a given `rounds`: the host replays halo2's Assembly::copy over one instance's
+// copy list (b2f_kernels.hip, perm_mapping) and this file expands the resulting mapping
+// pattern over the circuit:
+//   sigma_j(w^i) = delta^c' w^r'   with (c', r') = mapping[j][i] (identity off the cycles);
+//   for each set of chunk_len columns, the grand product with
+//     num_i = prod_j (v_j(i) + beta delta^j w^i + gamma),
+//     den_i = prod_j (v_j(i) + beta sigma_j(w^i) + gamma),
+//   z[0] = the previous set's last z (1 for the first), z[i + 1] = z[i] num_i / den_i
+//   (b2f_gprod.h), rows 0 .. usable (the blinding rows after it are the prover's).
+// delta^c w^r = OL[c][r mod 1024] OH[r / 1024]: two table reads and one product per value
+// (OL, BL = beta OL: 8 x 1024 entries; OH: 2^k / 1024 entries), built per call.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/b2f.h"
+#include "b2f_field.h"
+#include "b2f_gprod.h"
+
+namespace b2f {
+
+size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst);
+hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0,
+                              const uint64_t* d_inst, size_t n_inst, const uint32_t* d_pool,
+                              uint32_t k, uint64_t usable_rows, const uint64_t* omega,
+                              const uint64_t* delta, const uint64_t* beta, const uint64_t* gamma,
+                              uint32_t chunk_len, uint32_t form, uint64_t* d_sigma, uint64_t* d_z,
+                              uint64_t out_rows, void* scratch, hipStream_t s);
+
+namespace {
+
+using field::Fe;
+constexpr int NCOL = 8;    // equality columns a_1..a_8, permutation column j = a_{j+1}
+constexpr int LO = 1024;   // low table
+constexpr uint32_t ROW_BITS = 29;  // mapping entries: (column << 29) | instance-relative row
+
+struct Params {
+  uint64_t omega[4], delta[4], beta[4];
+};
+
+template <class F>
+__device__ Fe pow_u64(Fe b, uint64_t e) {
+  Fe r = field::one<F>();
+  while (e) {
+    if (e & 1) r = field::mul<F>(r, b);
+    b = field::mul<F>(b, b);
+    e >>= 1;
+  }
+  return r;
+}
+
+// OL[c][lo] = delta^c w^lo, BL[c][lo] = beta OL[c][lo] (c < 8, lo < 1024); OH[h] = w^(1024 h)
+template <class F>
+__global__ __launch_bounds__(256) void pm_table_kernel(Params prm, uint64_t n_hi, Fe* __restrict__ OL,
+                                                       Fe* __restrict__ BL, Fe* __restrict__ OH) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const Fe w = field::to_mont<F>(field::load_words(prm.omega));
+  if (i < (uint64_t)NCOL * LO) {
+    const uint32_t c = (uint32_t)(i / LO), lo = (uint32_t)(i % LO);
+    const Fe d = field::to_mont<F>(field::load_words(prm.delta));
+    const Fe b = field::to_mont<F>(field::load_words(prm.beta));
+    const Fe v = field::mul<F>(pow_u64<F>(d, c), pow_u64<F>(w, lo));
+    OL[i] = v;
+    BL[i] = field::mul<F>(b, v);
+  }
+  if (i < n_hi) OH[i] = pow_u64<F>(pow_u64<F>(w, LO), i);
+}
+
+// the instance holding circuit row r: last i with start[i] <= r (start[0] = 0 <= r), n if
+// r >= start[n]
+__device__ __forceinline__ uint32_t inst_of(const uint64_t* __restrict__ start, uint32_t n, uint64_t r) {
+  if (r >= start[n]) return n;
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (start[mid] <= r) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// d_inst: per instance (circuit start row, pool offset of its rounds' pattern), n + 1 starts
+struct Inst {
+  const uint64_t* start;  // n + 1
+  const uint64_t* pat;    // n: pool offset (u32 units) of the [8][R] pattern
+  uint32_t n;
+};
+
+// mapping of cell (j, r) -> circuit (c', r')
+__device__ __forceinline__ void mapped(const Inst& I, const uint32_t* __restrict__ pool, uint32_t ii,
+                                       uint32_t j, uint64_t r, uint32_t& c2, uint64_t& r2) {
+  if (ii >= I.n) {
+    c2 = j;
+    r2 = r;
+    return;
+  }
+  const uint64_t s = I.start[ii], R = I.start[ii + 1] - s;
+  const uint32_t m = pool[I.pat[ii] + j * R + (r - s)];
+  c2 = m >> ROW_BITS;
+  r2 = s + (m & ((1u << ROW_BITS) - 1));
+}
+
+template <class F>
+__device__ __forceinline__ Fe dw(const Fe* __restrict__ T, const Fe* __restrict__ OH, uint32_t c,
+                                 uint64_t r) {
+  return field::mul<F>(T[c * LO + (uint32_t)(r & (LO - 1))], OH[r >> 10]);
+}
+
+// sigma_j(w^r) for every row r < 2^k (keygen: the permutation polynomials' values)
+template <class F>
+__global__ __launch_bounds__(256) void pm_sigma_kernel(Inst I, const uint32_t* __restrict__ pool,
+                                                       uint64_t n_rows, const Fe* __restrict__ OL,
+                                                       const Fe* __restrict__ OH, bool mont,
+                                                       uint64_t* __restrict__ out, uint64_t out_rows) {
+  const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= n_rows) return;
+  const uint32_t ii = inst_of(I.start, I.n, r);
+#pragma unroll 1
+  for (uint32_t j = 0; j < NCOL; j++) {
+    uint32_t c2;
+    uint64_t r2;
+    mapped(I, pool, ii, j, r, c2, r2);
+    field::store(out + ((uint64_t)j * out_rows + r) * 4, gp::out_form<F>(dw<F>(OL, OH, c2, r2), mont));
+  }
+}
+
+// num/den of the columns [j0, j1) for rows r < usable
+template <class F>
+__global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* __restrict__ pool,
+                                                        const uint32_t* __restrict__ adv,
+                                                        uint64_t total_rows, uint64_t row0,
+                                                        uint64_t usable, uint32_t j0, uint32_t j1,
+                                                        const Fe* __restrict__ BL,
+                                                        const Fe* __restrict__ OH, Params prm_gamma,
+                                                        Fe* __restrict__ num, Fe* __restrict__ den) {
+  const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= usable) return;
+  const Fe gamma = field::to_mont<F>(field::load_words(prm_gamma.beta));  // gamma rides in .beta
+  const uint32_t ii = inst_of(I.start, I.n, r);
+  const uint64_t used = I.start[I.n];
+  Fe n = field::one<F>(), d = field::one<F>();
+#pragma unroll 1
+  for (uint32_t j = j0; j < j1; j++) {
+    // advice column a_{j+1}; cells past the circuit's instances are unassigned (zero)
+    const uint32_t x = r < used ? adv[(uint64_t)(j + 1) * total_rows + row0 + r] : 0u;
+    const Fe vg = field::add<F>(field::from_u32<F>(x), gamma);
+    uint32_t c2;
+    uint64_t r2;
+    mapped(I, pool, ii, j, r, c2, r2);
+    n = field::mul<F>(n, field::add<F>(vg, dw<F>(BL, OH, j, r)));
+    d = field::mul<F>(d, field::add<F>(vg, dw<F>(BL, OH, c2, r2)));
+  }
+  num[r] = n;
+  den[r] = d;
+}
+
+struct Carve {
+  Fe* OL;
+  Fe* BL;
+  Fe* OH;
+  Fe* num;
+  Fe* den;
+  Fe* zn;
+  Fe* zd;
+  Fe* seed;  // NCOL + 1 closing values (seed of set c = closing of set c - 1)
+  size_t total;
+};
+
+Carve carve(void* base, uint32_t k, uint64_t usable) {
+  Carve m;
+  char* p = (char*)base;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    void* r = p ? p + off : nullptr;
+    off += (bytes + 255) & ~(size_t)255;
+    return r;
+  };
+  const uint64_t n_hi = ((1ull << k) + LO - 1) / LO;
+  m.OL = (Fe*)take(sizeof(Fe) * NCOL * LO);
+  m.BL = (Fe*)take(sizeof(Fe) * NCOL * LO);
+  m.OH = (Fe*)take(sizeof(Fe) * n_hi);
+  m.num = (Fe*)take(sizeof(Fe) * usable);
+  m.den = (Fe*)take(sizeof(Fe) * usable);
+  m.zn = (Fe*)take(sizeof(Fe) * gp::n_chunks(usable));
+  m.zd = (Fe*)take(sizeof(Fe) * gp::n_chunks(usable));
+  m.seed = (Fe*)take(sizeof(Fe) * (NCOL + 1));
+  m.total = off;
+  return m;
+}
+
+template <class F>
+hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0, const Inst& I,
+                    const uint32_t* d_pool, uint32_t k, uint64_t usable, const Params& prm,
+                    const uint64_t* gamma, uint32_t chunk_len, bool mont, uint64_t* d_sigma,
+                    uint64_t* d_z, uint64_t out_rows, void* scratch, hipStream_t s) {
+  Carve m = carve(scratch, k, usable);
+  const uint64_t n_rows = 1ull << k, n_hi = n_rows / LO;
+  const uint64_t tab = n_hi > (uint64_t)NCOL * LO ? n_hi : (uint64_t)NCOL * LO;
+  hipLaunchKernelGGL(pm_table_kernel<F>, dim3((uint32_t)((tab + 255) / 256)), dim3(256), 0, s, prm,
+                     n_hi, m.OL, m.BL, m.OH);
+  if (d_sigma)
+    hipLaunchKernelGGL(pm_sigma_kernel<F>, dim3((uint32_t)((n_rows + 255) / 256)), dim3(256), 0, s, I,
+                       d_pool, n_rows, m.OL, m.OH, mont, d_sigma, out_rows);
+  Params pg;
+  for (int i = 0; i < 4; i++) pg.beta[i] = gamma[i];
+  const uint32_t sets = (NCOL + chunk_len - 1) / chunk_len;
+  for (uint32_t c = 0; c < sets; c++) {
+    const uint32_t j0 = c * chunk_len, j1 = j0 + chunk_len < (uint32_t)NCOL ? j0 + chunk_len : NCOL;
+    hipLaunchKernelGGL(pm_factor_kernel<F>, dim3((uint32_t)((usable + 255) / 256)), dim3(256), 0, s, I,
+                       d_pool, d_advice, total_rows, row0, usable, j0, j1, m.BL, m.OH, pg, m.num,
+                       m.den);
+    hipError_t e = gp::run<F>(1, usable, mont, d_z + (uint64_t)c * out_rows * 4, 0, m.num, m.den,
+                              m.zn, m.zd, c ? m.seed + c : nullptr, m.seed + c + 1, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t) {
+  return carve(nullptr, k, usable_rows).total;
+}
+
+// d_inst: n + 1 circuit start rows, then n pool offsets
+hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0,
+                              const uint64_t* d_inst, size_t n_inst, const uint32_t* d_pool,
+                              uint32_t k, uint64_t usable_rows, const uint64_t* omega,
+                              const uint64_t* delta, const uint64_t* beta, const uint64_t* gamma,
+                              uint32_t chunk_len, uint32_t form, uint64_t* d_sigma, uint64_t* d_z,
+                              uint64_t out_rows, void* scratch, hipStream_t s) {
+  Params prm;
+  for (int i = 0; i < 4; i++) {
+    prm.omega[i] = omega[i];
+    prm.delta[i] = delta[i];
+    prm.beta[i] = beta[i];
+  }
+  Inst I;
+  I.start = d_inst;
+  I.pat = d_inst + n_inst + 1;
+  I.n = (uint32_t)n_inst;
+  const bool mont = (form & 1u) != 0;
+  if (form >> 1)
+    return run_perm<field::Bn254>(d_advice, total_rows, row0, I, d_pool, k, usable_rows, prm, gamma,
+                                  chunk_len, mont, d_sigma, d_z, out_rows, scratch, s);
+  return run_perm<field::Pallas>(d_advice, total_rows, row0, I, d_pool, k, usable_rows, prm, gamma,
+                                 chunk_len, mont, d_sigma, d_z, out_rows, scratch, s);
+}
+
+}  // namespace b2f
