@@ -220,6 +220,16 @@ B2F_API int b2f_export_fp_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t t
                               uint64_t row_begin, uint64_t nrows, uint32_t form,
                               uint64_t* d_out, uint64_t out_rows, void* stream);
 
+/* The spread table as the prover's table columns (SpreadTableChip::load, spread_table.rs:470-508;
+ * rows from SpreadTableConfig::generate, spread_table.rs:574-600): column c = 0 tag, 1 dense,
+ * 2 spread, row x < 2^16 holds (tag(x), x, spread(x)), rows 2^16 .. usable_rows - 1 the
+ * layouter's fill_from_row default (row 0's values: zero). Written to
+ * d_out[(c * out_rows + row) * 4 + limb] in `form` (any B2F_FP_*), 2^16 <= usable_rows < 2^32,
+ * out_rows >= usable_rows, d_out 16-byte aligned. Keygen data (halo2 fixes it in the proving
+ * key); the lookup-columns call computes the compressed table internally. Asynchronous. */
+B2F_API int b2f_spread_table_dev(b2f_ctx* ctx, uint64_t usable_rows, uint32_t form, uint64_t* d_out,
+                                 uint64_t out_rows, void* stream);
+
 /* Lookup-argument prover columns of the spread lookup
  * (spread_table.rs:443-453), as halo2_proofs 0.3.0's lookup prover builds them
  * (plonk/lookup/prover.rs: commit_permuted, permute_expression_pair, commit_product), for

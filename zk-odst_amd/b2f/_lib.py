@@ -83,6 +83,7 @@ SIGNATURES = [
     ("b2f_export_fp_dev", I32, [P, P, U64, U64, U64, ctypes.c_uint32, P, U64, P]),
     ("b2f_lookup_columns_dev", I32, [P, P, U64, P, ctypes.c_uint32, U64, P, P, P,
                                      ctypes.c_uint32, P, U64, P, P]),
+    ("b2f_spread_table_dev", I32, [P, U64, ctypes.c_uint32, P, U64, P]),
     ("b2f_permutation_mapping", U64, [ctypes.c_uint32, P, U64]),
     ("b2f_permutation_columns_dev", I32, [P, P, U64, P, SIZE, ctypes.c_uint32, U64, P, P, P, P,
                                           ctypes.c_uint32, ctypes.c_uint32, P, P, U64, P]),

@@ -118,6 +118,20 @@ class Engine:
             int(usable_rows), lim[0], lim[1], lim[2], int(form), _vp(d_out), int(out_rows),
             _vp(d_first_bad), _vp(stream)))
 
+    def spread_table_dev(self, usable_rows, form, d_out, out_rows, stream=0):
+        self._check(self.lib.b2f_spread_table_dev(self.ctx, int(usable_rows), int(form), _vp(d_out),
+                                                  int(out_rows), _vp(stream)))
+
+    def spread_table(self, usable_rows, form=_lib.FP_MONTGOMERY, device="cuda:0", stream=None):
+        """The spread table's three prover columns (tag, dense, spread): int64 tensor
+        [3, usable_rows, 4] of field elements in `form` (b2f_spread_table_dev)."""
+        import torch
+
+        out = torch.empty((3, int(usable_rows), 4), dtype=torch.int64, device=device)
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self.spread_table_dev(usable_rows, form, out.data_ptr(), int(usable_rows), s)
+        return out
+
     def permutation_columns_dev(self, d_adv, total_rows, h_offsets, k, usable_rows, omega, delta,
                                 beta, gamma, chunk_len, form, d_sigma, d_z, out_rows, stream=0):
         """b2f_permutation_columns_dev; h_offsets: host u64 row map of the circuit's instances,

@@ -30,6 +30,8 @@ namespace b2f {
 hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
                             uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
                             int cu_count, hipStream_t s);
+hipError_t launch_spread_table(uint64_t usable_rows, uint32_t form, uint64_t* d_out,
+                               uint64_t out_rows, hipStream_t s);
 
 namespace {
 
@@ -118,7 +120,42 @@ __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
   }
 }
 
+// The spread table as the prover's three table (fixed) columns tag, dense, spread
+// (SpreadTableChip::load, spread_table.rs:470-508: row x < 2^16 holds (tag(x), x, spread(x)),
+// spread_table.rs:574-600), then the layouter's fill_from_row default -- row 0's values,
+// all zero -- up to the usable rows. Two lanes per element, as the export kernel.
+__device__ __forceinline__ uint32_t sp16(uint32_t x) {
+  x = (x | (x << 8)) & 0x00FF00FFu;
+  x = (x | (x << 4)) & 0x0F0F0F0Fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  x = (x | (x << 1)) & 0x55555555u;
+  return x;
+}
+__global__ __launch_bounds__(256) void spread_table_kernel(uint64_t usable_rows, uint32_t form,
+                                                           uint64_t* __restrict__ out,
+                                                           uint64_t out_rows) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // 2 lanes per row
+  const uint64_t row = i >> 1;
+  const uint32_t half = (uint32_t)(i & 1);
+  if (row >= usable_rows) return;
+  const uint32_t x = row < 65536u ? (uint32_t)row : 0u;
+  const uint32_t v[3] = {x < 256u ? 0u : (x < 32768u ? 1u : 2u), x, sp16(x)};
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    u64x2* dst = reinterpret_cast<u64x2*>(out + (uint64_t)c * out_rows * 4);
+    __builtin_nontemporal_store(fp_half(v[c], half, form), dst + 2 * row + half);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_spread_table(uint64_t usable_rows, uint32_t form, uint64_t* d_out,
+                               uint64_t out_rows, hipStream_t s) {
+  const uint64_t lanes = 2 * usable_rows;
+  hipLaunchKernelGGL(spread_table_kernel, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s,
+                     usable_rows, form, d_out, out_rows);
+  return hipGetLastError();
+}
 
 hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
                             uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,

@@ -9,8 +9,12 @@
 // chunk):
 //   gp_chunk:  the chunk's num prefix Nloc_p staged in z[p + 1], the chunk totals of num and
 //              den (2 products per row);
-//   gp_scan:   per product (one workgroup): K_q = seed N_before(q) D_end(q)^-1 per chunk, the
-//              inversion, and the closing value seed N / D (= z[usable]) for a next product;
+//   gp_scan:   K_q = seed N_before(q) D_end(q)^-1 per chunk, the inversion, and the closing
+//              value seed N / D (= z[usable]) for a next product. Up to SCAN_THREADS x 4
+//              chunks one workgroup per product scans them directly; beyond, three levels over
+//              blocks of SCAN_THREADS chunks (gp_block_reduce: block totals; gp_scan over the
+//              block totals; gp_block_down: in-block exclusive prefix / suffix combined with the
+//              block's K), so the serial run per lane stays short at any size;
 //   gp_write:  backward over the chunk: z[p + 1] = K_q Nloc_p prod_{p < i < e} den_i
 //              (2 products per row), converted to the output form.
 // Products are independent along blockIdx.y: product y reads num/den + y * usable and writes
@@ -63,12 +67,11 @@ __global__ __launch_bounds__(256) void gp_chunk(uint64_t usable, uint64_t* __res
 // of the run products in LDS (a prefix for num, a suffix for den), one inversion.
 // seed: Montgomery elements per product (nullptr: 1); closing (nullable) <- seed N / D.
 template <class F>
-__global__ __launch_bounds__(SCAN_THREADS) void gp_scan(uint64_t usable, Fe* __restrict__ zn,
+__global__ __launch_bounds__(SCAN_THREADS) void gp_scan(uint64_t nq, Fe* __restrict__ zn,
                                                         const Fe* __restrict__ zd,
                                                         const Fe* __restrict__ seed,
                                                         Fe* __restrict__ closing) {
   const uint32_t c = blockIdx.x, t = threadIdx.x;
-  const uint64_t nq = n_chunks(usable);
   const uint64_t per = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
   __shared__ Fe sn[SCAN_THREADS], sd[SCAN_THREADS];
   __shared__ Fe dinv;
@@ -111,6 +114,66 @@ __global__ __launch_bounds__(SCAN_THREADS) void gp_scan(uint64_t usable, Fe* __r
   }
 }
 
+// block b of product c: the products of its SCAN_THREADS chunks' zn and zd -> tn/td[c][b]
+template <class F>
+__global__ __launch_bounds__(SCAN_THREADS) void gp_block_reduce(uint64_t nq, const Fe* __restrict__ zn,
+                                                                const Fe* __restrict__ zd,
+                                                                Fe* __restrict__ tn, Fe* __restrict__ td) {
+  const uint32_t b = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
+  const uint64_t nb = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
+  const uint64_t q = (uint64_t)b * SCAN_THREADS + t;
+  __shared__ Fe sn[SCAN_THREADS], sd[SCAN_THREADS];
+  Fe pn = q < nq ? zn[(uint64_t)c * nq + q] : field::one<F>();
+  Fe pd = q < nq ? zd[(uint64_t)c * nq + q] : field::one<F>();
+  for (uint32_t w = SCAN_THREADS / 2; w > 0; w >>= 1) {
+    if (t >= w && t < 2 * w) {
+      sn[t] = pn;
+      sd[t] = pd;
+    }
+    __syncthreads();
+    if (t < w) {
+      pn = field::mul<F>(pn, sn[t + w]);
+      pd = field::mul<F>(pd, sd[t + w]);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    tn[(uint64_t)c * nb + b] = pn;
+    td[(uint64_t)c * nb + b] = pd;
+  }
+}
+
+// K_q = KB[b] * (exclusive in-block prefix of zn) * (exclusive in-block suffix of zd), KB[b] the
+// block's K from gp_scan over the block totals
+template <class F>
+__global__ __launch_bounds__(SCAN_THREADS) void gp_block_down(uint64_t nq, Fe* __restrict__ zn,
+                                                              const Fe* __restrict__ zd,
+                                                              const Fe* __restrict__ kb) {
+  const uint32_t b = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
+  const uint64_t nb = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
+  const uint64_t q = (uint64_t)b * SCAN_THREADS + t;
+  __shared__ Fe sn[SCAN_THREADS], sd[SCAN_THREADS];
+  Fe pn = q < nq ? zn[(uint64_t)c * nq + q] : field::one<F>();
+  Fe pd = q < nq ? zd[(uint64_t)c * nq + q] : field::one<F>();
+  sn[t] = pn;
+  sd[t] = pd;
+  __syncthreads();
+  for (int off = 1; off < SCAN_THREADS; off <<= 1) {  // inclusive prefix of sn, suffix of sd
+    Fe xn = pn, xd = pd;
+    if (t >= (uint32_t)off) xn = field::mul<F>(sn[t - off], pn);
+    if (t + off < (uint32_t)SCAN_THREADS) xd = field::mul<F>(pd, sd[t + off]);
+    __syncthreads();
+    sn[t] = pn = xn;
+    sd[t] = pd = xd;
+    __syncthreads();
+  }
+  if (q >= nq) return;
+  Fe k = kb[(uint64_t)c * nb + b];
+  if (t) k = field::mul<F>(k, sn[t - 1]);
+  if (t + 1 < (uint32_t)SCAN_THREADS) k = field::mul<F>(k, sd[t + 1]);
+  zn[(uint64_t)c * nq + q] = k;
+}
+
 template <class F>
 __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint64_t* __restrict__ z_base,
                                                 uint64_t z_stride, const Fe* __restrict__ den,
@@ -131,16 +194,32 @@ __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint
   }
 }
 
-// The three passes for `g` independent products on `s`. zn, zd: scratch of g * n_chunks
-// elements each.
+// Scratch (Fe elements) gp::run needs per product: chunk products, and block totals + K.
+__host__ __device__ inline uint64_t scratch_elems(uint64_t usable) {
+  const uint64_t nq = n_chunks(usable), nb = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
+  return 2 * nq + 2 * nb;
+}
+
+// The passes for `g` independent products on `s`. zs: scratch of g * scratch_elems(usable).
 template <class F>
 hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_t z_stride,
-               const Fe* num, const Fe* den, Fe* zn, Fe* zd, const Fe* seed, Fe* closing,
-               hipStream_t s) {
-  const uint32_t zq = (uint32_t)((n_chunks(usable) + 255) / 256);
+               const Fe* num, const Fe* den, Fe* zs, const Fe* seed, Fe* closing, hipStream_t s) {
+  const uint64_t nq = n_chunks(usable), nb = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
+  Fe* zn = zs;
+  Fe* zd = zs + (uint64_t)g * nq;
+  Fe* tn = zd + (uint64_t)g * nq;
+  Fe* td = tn + (uint64_t)g * nb;
+  const uint32_t zq = (uint32_t)((nq + 255) / 256);
   hipLaunchKernelGGL(gp_chunk<F>, dim3(zq, g), dim3(256), 0, s, usable, z_base, z_stride, num, den,
                      zn, zd);
-  hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, usable, zn, zd, seed, closing);
+  if (nq <= 4ull * SCAN_THREADS) {
+    hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, seed, closing);
+  } else {
+    hipLaunchKernelGGL(gp_block_reduce<F>, dim3((uint32_t)nb, g), dim3(SCAN_THREADS), 0, s, nq, zn, zd,
+                       tn, td);
+    hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, tn, td, seed, closing);
+    hipLaunchKernelGGL(gp_block_down<F>, dim3((uint32_t)nb, g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, tn);
+  }
   hipLaunchKernelGGL(gp_write<F>, dim3(zq, g), dim3(256), 0, s, usable, mont, z_base, z_stride, den,
                      zn, seed);
   return hipGetLastError();

@@ -39,6 +39,8 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
                          void* scratch, uint32_t group, hipStream_t s);
+hipError_t launch_spread_table(uint64_t usable_rows, uint32_t form, uint64_t* d_out,
+                               uint64_t out_rows, hipStream_t s);
 size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst);
 hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0,
                               const uint64_t* d_inst, size_t n_inst, const uint32_t* d_pool,
@@ -1305,6 +1307,21 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
   int tk = timed_begin(ctx, B2F_KERNEL_LOOKUP, s);
   HIPCHK(ctx, launch_lookup(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, theta, beta,
                             gamma, form, d_out, out_rows, d_first_bad, ctx->d_lk, group, s));
+  timed_end(ctx, tk, s);
+  return B2F_OK;
+}
+
+B2F_API int b2f_spread_table_dev(b2f_ctx* ctx, uint64_t usable_rows, uint32_t form, uint64_t* d_out,
+                                 uint64_t out_rows, void* stream) {
+  if (!ctx) return B2F_ERR_ARG;
+  if (!d_out || ((uintptr_t)d_out & 15)) return set_err(ctx, B2F_ERR_ARG, "spread table: d_out null or unaligned");
+  if (form > B2F_FP_BN254_MONTGOMERY) return set_err(ctx, B2F_ERR_ARG, "spread table: unknown form %u", form);
+  if (usable_rows < (1ull << 16) || usable_rows >= (1ull << 32) || out_rows < usable_rows)
+    return set_err(ctx, B2F_ERR_ROWS, "spread table: need 2^16 <= usable_rows < 2^32, out_rows >= usable_rows");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  int tk = timed_begin(ctx, B2F_KERNEL_EXPORT, s);
+  HIPCHK(ctx, launch_spread_table(usable_rows, form, d_out, out_rows, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }

@@ -278,8 +278,7 @@ struct Carve {
   uint32_t* samp;  // group x 2 x SAMPLE
   Fe* num;  // group x usable
   Fe* den;
-  Fe* zn;  // group x nq
-  Fe* zd;
+  Fe* zs;  // group x gp::scratch_elems
   void* sort_tmp;
   size_t sort_bytes;
   size_t total;
@@ -301,7 +300,6 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
     off += (bytes + 255) & ~(size_t)255;
     return r;
   };
-  const uint64_t nq = (usable + ZC - 1) / ZC;
   k.Tx = (Fe*)take(sizeof(Fe) * TROWS);
   k.Ts = (Fe*)take(sizeof(Fe) * TROWS);
   k.key = (uint64_t*)take(8ull * 4 * TROWS);
@@ -316,8 +314,7 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.samp = (uint32_t*)take(8ull * SAMPLE * group);
   k.num = (Fe*)take(sizeof(Fe) * usable * group);
   k.den = (Fe*)take(sizeof(Fe) * usable * group);
-  k.zn = (Fe*)take(sizeof(Fe) * nq * group);
-  k.zd = (Fe*)take(sizeof(Fe) * nq * group);
+  k.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * group);
   k.sort_bytes = sort_temp_bytes();
   k.sort_tmp = take(k.sort_bytes);
   k.total = off;
@@ -364,7 +361,7 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
                        d_row_begin, c0, usable_rows, k.Tx, k.Ts, k.pos, k.dcnt, k.lp, k.samp, mont,
                        d_out, out_rows, ch, k.num, k.den);
     e = gp::run<F>(g, usable_rows, mont, d_out + ((uint64_t)c0 * 5 + 4) * out_rows * 4,
-                   5 * out_rows * 4, k.num, k.den, k.zn, k.zd, nullptr, nullptr, s);
+                   5 * out_rows * 4, k.num, k.den, k.zs, nullptr, nullptr, s);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

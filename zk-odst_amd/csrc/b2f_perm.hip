@@ -164,8 +164,7 @@ struct Carve {
   Fe* OH;
   Fe* num;
   Fe* den;
-  Fe* zn;
-  Fe* zd;
+  Fe* zs;
   Fe* seed;  // NCOL + 1 closing values (seed of set c = closing of set c - 1)
   size_t total;
 };
@@ -185,8 +184,7 @@ Carve carve(void* base, uint32_t k, uint64_t usable) {
   m.OH = (Fe*)take(sizeof(Fe) * n_hi);
   m.num = (Fe*)take(sizeof(Fe) * usable);
   m.den = (Fe*)take(sizeof(Fe) * usable);
-  m.zn = (Fe*)take(sizeof(Fe) * gp::n_chunks(usable));
-  m.zd = (Fe*)take(sizeof(Fe) * gp::n_chunks(usable));
+  m.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable));
   m.seed = (Fe*)take(sizeof(Fe) * (NCOL + 1));
   m.total = off;
   return m;
@@ -214,7 +212,7 @@ hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0
                        d_pool, d_advice, total_rows, row0, usable, j0, j1, m.BL, m.OH, pg, m.num,
                        m.den);
     hipError_t e = gp::run<F>(1, usable, mont, d_z + (uint64_t)c * out_rows * 4, 0, m.num, m.den,
-                              m.zn, m.zd, c ? m.seed + c : nullptr, m.seed + c + 1, s);
+                              m.zs, c ? m.seed + c : nullptr, m.seed + c + 1, s);
     if (e != hipSuccess) return e;
   }
   return hipGetLastError();
