@@ -1,0 +1,42 @@
+"""Average FETCH_SIZE / WRITE_SIZE per dispatch, per kernel name (template arguments kept), from
+rocprofv3 --pmc counter_collection CSVs, with the gfx950 correction of MI355X_MICROARCH.md
+(FETCH_SIZE x2 for wide streaming reads; KiB -> bytes).
+    python tools/pmc_fetch_by_kernel.py <dir> [name-substring ...]"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main():
+    d = sys.argv[1]
+    want = sys.argv[2:]
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    names = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "")
+            if want and not any(w in k for w in want):
+                continue
+            acc[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+            names[r["Dispatch_Id"]] = k
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for disp, ctr in acc.items():
+        for c, v in ctr.items():
+            per[names[disp]][c].append(v)
+    out = {}
+    for k, ctr in per.items():
+        o = {}
+        for c, vs in ctr.items():
+            kib = sum(vs) / len(vs)
+            o[c + "_kib_raw"] = kib
+            o[c + "_bytes_corrected"] = kib * 1024 * (2.0 if c == "FETCH_SIZE" else 1.0)
+            o["dispatches"] = len(vs)
+        out[k] = o
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
