@@ -17,7 +17,7 @@ def main():
     names = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "")
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
             if want and not any(w in k for w in want):
                 continue
             acc[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])

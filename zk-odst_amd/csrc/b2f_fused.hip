@@ -597,6 +597,144 @@ __device__ __forceinline__ void edge_tile(uint32_t* S, uint32_t* accw, const uin
     }
 }
 
+// Failure bookkeeping of a half-round tile's checks. REC = false: every check is evaluated and
+// only "some check failed" is kept (a flag, no branch around the bookkeeping: the common case,
+// a valid trace); REC = true: every failure is recorded exactly as the eval kernel records it
+// (counters, first failing row, deferred rows) -- run only when the fast pass flagged the tile.
+template <bool REC>
+struct Fails {
+  EvalAcc A;
+  bool bad;
+  __device__ __forceinline__ void fail(bool cond, uint64_t row, uint32_t code) {
+    if (REC) {
+      if (cond) A.fail(row, code);
+    } else {
+      bad |= cond;
+    }
+  }
+  __device__ __forceinline__ void gates(bool cond, uint64_t row, uint32_t mask) {
+    if (REC) {
+      if (cond) A.fail_gates(row, mask);
+    } else {
+      bad |= cond;
+    }
+  }
+};
+
+// message words (the last use of the loaded operands): a1 (x) at +0 and a2 (y) at +28 of
+// every G, lanes 0..31
+template <int MODE, bool REC>
+__device__ __forceinline__ void hr_msg_copies(Fails<REC>& F, const WaveTile& T, uint32_t lane,
+                                              const Ctx& c, const Ops& P, const uint8_t* Sg,
+                                              const Inject& inj) {
+  if ((MODE & FZ_COPIES) && lane < 32) {
+    const uint32_t mg = lane >> 3, which = (lane >> 2) & 1u, k = lane & 3u;
+    const uint32_t dr = 52 * mg + (which ? 28u : 0u) + k;
+    uint32_t sv = limb(P.w[6], k);
+    if (MODE & FZ_INJECT) {
+      const uint32_t g = mg + 4 * (c.hr & 1u);
+      const uint32_t mj = Sg[16 * ((c.hr >> 1) % 10) + 2 * g + which];
+      sv ^= inj_at(inj, c.off + 32 + 4 * mj + k, A1);
+    }
+    F.fail(T.at(A5, dr) != sv, c.row0 + dr, B2F_CODE_COPY);
+  }
+}
+
+// lookups, the fixed column, the canonical gate passes and the copies of a half-round tile
+template <int MODE, bool REC>
+__device__ __forceinline__ void hr_checks(Fails<REC>& F, const WaveTile& T, uint32_t lane,
+                                          const Ctx& c, const uint32_t* L, const uint64_t* prod,
+                                          const Inject& inj, uint64_t* defer, uint32_t defer_cap) {
+  const uint32_t nq = c.nq;
+  const bool qlane = lane < nq;
+  const uint64_t qrow = c.row0 + 4ull * lane;
+  const uint32_t gg = lane / G_QUADS, p = lane - G_QUADS * gg;
+  if (qlane) {
+    const uint4 fx = T.quad(FXC, 4 * lane);
+    const uint32_t xs = expected_sel(p);
+    if (MODE & FZ_LOOKUP) {
+      const uint4 q0 = T.quad(A0, 4 * lane), q1 = T.quad(A1, 4 * lane), q2 = T.quad(A2, 4 * lane);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t tg = comp(q0, j), de = comp(q1, j), sp = comp(q2, j);
+        F.fail(!(de < 65536u && tg == tag16(de) && sp == spread16(de & 0xffffu)), qrow + j, B2F_CODE_LOOKUP);
+      }
+    }
+    if (MODE & FZ_GATES) {
+      if (REC) {
+        const bool canon = (fx.x & 0xffffu) == xs && ((fx.y | fx.z | fx.w) & 0xffffu) == 0;
+        check_fixed(F.A, fx, make_uint4(xs, 0, 0, 0), qrow);
+        if (!canon) defer_rows(fx, qrow, defer, defer_cap);
+      } else {
+        F.bad |= ((fx.x ^ xs) | fx.y | fx.z | fx.w) != 0;  // any fixed cell off the structure
+      }
+    }
+  }
+  if (MODE & FZ_GATES) {
+    // canonical blocks, one kind per pass so each pass is one evaluator: the adds
+    // (lanes 0-15: a1 +0, c1 +12, a2 +28, c2 +40 of G lane / 4), the XORs (lanes 0-7:
+    // d1 +4, d2 +32 of G lane / 2), XOR24 limbs (lanes 0-15: b1 + efgh at +16, limb
+    // lane % 4, OR-combined over the DPP quad) and XOR63 limbs (b2 + ijkl at +44)
+    const uint32_t w4 = lane & 3u;
+    auto canon_block = [&](uint32_t r, uint32_t want) {
+      const uint4 bf = T.quad(FXC, r);  // the block's first quad
+      return (bf.x & 0xffffu) == want && ((bf.y | bf.z | bf.w) & 0xffffu) == 0;
+    };
+    if (lane < 16) {
+      const uint32_t r = 52 * (lane >> 2) + (w4 == 0 ? 0u : w4 == 1 ? 12u : w4 == 2 ? 28u : 40u);
+      const uint32_t want = 1u << (w4 == 0 ? S_A1 : w4 == 1 ? S_C1 : w4 == 2 ? S_A2 : S_C2);
+      F.gates(canon_block(r, want) && !g_add(T, r, T.at(A9, r), (w4 & 1u) == 0), c.row0 + r, want);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 8) {
+      const uint32_t r = 52 * (lane >> 1) + ((lane & 1u) ? 32u : 4u);
+      const uint32_t want = 1u << ((lane & 1u) ? S_D2 : S_D1);
+      F.gates(canon_block(r, want) && !g_xor(T, r, false), c.row0 + r, want);
+    }
+    __builtin_amdgcn_wave_barrier();
+    {
+      const uint32_t r = 52 * ((lane >> 2) & 3u) + 16;
+      const uint32_t want = (1u << S_B1) | (1u << S_EFGH);
+      const bool take = lane < 16 && canon_block(r, want);
+      const uint32_t qb = quad_or(take ? g_xor24_limb(T, r, w4) : 0u);
+      F.gates(take && w4 == 0 && qb, c.row0 + r,
+              ((qb & 1u) ? 1u << S_B1 : 0u) | ((qb & 2u) ? 1u << S_EFGH : 0u));
+    }
+    __builtin_amdgcn_wave_barrier();
+    {
+      const uint32_t r = 52 * ((lane >> 2) & 3u) + 44;
+      const uint32_t want = (1u << S_B2) | (1u << S_IJKL);
+      const bool take = lane < 16 && canon_block(r, want);
+      const uint32_t qb = quad_or(take ? g_xor63_limb(T, r, w4) : 0u);
+      F.gates(take && w4 == 0 && qb, c.row0 + r,
+              ((qb & 1u) ? 1u << S_B2 : 0u) | ((qb & 2u) ? 1u << S_IJKL : 0u));
+    }
+  }
+  if (MODE & FZ_COPIES) {
+    const uint32_t* ct = L + L_CT + (c.hr & 1u) * HR_CHECKS;
+#pragma unroll
+    for (int it = 0; it < HR_CHECKS / FW; it++) {
+      const uint32_t e = ct[it * FW + lane];
+      const uint32_t dr = e & 255u, dc = (e >> 8) & 3u;
+      const uint32_t dv = T.at(A3 + (int)dc, dr);
+      uint32_t sv;
+      if (!((e >> 10) & 1u)) {
+        sv = T.at(wcol((e >> 19) & 3u), (e >> 11) & 255u);
+      } else {
+        const uint32_t w = (e >> 11) & 15u, k = (e >> 15) & 3u, sp = (e >> 17) & 1u;
+        const uint32_t lv = limb(prod[w], k);
+        sv = sp ? spread16(lv) : lv;
+        if (MODE & FZ_INJECT) {
+          uint32_t col = 0;
+          const uint32_t sr = state_src(w, k, sp, c.hr, col);
+          sv ^= inj_at(inj, c.off + sr, col);
+        }
+      }
+      F.fail(dv != sv, c.row0 + dr, B2F_CODE_COPY);
+    }
+  }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES, B2F_FUSED_WAVES)
 fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
@@ -671,97 +809,19 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
         tick(2);  // cells computed and staged
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staging is complete
         __builtin_amdgcn_wave_barrier();
-        if ((MODE & FZ_COPIES) && lane < 32) {
-          // message words (the last use of the loaded operands, so before the stores): a1 (x)
-          // at +0 and a2 (y) at +28 of every G
-          const uint32_t mg = lane >> 3, which = (lane >> 2) & 1u, k = lane & 3u;
-          const uint32_t dr = 52 * mg + (which ? 28u : 0u) + k;
-          uint32_t sv = limb(P.w[6], k);
-          if (MODE & FZ_INJECT) {
-            const uint32_t g = mg + 4 * (c.hr & 1u);
-            const uint32_t mj = Sg[16 * ((c.hr >> 1) % 10) + 2 * g + which];
-            sv ^= inj_at(inj, c.off + 32 + 4 * mj + k, A1);
-          }
-          if (T.at(A5, dr) != sv) A.fail(c.row0 + dr, B2F_CODE_COPY);
-        }
+        Fails<false> F{A, false};
+        hr_msg_copies<MODE, false>(F, T, lane, c, P, Sg, inj);
         tick(3);  // staging visible, message copies
         settle(Pn);
         tick(4);  // the next tile's operands arrived
         store_staged<MODE>(S, lane, nq, c.row0, adv, fixed, total_rows);
         tick(5);  // stores issued
-        if (qlane) {
-          const uint4 fx = T.quad(FXC, 4 * lane);
-          const bool canon = (fx.x & 0xffffu) == expected_sel(p) && ((fx.y | fx.z | fx.w) & 0xffffu) == 0;
-          if (MODE & FZ_LOOKUP) check_lookups(A, T.quad(A0, 4 * lane), T.quad(A1, 4 * lane), T.quad(A2, 4 * lane), qrow);
-          if (MODE & FZ_GATES) {
-            check_fixed(A, fx, make_uint4(expected_sel(p), 0, 0, 0), qrow);
-            if (!canon) defer_rows(fx, qrow, defer, defer_cap);
-          }
-        }
-        if (MODE & FZ_GATES) {
-          // canonical blocks, one kind per pass so each pass is one evaluator: the adds
-          // (lanes 0-15: a1 +0, c1 +12, a2 +28, c2 +40 of G lane / 4), the XORs (lanes 0-7:
-          // d1 +4, d2 +32 of G lane / 2), XOR24 limbs (lanes 0-15: b1 + efgh at +16, limb
-          // lane % 4, OR-combined over the DPP quad) and XOR63 limbs (b2 + ijkl at +44)
-          const uint32_t w4 = lane & 3u;
-          auto canon_block = [&](uint32_t r, uint32_t want) {
-            const uint4 bf = T.quad(FXC, r);  // the block's first quad
-            return (bf.x & 0xffffu) == want && ((bf.y | bf.z | bf.w) & 0xffffu) == 0;
-          };
-          if (lane < 16) {
-            const uint32_t r = 52 * (lane >> 2) + (w4 == 0 ? 0u : w4 == 1 ? 12u : w4 == 2 ? 28u : 40u);
-            const uint32_t want = 1u << (w4 == 0 ? S_A1 : w4 == 1 ? S_C1 : w4 == 2 ? S_A2 : S_C2);
-            if (canon_block(r, want) && !g_add(T, r, T.at(A9, r), (w4 & 1u) == 0))
-              A.fail_gates(c.row0 + r, want);
-          }
-          __builtin_amdgcn_wave_barrier();
-          if (lane < 8) {
-            const uint32_t r = 52 * (lane >> 1) + ((lane & 1u) ? 32u : 4u);
-            const uint32_t want = 1u << ((lane & 1u) ? S_D2 : S_D1);
-            if (canon_block(r, want) && !g_xor(T, r, false)) A.fail_gates(c.row0 + r, want);
-          }
-          __builtin_amdgcn_wave_barrier();
-          {
-            const uint32_t r = 52 * ((lane >> 2) & 3u) + 16;
-            const uint32_t want = (1u << S_B1) | (1u << S_EFGH);
-            const bool take = lane < 16 && canon_block(r, want);
-            const uint32_t qb = quad_or(take ? g_xor24_limb(T, r, w4) : 0u);
-            if (take && w4 == 0 && qb)
-              A.fail_gates(c.row0 + r, ((qb & 1u) ? 1u << S_B1 : 0u) | ((qb & 2u) ? 1u << S_EFGH : 0u));
-          }
-          __builtin_amdgcn_wave_barrier();
-          {
-            const uint32_t r = 52 * ((lane >> 2) & 3u) + 44;
-            const uint32_t want = (1u << S_B2) | (1u << S_IJKL);
-            const bool take = lane < 16 && canon_block(r, want);
-            const uint32_t qb = quad_or(take ? g_xor63_limb(T, r, w4) : 0u);
-            if (take && w4 == 0 && qb)
-              A.fail_gates(c.row0 + r, ((qb & 1u) ? 1u << S_B2 : 0u) | ((qb & 2u) ? 1u << S_IJKL : 0u));
-          }
-        }
-        tick(6);  // lookups, fixed column, gates
-        if (MODE & FZ_COPIES) {
-          const uint32_t* ct = L + L_CT + (c.hr & 1u) * HR_CHECKS;
-#pragma unroll
-          for (int it = 0; it < HR_CHECKS / FW; it++) {
-            const uint32_t e = ct[it * FW + lane];
-            const uint32_t dr = e & 255u, dc = (e >> 8) & 3u;
-            const uint32_t dv = T.at(A3 + (int)dc, dr);
-            uint32_t sv;
-            if (!((e >> 10) & 1u)) {
-              sv = T.at(wcol((e >> 19) & 3u), (e >> 11) & 255u);
-            } else {
-              const uint32_t w = (e >> 11) & 15u, k = (e >> 15) & 3u, sp = (e >> 17) & 1u;
-              const uint32_t lv = limb(prod[w], k);
-              sv = sp ? spread16(lv) : lv;
-              if (MODE & FZ_INJECT) {
-                uint32_t col = 0;
-                const uint32_t sr = state_src(w, k, sp, c.hr, col);
-                sv ^= inj_at(inj, c.off + sr, col);
-              }
-            }
-            if (dv != sv) A.fail(c.row0 + dr, B2F_CODE_COPY);
-          }
+        hr_checks<MODE, false>(F, T, lane, c, L, prod, inj, defer, defer_cap);
+        tick(6);  // lookups, fixed column, gates, copies
+        if (__builtin_amdgcn_ballot_w64(F.bad)) {  // rare: a failure in this tile, record it exactly
+          Fails<true> R{A, false};
+          hr_msg_copies<MODE, true>(R, T, lane, c, P, Sg, inj);
+          hr_checks<MODE, true>(R, T, lane, c, L, prod, inj, defer, defer_cap);
         }
       } else if (c.kind == T_INIT || c.kind == T_FINAL) {
         settle(Pn);
