@@ -353,6 +353,7 @@ template <int MODE>
 __device__ __forceinline__ void store_staged(const uint32_t* S, uint32_t lane, uint32_t nq, uint64_t row0,
                                              uint32_t* adv, uint32_t* fixed, uint64_t total_rows) {
   if (!(MODE & FZ_STORE)) return;
+
   const uint32_t l = lane < nq ? lane : 0;
 #pragma unroll
   for (int col = 0; col < NSTAGE; col++)
@@ -735,8 +736,15 @@ __device__ __forceinline__ void hr_checks(Fails<REC>& F, const WaveTile& T, uint
   }
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(FW * WAVES, B2F_FUSED_WAVES)
+// PART: the tiles one launch walks. PART_HR: the half-round tiles (96 % of the quads) -- the
+// init / final / zero-row paths compiled out, so this kernel's register budget is the
+// half-round path's alone (no spills: a spill reload is a vector memory load, which would wait
+// for every store the wave has in flight); PART_EDGE: the init and final tiles and the zero
+// rows past the last instance. Both walk their own descriptor list (tile_desc_kernel).
+enum { PART_HR = 1, PART_EDGE = 2 };
+
+template <int MODE, int PART>
+__global__ void __launch_bounds__(FW * WAVES, PART == PART_HR ? B2F_FUSED_WAVES : 3)
 fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
              uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
              uint32_t* __restrict__ fixed, const TileDesc* __restrict__ desc,
@@ -770,27 +778,34 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
 
   if (*status == 0) {  // the record kernel accepted the layout
     const uint64_t used_rows = off[n];
-    const uint64_t t_inst = (used_rows - (uint64_t)FIXED_ROWS * n) / 208 + 2ull * n;
-    const uint64_t t_all = t_inst + ((total_rows - used_rows) / 4 + PAD_Q - 1) / PAD_Q;
+    const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
+    const uint64_t t_inst = PART == PART_HR ? n_hr : 2ull * n;
+    const uint64_t t_all = PART == PART_HR ? n_hr : t_inst + ((total_rows - used_rows) / 4 + PAD_Q - 1) / PAD_Q;
     const uint64_t W = (uint64_t)gridDim.x * WAVES;
     // wave-uniform tile index: descriptors come in by scalar loads (lgkmcnt), never queued
     // behind the wave's vector stores
     uint64_t t = (uint64_t)blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(wv);
 
+    const TileDesc* dsc = PART == PART_EDGE ? desc + n_hr : desc;  // this part's list
     auto raw_desc = [&](uint64_t tt) -> uint4 {
       const uint64_t ti = tt < t_inst ? tt : 0;
-      const uint4 v = desc[ti].v;
+      const uint4 v = dsc[ti].v;
       return tt < t_inst ? v : make_uint4(0, 0, 0, 0);
     };
     // software pipeline: operands one tile ahead, descriptors two tiles ahead (every load of
     // an iteration is issued before its stores: vmcnt retires loads and stores in order)
-    Ctx c = make_ctx(t, t_inst, raw_desc(t), used_rows, total_rows);
+    auto ctx_of = [&](uint64_t tt, const uint4& raw) {
+      Ctx k = make_ctx(tt, t_inst, raw, used_rows, total_rows);
+      if (PART == PART_HR) k.kind = T_HR;  // lets the compiler drop the other tile kinds' paths
+      return k;
+    };
+    Ctx c = ctx_of(t, raw_desc(t));
     Ops P{};
     if (t < t_all) P = load_ops(c, lane, in, rec, Sg);
     uint4 dn = raw_desc(t + W);
     for (; t < t_all; t += W) {
       tick(-1);
-      const Ctx cn = make_ctx(t + W, t_inst, dn, used_rows, total_rows);
+      const Ctx cn = ctx_of(t + W, dn);
       const Ops Pn = load_ops(cn, lane, in, rec, Sg);  // past the end: harmless loads
       dn = raw_desc(t + 2 * W);
       tick(0);  // next tile's context and loads issued
@@ -823,12 +838,12 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
           hr_msg_copies<MODE, true>(R, T, lane, c, P, Sg, inj);
           hr_checks<MODE, true>(R, T, lane, c, L, prod, inj, defer, defer_cap);
         }
-      } else if (c.kind == T_INIT || c.kind == T_FINAL) {
+      } else if (PART == PART_EDGE && (c.kind == T_INIT || c.kind == T_FINAL)) {
         settle(Pn);
 #ifndef B2F_FZ_NOEDGE  // diagnostics: the register budget of the half-round path alone
         edge_tile<MODE>(S, L + L_ACC, IV, inj, adv, fixed, total_rows, defer, defer_cap, c, P, lane);
 #endif
-      } else {
+      } else if (PART == PART_EDGE) {
         // ---- the zero rows past the last instance: written and checked from registers (a
         // selector here can only come from the test hook, and its gate is deferred)
         Quad Q;
@@ -890,10 +905,12 @@ __global__ void tile_desc_kernel(const uint64_t* __restrict__ off, const b2f_inp
   if (i >= n || *status) return;
   const uint32_t rounds = in[i].rounds;
   const uint64_t st = 2 * ((off[i] - (uint64_t)FIXED_ROWS * i) / ROUND_ROWS) + i;
-  const uint64_t t0 = st + i;
-  for (uint32_t j = 0; j <= 2 * rounds + 1; j++) {
-    desc[t0 + j].v = make_uint4(i, j, rounds, (uint32_t)st);
-  }
+  // the half-round tiles first (instance i's at 2 sum(rounds before i) = st - i), then the
+  // init / final pairs (at n_hr + 2 i)
+  const uint64_t n_hr = (off[n] - (uint64_t)FIXED_ROWS * n) / 208;
+  for (uint32_t j = 1; j <= 2 * rounds; j++) desc[st - i + j - 1].v = make_uint4(i, j, rounds, (uint32_t)st);
+  desc[n_hr + 2ull * i].v = make_uint4(i, 0, rounds, (uint32_t)st);
+  desc[n_hr + 2ull * i + 1].v = make_uint4(i, 2 * rounds + 1, rounds, (uint32_t)st);
 }
 
 // Gates of selector rows the fused kernel deferred (their gate reads rows past the tile that
@@ -955,21 +972,33 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
 #endif
   if (inj_row != ~0ull) mode |= FZ_INJECT;
   // persistent grid: the workgroups that are resident at once (VGPRs and LDS bound them)
-  static int per_cu = 0;
-  if (!per_cu) {
+  static int per_cu[2] = {0, 0};
+  if (!per_cu[0]) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fused_kernel<FZ_FULL>, FW * WAVES, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fused_kernel<FZ_FULL, PART_HR>, FW * WAVES, 0) !=
             hipSuccess || nb < 1)
       nb = 2;
-    per_cu = nb;
+    per_cu[0] = nb;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fused_kernel<FZ_FULL, PART_EDGE>, FW * WAVES, 0) !=
+            hipSuccess || nb < 1)
+      nb = 2;
+    per_cu[1] = nb;
   }
-  const uint32_t grid = (uint32_t)(cu_count * per_cu);
+  // the edge tiles: 2 per instance plus the zero rows; no more workgroups than they fill
+  const uint64_t edge_tiles = 2ull * n + ((total_rows / 4) + PAD_Q - 1) / PAD_Q;
+  const uint64_t edge_wgs = (edge_tiles + WAVES - 1) / WAVES;
+  const uint32_t grid = (uint32_t)(cu_count * per_cu[0]);
+  const uint32_t grid_e = (uint32_t)(edge_wgs < (uint64_t)cu_count * per_cu[1] ? edge_wgs : (uint64_t)cu_count * per_cu[1]);
+  const TileDesc* desc_e = desc;  // the kernels offset the edge list themselves (n_hr is on the device)
   switch (mode) {
-#define B2F_FUSED(M)                                                                          \
-  case M:                                                                                     \
-    hipLaunchKernelGGL(fused_kernel<M>, dim3(grid), dim3(FW * WAVES), 0, s, d_in, n, d_off,   \
-                       total_rows, rec, d_adv, d_fixed, desc, d_rep, d_status, inj, defer,    \
-                       DEFER_CAP, clk);                                                       \
+#define B2F_FUSED(M)                                                                               \
+  case M:                                                                                          \
+    hipLaunchKernelGGL((fused_kernel<M, PART_HR>), dim3(grid), dim3(FW * WAVES), 0, s, d_in, n,     \
+                       d_off, total_rows, rec, d_adv, d_fixed, desc, d_rep, d_status, inj, defer,  \
+                       DEFER_CAP, clk);                                                            \
+    hipLaunchKernelGGL((fused_kernel<M, PART_EDGE>), dim3(grid_e), dim3(FW * WAVES), 0, s, d_in, n, \
+                       d_off, total_rows, rec, d_adv, d_fixed, desc_e, d_rep, d_status, inj, defer, \
+                       DEFER_CAP, clk);                                                            \
     break;
 #ifdef B2F_DIAG
     B2F_FUSED(0) B2F_FUSED(2) B2F_FUSED(3) B2F_FUSED(10) B2F_FUSED(18) B2F_FUSED(8) B2F_FUSED(16)
