@@ -26,6 +26,7 @@ def per_kernel(d, counter):
                 continue
             k = r["Kernel_Name"]
             kind = ("fill" if "fill_kernel" in k else "eval" if "eval_kernel" in k
+                    else "fill_eval_edge" if "fused_kernel<27, 2>" in k
                     else "fill_eval" if "fused_kernel" in k else None)
             if kind is None:
                 continue
@@ -41,6 +42,10 @@ def main():
     out = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
     fetch = per_kernel(fetch_dir, "FETCH_SIZE")
     write = per_kernel(write_dir, "WRITE_SIZE")
+    # the fused path is two launches per step (half-round tiles, then init/final/zero tiles)
+    for d in (fetch, write):
+        if "fill_eval_edge" in d:
+            d["fill_eval"] = d.get("fill_eval", 0.0) + d.pop("fill_eval_edge")
     res = json.load(open(out)) if os.path.exists(out) else {}
     for kind in ("fill", "eval", "fill_eval"):
         if kind not in fetch or kind not in write:
