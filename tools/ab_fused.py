@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 18)
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--eval", action="store_true", help="also time each variant's eval kernel")
     args = ap.parse_args()
     import torch
 
@@ -44,6 +45,12 @@ def main():
         kt = prod.kernel_times()
         res.setdefault("split(fill+eval)", []).append(kt["fill"][0] + kt["eval"][0] + kt["record"][0])
         for name, eng in engines:
+            if args.eval:
+                eng.set_timing(True)
+                batch.evaluate(eng, s)
+                kt = eng.kernel_times()
+                res.setdefault("%s/eval" % name, []).append(kt["eval"][0])
+                eng.sync(s)
             for m in modes if name != "product" else ["27"]:
                 os.environ["B2F_DIAG_FUSED"] = m
                 eng.set_timing(True)

@@ -774,6 +774,31 @@ struct EvalAcc {
 };
 static_assert(B2F_CODE_FIXED == 18, "the fixed-column counter is word 18 of the accumulator");
 
+// Failure bookkeeping of a half-round tile's checks. REC = false: every check is evaluated and
+// only "some check failed" is kept (a flag, no branch around the bookkeeping: the common case,
+// a valid trace); REC = true: every failure is recorded exactly as the eval kernel records it
+// (counters, first failing row, deferred rows) -- run only when the fast pass flagged the tile.
+template <bool REC>
+struct Fails {
+  EvalAcc A;
+  bool bad;
+  __device__ __forceinline__ void fail(bool cond, uint64_t row, uint32_t code) {
+    if (REC) {
+      if (cond) A.fail(row, code);
+    } else {
+      bad |= cond;
+    }
+  }
+  __device__ __forceinline__ void gates(bool cond, uint64_t row, uint32_t mask) {
+    if (REC) {
+      if (cond) A.fail_gates(row, mask);
+    } else {
+      bad |= cond;
+    }
+  }
+};
+
+
 // A workgroup's counters into the report: one global atomic per non-zero counter (call after
 // a barrier, every thread of the workgroup).
 __device__ __forceinline__ void flush_report(const EvalAcc& A, b2f_eval_report* rep, int tid) {
@@ -1141,8 +1166,8 @@ __device__ __forceinline__ uint32_t quad_or(uint32_t v) {
 // block on the four lanes of a DPP quad, combined before the block is reported. A block is
 // taken only if its quad carries exactly the canonical selectors (QSEL); every other selector
 // row goes through the per-quad path.
-template <class Tile>
-__device__ __forceinline__ void g_pass(const Tile& T, EvalAcc& A, const uint32_t* L,
+template <class Tile, class Sink>
+__device__ __forceinline__ void g_pass(const Tile& T, Sink& A, const uint32_t* L,
                                        const uint32_t* gt_base, uint32_t ng, int64_t row_base,
                                        uint32_t lane, uint32_t wave, const GCarve& C) {
   const uint32_t per_g = wave == 1 ? 2u : 4u;
@@ -1174,7 +1199,7 @@ __device__ __forceinline__ void g_pass(const Tile& T, EvalAcc& A, const uint32_t
     } else if (take) {
       f = (wave == 0 ? g_add(T, r, L[C.a9 + (r >> 2)], (w & 1u) == 0) : g_xor(T, r, false)) ? 0u : want;
     }
-    if (f) A.fail_gates((uint64_t)(row_base + rl), f);
+    A.gates(f != 0, (uint64_t)(row_base + rl), f);
   }
 }
 
@@ -1192,7 +1217,8 @@ constexpr int LPG = 10;
 #define B2F_GT_WAVE 1
 #endif
 constexpr int GT_WAVE = B2F_GT_WAVE;  // wave that builds the next tile's G table (g_pass: XOR)
-__device__ __forceinline__ void g_copies(EvalAcc& A, const uint32_t* L, const uint32_t* gt_base,
+template <class Sink>
+__device__ __forceinline__ void g_copies(Sink& A, const uint32_t* L, const uint32_t* gt_base,
                                          uint32_t ng, int64_t row_base, uint32_t tid,
                                          const GCarve& C) {
   // the wave that built the G table takes the last slice of lanes (the fewest G entries)
@@ -1214,7 +1240,7 @@ __device__ __forceinline__ void g_copies(EvalAcc& A, const uint32_t* L, const ui
     const uint32_t sv = L[src < 0 ? 0 : src];  // < 0 only for checks outside the tile
     const int dlc = dl < C.lo ? C.lo : (dl >= C.hi ? C.hi - 1 : dl);
     const uint32_t dv = L[C.g + (1 + ((e >> 17) & 3u)) * C.ts + dlc];
-    if (dl >= C.lo && dl < C.hi && dv != sv) A.fail((uint64_t)(row_base + dl), B2F_CODE_COPY);
+    A.fail(dl >= C.lo && dl < C.hi && dv != sv, (uint64_t)(row_base + dl), B2F_CODE_COPY);
   }
 }
 
@@ -1276,8 +1302,9 @@ struct Src {
   }
 };
 
-__device__ __forceinline__ void copy_check(EvalAcc& A, uint32_t dv, uint32_t sv, uint64_t gd) {
-  if (dv != sv) A.fail(gd, B2F_CODE_COPY);
+template <class Sink>
+__device__ __forceinline__ void copy_check(Sink& A, uint32_t dv, uint32_t sv, uint64_t gd) {
+  A.fail(dv != sv, gd, B2F_CODE_COPY);
 }
 
 // canonical cell of limb k of state word w as half-round hr starts (instance-local row)
@@ -1301,8 +1328,8 @@ __host__ __device__ __forceinline__ uint32_t state_src(uint32_t w, uint32_t k, u
 
 // Copy constraints of the init XOR blocks and of the final XOR3 blocks (57 of the R/4 quads
 // of an instance): decoded directly.
-template <class Src>
-__device__ void copies_edge(EvalAcc& A, uint4 d0, uint4 d1, uint4 d2, const Src& src, uint64_t o,
+template <class Sink, class Src>
+__device__ void copies_edge(Sink& A, uint4 d0, uint4 d1, uint4 d2, const Src& src, uint64_t o,
                             uint32_t rounds, uint32_t lq) {
   QuadInfo d = decode_quad(lq, rounds);
   const uint32_t r0 = 4 * lq;

@@ -598,30 +598,6 @@ __device__ __forceinline__ void edge_tile(uint32_t* S, uint32_t* accw, const uin
     }
 }
 
-// Failure bookkeeping of a half-round tile's checks. REC = false: every check is evaluated and
-// only "some check failed" is kept (a flag, no branch around the bookkeeping: the common case,
-// a valid trace); REC = true: every failure is recorded exactly as the eval kernel records it
-// (counters, first failing row, deferred rows) -- run only when the fast pass flagged the tile.
-template <bool REC>
-struct Fails {
-  EvalAcc A;
-  bool bad;
-  __device__ __forceinline__ void fail(bool cond, uint64_t row, uint32_t code) {
-    if (REC) {
-      if (cond) A.fail(row, code);
-    } else {
-      bad |= cond;
-    }
-  }
-  __device__ __forceinline__ void gates(bool cond, uint64_t row, uint32_t mask) {
-    if (REC) {
-      if (cond) A.fail_gates(row, mask);
-    } else {
-      bad |= cond;
-    }
-  }
-};
-
 // message words (the last use of the loaded operands): a1 (x) at +0 and a2 (y) at +28 of
 // every G, lanes 0..31
 template <int MODE, bool REC>

@@ -459,6 +459,7 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
   const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + L_SG);  // [10][16]
 
   EvalAcc A{L + L_ACC};
+  Fails<true> Rec{A, false};  // failures recorded as they are found (a fast-flag pass measured slower here)
   if (tid < 20) L[L_ACC + tid] = 0;
   if (tid == 20) *reinterpret_cast<uint64_t*>(L + L_ACC + 20) = ~0ull;
 
@@ -565,9 +566,9 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
       const GCarve C{L_QSEL, L_A9, L_CT, L_G, TSTRIDE, 0, TILE_ROWS, false};
       const uint32_t ng = S[GS_NG];
       if (MODE & EVAL_GATES)
-        g_pass(T, A, L, S + GS_GT, ng, (int64_t)tile0, (uint32_t)tid & 63u, (uint32_t)tid >> 6, C);
+        g_pass(T, Rec, L, S + GS_GT, ng, (int64_t)tile0, (uint32_t)tid & 63u, (uint32_t)tid >> 6, C);
       tick(4);
-      if (MODE & EVAL_COPIES) g_copies(A, L, S + GS_GT, ng, (int64_t)tile0, (uint32_t)tid, C);
+      if (MODE & EVAL_COPIES) g_copies(Rec, L, S + GS_GT, ng, (int64_t)tile0, (uint32_t)tid, C);
       tick(5);
       // ---- per quad: selector rows the G pass does not take, and init/final-block copies
       if (gq < total_quads) {
@@ -614,7 +615,7 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
               const uint64_t ofirst = first < n ? Off[0] : ~0ull;
               const Src<WSTRIDE> src{L + L_W, L + L_IC, adv, total_rows, tile0 - HIST, ofirst};
               const uint4 dq[3] = {T.quad(A3, lr0), T.quad(A4, lr0), T.quad(A5, lr0)};
-              copies_edge(A, dq[0], dq[1], dq[2], src, o, rounds, lq);
+              copies_edge(Rec, dq[0], dq[1], dq[2], src, o, rounds, lq);
             }
           }
         }
