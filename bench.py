@@ -455,22 +455,27 @@ def main():
     # Fp export, reported beside the headline, not part of it:
     # Montgomery pallas limbs for a chunk of the resident trace (4 B read, 32 B written/cell)
     fp_export = None
+    fp_export_bn254 = None
     if args.export_rows > 0 and world == 1:
         nr = min(args.export_rows, batch.total_rows)
         out = torch.empty((10, nr, 4), dtype=torch.int64, device=batch.advice.device)
-        batch.export_fp(eng, nrows=nr, out=out, stream=stream)
-        eng.sync(stream)
-        eng.set_timing(True)
-        reps = 5
-        for _ in range(reps):
-            batch.export_fp(eng, nrows=nr, out=out, stream=stream)
-        tot, cnt = eng.kernel_times()["export"]
-        avg = tot / max(cnt, 1)
-        nbytes = nr * 10 * (4 + 32)
-        fp_export = {"rows": nr, "form": "montgomery", "avg_ms": round(avg, 4),
-                     "bytes_per_launch": nbytes,
-                     "achieved_GBs": round(nbytes / (avg * 1e-3) / 1e9, 1),
-                     "frac": round(nbytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        res = {}
+        for form, name in ((b2f.FP_MONTGOMERY, "pasta Fp montgomery"),
+                           (b2f.FP_BN254_MONTGOMERY, "bn254 Fr montgomery")):
+            batch.export_fp(eng, nrows=nr, out=out, form=form, stream=stream)
+            eng.sync(stream)
+            eng.set_timing(True)
+            reps = 5
+            for _ in range(reps):
+                batch.export_fp(eng, nrows=nr, out=out, form=form, stream=stream)
+            tot, cnt = eng.kernel_times()["export"]
+            avg = tot / max(cnt, 1)
+            nbytes = nr * 10 * (4 + 32)
+            res[form] = {"rows": nr, "form": name, "avg_ms": round(avg, 4),
+                         "bytes_per_launch": nbytes,
+                         "achieved_GBs": round(nbytes / (avg * 1e-3) / 1e9, 1),
+                         "frac": round(nbytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        fp_export, fp_export_bn254 = res[b2f.FP_MONTGOMERY], res[b2f.FP_BN254_MONTGOMERY]
         del out
 
     # Lookup-argument prover columns for circuits cut from the resident
@@ -577,7 +582,7 @@ def main():
                "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "floors": floors,
                "other_path": aux,
                "collectives": collectives, "witness_gather": witness, "config4": config4,
-               "fp_export": fp_export, "lookup_columns": lookup, "hasher": hasher_aux,
+               "fp_export": fp_export, "fp_export_bn254": fp_export_bn254, "lookup_columns": lookup, "hasher": hasher_aux,
                "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
                "gpu_vs_cpu_threads": cpu["cores"] if cpu else None}
         print(json.dumps(out), flush=True)

@@ -42,19 +42,14 @@ constexpr uint64_t kD1 = 0x224698fc094cf91bull;  // d, high limb
 constexpr int EXPORT_BLOCK = 256;
 constexpr int CELLS_PER_ITER = EXPORT_BLOCK / 2;  // 128 cells = 4 KiB of output per WG pass
 
-// limbs (2*half, 2*half+1) of the field element for cell value x
-__device__ __forceinline__ u64x2 fp_half(uint32_t x, uint32_t half, uint32_t form) {
+// limbs (2*half, 2*half+1) of the field element for cell value x: canonical (either field)
+// or pasta Montgomery (the closed form above)
+template <int FORM>
+__device__ __forceinline__ u64x2 fp_half(uint32_t x, uint32_t half) {
   u64x2 r;
-  if (!(form & 1u)) {  // canonical, either field
+  if (!(FORM & 1)) {  // canonical, either field
     r.x = half ? 0 : x;
     r.y = 0;
-    return r;
-  }
-  if (form == B2F_FP_BN254_MONTGOMERY) {
-    const field::Fe m = field::from_u32<field::Bn254>(x);
-    const uint32_t o = 4 * half;
-    r.x = (uint64_t)m.w[o] | ((uint64_t)m.w[o + 1] << 32);
-    r.y = (uint64_t)m.w[o + 2] | ((uint64_t)m.w[o + 3] << 32);
     return r;
   }
   if (x == 0) {
@@ -92,9 +87,10 @@ constexpr int XT = 512;
 constexpr int XSUB = XT / CELLS_PER_ITER;  // 4 store passes per column per tile
 constexpr int kAofH[10] = {5, 3, 4, 6, 7, 8, 9, 0, 1, 2};
 
+template <int FORM>
 __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
     const uint32_t* __restrict__ advice, uint64_t total_rows, uint64_t row_begin,
-    uint64_t nrows, uint32_t form, uint64_t* __restrict__ out, uint64_t out_rows) {
+    uint64_t nrows, uint64_t* __restrict__ out, uint64_t out_rows) {
   const uint32_t t = threadIdx.x;
   const uint32_t half = t & 1;
   const uint64_t n_tiles = (nrows + XT - 1) / XT;
@@ -114,8 +110,29 @@ __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
 #pragma unroll
       for (int i = 0; i < XSUB; i++) {
         uint64_t cell = r0 + i * CELLS_PER_ITER + (t >> 1);
-        if (cell < nrows) __builtin_nontemporal_store(fp_half(x[h][i], half, form), dst + 2 * cell + half);
+        if (cell < nrows) __builtin_nontemporal_store(fp_half<FORM>(x[h][i], half), dst + 2 * cell + half);
       }
+    }
+  }
+}
+
+// BN254 Fr Montgomery form: a generic Montgomery product per element (b2f_field.h), so one lane
+// per element (two 16-byte stores; a wave's pair covers 2 KiB contiguous), grid-stride.
+__global__ __launch_bounds__(256) void export_bn254_kernel(const uint32_t* __restrict__ advice,
+                                                           uint64_t total_rows, uint64_t row_begin,
+                                                           uint64_t nrows, uint64_t* __restrict__ out,
+                                                           uint64_t out_rows) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t cell = (uint64_t)blockIdx.x * 256 + threadIdx.x; cell < nrows; cell += stride) {
+#pragma unroll 2
+    for (int h = 0; h < 10; h++) {
+      const uint32_t x = advice[(uint64_t)kAofH[h] * total_rows + row_begin + cell];
+      const field::Fe m = field::from_u32<field::Bn254>(x);
+      u64x2* dst = reinterpret_cast<u64x2*>(out + ((uint64_t)h * out_rows + cell) * 4);
+      __builtin_nontemporal_store(u64x2{(uint64_t)m.w[0] | ((uint64_t)m.w[1] << 32),
+                                        (uint64_t)m.w[2] | ((uint64_t)m.w[3] << 32)}, dst);
+      __builtin_nontemporal_store(u64x2{(uint64_t)m.w[4] | ((uint64_t)m.w[5] << 32),
+                                        (uint64_t)m.w[6] | ((uint64_t)m.w[7] << 32)}, dst + 1);
     }
   }
 }
@@ -143,7 +160,15 @@ __global__ __launch_bounds__(256) void spread_table_kernel(uint64_t usable_rows,
 #pragma unroll
   for (int c = 0; c < 3; c++) {
     u64x2* dst = reinterpret_cast<u64x2*>(out + (uint64_t)c * out_rows * 4);
-    __builtin_nontemporal_store(fp_half(v[c], half, form), dst + 2 * row + half);
+    u64x2 e;
+    if (form == B2F_FP_BN254_MONTGOMERY) {
+      const field::Fe m = field::from_u32<field::Bn254>(v[c]);
+      const uint32_t o = 4 * half;
+      e = u64x2{(uint64_t)m.w[o] | ((uint64_t)m.w[o + 1] << 32), (uint64_t)m.w[o + 2] | ((uint64_t)m.w[o + 3] << 32)};
+    } else {
+      e = form & 1u ? fp_half<1>(v[c], half) : fp_half<0>(v[c], half);
+    }
+    __builtin_nontemporal_store(e, dst + 2 * row + half);
   }
 }
 
@@ -165,8 +190,17 @@ hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint6
   uint64_t want = (uint64_t)cu_count * 4;  // 122 VGPRs: 4 waves/SIMD
   uint32_t gx = (uint32_t)(tiles < want ? tiles : want);
   if (gx == 0) return hipSuccess;
-  hipLaunchKernelGGL(export_fp_kernel, dim3(gx), dim3(EXPORT_BLOCK), 0, s, d_advice,
-                     total_rows, row_begin, nrows, form, d_out, out_rows);
+  if (form == B2F_FP_BN254_MONTGOMERY) {
+    const uint64_t blocks = (nrows + 255) / 256, cap = (uint64_t)cu_count * 8;
+    hipLaunchKernelGGL(export_bn254_kernel, dim3((uint32_t)(blocks < cap ? blocks : cap)), dim3(256), 0, s,
+                       d_advice, total_rows, row_begin, nrows, d_out, out_rows);
+  } else if (form & 1u) {
+    hipLaunchKernelGGL(export_fp_kernel<1>, dim3(gx), dim3(EXPORT_BLOCK), 0, s, d_advice,
+                       total_rows, row_begin, nrows, d_out, out_rows);
+  } else {
+    hipLaunchKernelGGL(export_fp_kernel<0>, dim3(gx), dim3(EXPORT_BLOCK), 0, s, d_advice,
+                       total_rows, row_begin, nrows, d_out, out_rows);
+  }
   return hipGetLastError();
 }
 
