@@ -531,7 +531,9 @@ def main():
                           "compressions": int(plan.start[-1]), "ms": round(el2 * 1e3, 3),
                           "compressions_per_s": round(int(plan.start[-1]) / el2),
                           "digests_match_hashlib": ok,
-                          "note": "wall clock incl. block upload and h' download"}
+                          "path": "fused",
+                          "note": "wall clock incl. block upload (one async copy from pinned "
+                                  "memory) and the final h' download"}
         except Exception as e:
             hasher_aux = {"error": repr(e)}
 

@@ -71,6 +71,19 @@ class Plan:
                                         np.uint64(len(d)))
             self.f[idx[-1]] = 1
 
+    def pinned(self):
+        """The plan's blocks, counters and flags as page-locked host tensors (built once and
+        cached), so their upload is one asynchronous DMA."""
+        if not hasattr(self, "_pinned"):
+            import torch
+
+            def pin(a):
+                a = np.ascontiguousarray(a)
+                return torch.from_numpy(a.view(np.int64 if a.dtype == np.uint64 else np.int32)).pin_memory()
+
+            self._pinned = (pin(self.blocks), pin(self.t), pin(self.f))
+        return self._pinned
+
     def step(self, j):
         """(blocks, t, f) of step j: arrays over messages 0 .. active[j] - 1 (sorted order)."""
         s, e = int(self.start[j]), int(self.start[j + 1])
@@ -110,15 +123,18 @@ class ChainResult:
         return all(r["first_failure"] == 2**64 - 1 for r in self.reports)
 
 
-def blake2b_batch(engine, messages, digest_size=64, key=b"", path="split", device="cuda:0",
+def blake2b_batch(engine, messages, digest_size=64, key=b"", path="fused", device="cuda:0",
                   stream=None):
     """BLAKE2b digests of `messages` (a list of bytes-like) through the chip on one GPU, every
-    block step witnessed (fill) and checked (eval); path "fused" uses b2f_fill_eval_dev."""
+    block step witnessed and checked: path "fused" (b2f_fill_eval_dev, the default) or "split"
+    (b2f_fill_dev + b2f_eval_dev)."""
     return run_plan(engine, Plan(messages, digest_size, key), path, device, stream)
 
 
-def run_plan(engine, plan, path="split", device="cuda:0", stream=None):
-    """The device half of blake2b_batch for a prebuilt Plan."""
+def run_plan(engine, plan, path="fused", device="cuda:0", stream=None):
+    """The device half of blake2b_batch for a prebuilt Plan. The blocks go up in one
+    asynchronous copy from page-locked memory (Plan.pinned), every block step runs on the
+    stream, and only the final chaining values come back to the host."""
     import torch
 
     if path not in ("split", "fused"):
@@ -128,23 +144,30 @@ def run_plan(engine, plan, path="split", device="cuda:0", stream=None):
         return ChainResult(plan, [], np.zeros((0, 8), dtype=np.uint64))
     dev = torch.device(device)
     s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-
-    def up(a):
-        return torch.from_numpy(np.ascontiguousarray(a).view(
-            np.int64 if a.dtype == np.uint64 else np.int32).copy()).to(dev)
-
-    d_blocks, d_t, d_f = up(plan.blocks), up(plan.t), up(plan.f)
+    compute = torch.cuda.ExternalStream(s, device=dev)
+    p_blocks, p_t, p_f = plan.pinned()
+    d_blocks = torch.empty(p_blocks.shape, dtype=p_blocks.dtype, device=dev)
+    d_t = torch.empty(p_t.shape, dtype=p_t.dtype, device=dev)
+    d_f = torch.empty(p_f.shape, dtype=p_f.dtype, device=dev)
     R = rows(BLAKE2B_ROUNDS)
     # h' of every compression, step-major like the plan: step j's outputs are rows
     # start[j] .. start[j] + active[j] - 1, and step j + 1 reads its h from that prefix
-    h0 = up(np.broadcast_to(plan.h0, (n, 8)))
+    with torch.cuda.stream(compute):
+        h0 = torch.from_numpy(np.broadcast_to(plan.h0, (n, 8)).copy().view(np.int64)).to(dev)
+        offsets = torch.arange(n + 1, dtype=torch.int64, device=dev) * R
     hs = torch.empty((int(plan.start[-1]), 8), dtype=torch.int64, device=dev)
     inputs = torch.empty(n * 216, dtype=torch.uint8, device=dev)
-    offsets = torch.arange(n + 1, dtype=torch.int64, device=dev) * R
     advice = torch.empty((_lib.NUM_ADVICE, R * n), dtype=torch.int32, device=dev)
     fixed = torch.empty(R * n, dtype=torch.int32, device=dev)
     report = torch.empty((plan.steps, _lib.REPORT_BYTES // 8), dtype=torch.int64, device=dev)
-    torch.cuda.synchronize(dev)  # the uploads above ran on torch's stream
+    with torch.cuda.stream(compute):  # one asynchronous DMA from page-locked memory
+        d_blocks.copy_(p_blocks, non_blocking=True)
+        d_t.copy_(p_t, non_blocking=True)
+        d_f.copy_(p_f, non_blocking=True)
+    # torch's copies and allocations are ordered before the library's launches by a host
+    # synchronize, not by stream order alone (measured: without it, the first split-path batch
+    # after a fused one read stale blocks)
+    torch.cuda.synchronize(dev)
     for j in range(plan.steps):
         a = int(plan.active[j])
         s0 = int(plan.start[j])
@@ -163,13 +186,14 @@ def run_plan(engine, plan, path="split", device="cuda:0", stream=None):
             engine.eval_dev(advice.data_ptr(), fixed.data_ptr(), offsets.data_ptr(), a, total,
                             report[j].data_ptr(), s)
     engine.sync(s)
-    hs_host = hs.cpu().numpy().view(np.uint64)
+    # message at sorted position p ends at step nblocks - 1, i.e. at row start[nb - 1] + p
+    last = (plan.active[None, :] > np.arange(n)[:, None]).sum(1) - 1
+    idx = torch.from_numpy((plan.start[last] + np.arange(n)).astype(np.int64)).to(dev)
+    fin_host = hs.index_select(0, idx).cpu().numpy().view(np.uint64)
     raw = report.cpu().numpy().view(np.uint64)
     reps = [_lib.EvalReport.from_buffer_copy(raw[j].tobytes()).as_dict()
             for j in range(plan.steps)]
-    # message at sorted position p ends at step nblocks - 1, i.e. at row start[nb - 1] + p
-    last = (plan.active[None, :] > np.arange(n)[:, None]).sum(1) - 1
-    return ChainResult(plan, reps, hs_host[plan.start[last] + np.arange(n)])
+    return ChainResult(plan, reps, fin_host)
 
 
 class Blake2f:
@@ -179,7 +203,7 @@ class Blake2f:
     every block step through the chip and raises B2FError if any step's trace fails its
     constraints."""
 
-    def __init__(self, engine, digest_size=64, key=b"", device="cuda:0", path="split"):
+    def __init__(self, engine, digest_size=64, key=b"", device="cuda:0", path="fused"):
         param_state(digest_size, len(key))  # validates
         self.engine, self.digest_size, self.key = engine, digest_size, bytes(key)
         self.device, self.path = device, path
