@@ -310,7 +310,10 @@ enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16,
 // the lanes past the tile's last quad are dropped by the range check. Straight-line stores keep
 // the compiler's vmcnt bookkeeping exact: a branch that might skip a tile's stores would make
 // every later wait for an older load wait for those stores too (vmcnt is in order).
-constexpr int BUF_NT = 2;  // gfx94x/gfx950 cache-policy bit 1: non-temporal
+#ifndef B2F_BUF_POLICY
+#define B2F_BUF_POLICY 2
+#endif
+constexpr int BUF_NT = B2F_BUF_POLICY;  // gfx94x/gfx950 cache-policy bit 1: non-temporal
 __device__ __forceinline__ void tile_store(uint32_t* base, uint32_t nq, uint32_t lane, uint4 v) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const i32x4 rsrc = {(int32_t)(uint32_t)a, (int32_t)(uint32_t)(a >> 32), (int32_t)(nq * 16u), 0x00020000};

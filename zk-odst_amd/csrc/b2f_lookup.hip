@@ -10,8 +10,9 @@
 //   table pass (once per theta): T[x] = theta^2 tag(x) + theta x + spread(x) for x < 2^16,
 //     sorted by canonical value (four stable LSD passes of a 64-bit radix sort), giving the
 //     rank order x_of_rank[r] and Ts[r] = T[x_of_rank[r]];
-//   count:   histogram of the dense cell (a_1) over the circuit's rows, with the row check
-//            (tag, dense, spread) in table (first failing row reported);
+//   count:   histogram of the dense cell (a_1) over the circuit's rows (LDS-privatised, four
+//            workgroups per circuit, a quarter of the bins each), with the row check (tag,
+//            dense, spread) in table (first failing row reported);
 //   scan:    in rank order, run starts pos[r] (exclusive prefix of counts), D[r] (runs up to
 //            and including r) and LP[r] (exclusive prefix of leftover table multiplicities);
 //   permute: row p of A' is Ts[r] for the run r holding p (binary search of pos); a run
@@ -107,33 +108,41 @@ __device__ __forceinline__ Circ circ(const uint64_t* row_begin, uint64_t total_r
   return k;
 }
 
-__global__ __launch_bounds__(256) void lk_count_kernel(
+// Histogram of the dense cell over a circuit's rows, privatised in LDS: workgroup (b, c) owns
+// bins [b * 2^14, (b + 1) * 2^14) of circuit c (64 KiB of LDS counters), reads every row's
+// dense cell (the later passes hit L2), counts the rows that fall in its range with LDS
+// atomics and writes its bins with plain stores -- no global atomics and no memset. The
+// table-membership check runs on each row once (rows dealt to the 4 workgroups by 1,024-row
+// block); a circuit with a bad row reports it and its columns are meaningless, so rows are
+// binned by their low 16 bits regardless.
+constexpr int CNT_SPLIT = 4, CNT_BINS = TROWS / CNT_SPLIT, CNT_THREADS = 1024;
+__global__ __launch_bounds__(CNT_THREADS) void lk_count_kernel(
     const uint32_t* __restrict__ adv, uint64_t total_rows, const uint64_t* __restrict__ row_begin,
     uint32_t c0, uint64_t usable, uint32_t* __restrict__ count, uint64_t* __restrict__ first_bad) {
-  const uint32_t c = blockIdx.y;
+  __shared__ uint32_t bins[CNT_BINS];
+  const uint32_t b = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
   const Circ k = circ(row_begin, total_rows, usable, c0 + c);
-  uint32_t* cnt = count + (uint64_t)c * TROWS;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && usable > k.n_in)
-    atomicAdd(cnt, (uint32_t)(usable - k.n_in));  // zero rows past the trace: table row 0
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t base = (uint64_t)blockIdx.x * 256; base < k.n_in; base += stride) {
-    const uint64_t p = base + threadIdx.x;
-    const bool act = p < k.n_in;
-    uint32_t a0 = 0, a1 = 0, a2 = 0;
-    if (act) {
-      const uint64_t row = k.first + p;
-      a0 = adv[row];
-      a1 = adv[total_rows + row];
-      a2 = adv[2 * total_rows + row];
+  for (uint32_t i = t; i < (uint32_t)CNT_BINS; i += CNT_THREADS) bins[i] = 0;
+  __syncthreads();
+  if (b == 0 && t == 0 && usable > k.n_in) atomicAdd(&bins[0], (uint32_t)(usable - k.n_in));  // zero rows
+  uint64_t bad = ~0ull;
+  for (uint64_t base = 0; base < k.n_in; base += CNT_THREADS) {
+    const uint64_t p = base + t;
+    if (p >= k.n_in) break;
+    const uint64_t row = k.first + p;
+    const uint32_t a1 = adv[total_rows + row];
+    if (((base / CNT_THREADS) % CNT_SPLIT) == b) {  // this workgroup checks this block of rows
+      const uint32_t a0 = adv[row], a2 = adv[2 * total_rows + row];
+      const bool ok = a1 < (uint32_t)TROWS && a0 == tag16(a1) && a2 == spread16(a1);
+      if (!ok && bad == ~0ull) bad = p;
     }
-    const bool ok = a1 < (uint32_t)TROWS && a0 == tag16(a1) && a2 == spread16(a1);
-    if (act && !ok) atomicMin((unsigned long long*)first_bad + c0 + c, (unsigned long long)p);
-    const bool zero = act && ok && a1 == 0;
-    const uint64_t zb = __ballot(zero);
-    if (zb && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(zb))
-      atomicAdd(cnt, (uint32_t)__builtin_popcountll(zb));
-    if (act && ok && a1 != 0) atomicAdd(cnt + a1, 1u);
+    const uint32_t x = a1 & 0xffffu;
+    if ((x >> 14) == b) atomicAdd(&bins[x & (CNT_BINS - 1)], 1u);
   }
+  if (bad != ~0ull) atomicMin((unsigned long long*)first_bad + c0 + c, (unsigned long long)bad);
+  __syncthreads();
+  uint32_t* cnt = count + (uint64_t)c * TROWS + (uint64_t)b * CNT_BINS;
+  for (uint32_t i = t; i < (uint32_t)CNT_BINS; i += CNT_THREADS) cnt[i] = bins[i];
 }
 
 // one workgroup per circuit: 1024 threads x 64 ranks
@@ -348,11 +357,8 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   if (e != hipSuccess) return e;
   for (uint32_t c0 = 0; c0 < n_circuits; c0 += group) {
     const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
-    e = hipMemsetAsync(k.count, 0, 4ull * TROWS * g, s);
-    if (e != hipSuccess) return e;
-    const uint32_t bx = (uint32_t)((usable_rows + 255) / 256 < 512 ? (usable_rows + 255) / 256 : 512);
-    hipLaunchKernelGGL(lk_count_kernel, dim3(bx, g), dim3(256), 0, s, d_advice, total_rows,
-                       d_row_begin, c0, usable_rows, k.count, d_first_bad);
+    hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
+                       total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
     hipLaunchKernelGGL(lk_scan_kernel, dim3(g), dim3(1024), 0, s, pa, k.count, usable_rows, k.pos,
                        k.dcnt, k.lp, k.samp);
     // permute: ~4096 rows per workgroup (the LDS samples are staged once per workgroup)
