@@ -178,7 +178,8 @@ template <class F>
 __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint64_t* __restrict__ z_base,
                                                 uint64_t z_stride, const Fe* __restrict__ den,
                                                 const Fe* __restrict__ zn,
-                                                const Fe* __restrict__ seed) {
+                                                const Fe* __restrict__ seed,
+                                                const Fe* __restrict__ post) {
   const uint32_t c = blockIdx.y;
   const uint64_t nq = n_chunks(usable);
   const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -186,11 +187,28 @@ __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint
   const Fe* dn = den + (uint64_t)c * usable;
   uint64_t* zcol = z_base + (uint64_t)c * z_stride;
   const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
-  if (q == 0) field::store(zcol, out_form<F>(seed ? seed[c] : field::one<F>(), mont));
+  // post: a factor applied here rather than in the scan (chained products: the seed of
+  // product c is only known once the scans of products 0 .. c - 1 are done)
+  const Fe s0 = post ? post[c] : (seed ? seed[c] : field::one<F>());
+  if (q == 0) field::store(zcol, out_form<F>(s0, mont));
   Fe k = zn[(uint64_t)c * nq + q];
+  if (post) k = field::mul<F>(k, post[c]);
   for (uint64_t p = e; p-- > b;) {
     field::store(zcol + 4 * (p + 1), out_form<F>(field::mul<F>(field::load(zcol + 4 * (p + 1)), k), mont));
     if (p > b) k = field::mul<F>(k, dn[p]);
+  }
+}
+
+// Chained products: S[0] = 1, S[c] = S[c - 1] T[c - 1] with T[c] product c's closing value
+// for seed 1 (the permutation argument's column sets: each set's z starts where the previous
+// one closed).
+template <class F>
+__global__ void gp_chain_seeds(const Fe* __restrict__ T, Fe* __restrict__ S, uint32_t g) {
+  if (threadIdx.x != 0) return;
+  Fe acc = field::one<F>();
+  for (uint32_t c = 0; c < g; c++) {
+    S[c] = acc;
+    acc = field::mul<F>(acc, T[c]);
   }
 }
 
@@ -200,10 +218,20 @@ __host__ __device__ inline uint64_t scratch_elems(uint64_t usable) {
   return 2 * nq + 2 * nb;
 }
 
-// The passes for `g` independent products on `s`. zs: scratch of g * scratch_elems(usable).
+// The passes for `g` products on `s`. zs: scratch of g * scratch_elems(usable). With `chain`
+// (2 g elements of scratch) the products are chained -- product c starts from product c - 1's
+// closing value, product 0 from 1 -- and still scanned side by side: their single inversions
+// run in parallel, the seeds are applied in gp_write.
 template <class F>
 hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_t z_stride,
-               const Fe* num, const Fe* den, Fe* zs, const Fe* seed, Fe* closing, hipStream_t s) {
+               const Fe* num, const Fe* den, Fe* zs, const Fe* seed, Fe* closing, hipStream_t s,
+               Fe* chain = nullptr) {
+  Fe* post = nullptr;
+  if (chain) {
+    seed = nullptr;
+    closing = chain;  // T
+    post = chain + g;  // S
+  }
   const uint64_t nq = n_chunks(usable), nb = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
   Fe* zn = zs;
   Fe* zd = zs + (uint64_t)g * nq;
@@ -220,8 +248,9 @@ hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_
     hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, tn, td, seed, closing);
     hipLaunchKernelGGL(gp_block_down<F>, dim3((uint32_t)nb, g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, tn);
   }
+  if (chain) hipLaunchKernelGGL(gp_chain_seeds<F>, dim3(1), dim3(64), 0, s, chain, post, g);
   hipLaunchKernelGGL(gp_write<F>, dim3(zq, g), dim3(256), 0, s, usable, mont, z_base, z_stride, den,
-                     zn, seed);
+                     zn, seed, post);
   return hipGetLastError();
 }
 

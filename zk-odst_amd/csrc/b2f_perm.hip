@@ -133,12 +133,16 @@ template <class F>
 __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* __restrict__ pool,
                                                         const uint32_t* __restrict__ adv,
                                                         uint64_t total_rows, uint64_t row0,
-                                                        uint64_t usable, uint32_t j0, uint32_t j1,
+                                                        uint64_t usable, uint32_t chunk_len,
                                                         const Fe* __restrict__ BL,
                                                         const Fe* __restrict__ OH, Params prm_gamma,
                                                         Fe* __restrict__ num, Fe* __restrict__ den) {
   const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (r >= usable) return;
+  const uint32_t set = blockIdx.y;  // column set: columns [j0, j1)
+  const uint32_t j0 = set * chunk_len, j1 = j0 + chunk_len < (uint32_t)NCOL ? j0 + chunk_len : NCOL;
+  num += (uint64_t)set * usable;
+  den += (uint64_t)set * usable;
   const Fe gamma = field::to_mont<F>(field::load_words(prm_gamma.beta));  // gamma rides in .beta
   const uint32_t ii = inst_of(I.start, I.n, r);
   const uint64_t used = I.start[I.n];
@@ -165,7 +169,7 @@ struct Carve {
   Fe* num;
   Fe* den;
   Fe* zs;
-  Fe* seed;  // NCOL + 1 closing values (seed of set c = closing of set c - 1)
+  Fe* seed;  // chained grand products: closing values and seeds, NCOL each
   size_t total;
 };
 
@@ -182,10 +186,10 @@ Carve carve(void* base, uint32_t k, uint64_t usable) {
   m.OL = (Fe*)take(sizeof(Fe) * NCOL * LO);
   m.BL = (Fe*)take(sizeof(Fe) * NCOL * LO);
   m.OH = (Fe*)take(sizeof(Fe) * n_hi);
-  m.num = (Fe*)take(sizeof(Fe) * usable);
-  m.den = (Fe*)take(sizeof(Fe) * usable);
-  m.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable));
-  m.seed = (Fe*)take(sizeof(Fe) * (NCOL + 1));
+  m.num = (Fe*)take(sizeof(Fe) * usable * NCOL);  // one slice per column set (<= 8)
+  m.den = (Fe*)take(sizeof(Fe) * usable * NCOL);
+  m.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * NCOL);
+  m.seed = (Fe*)take(sizeof(Fe) * 2 * NCOL);
   m.total = off;
   return m;
 }
@@ -205,16 +209,15 @@ hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0
                        d_pool, n_rows, m.OL, m.OH, mont, d_sigma, out_rows);
   Params pg;
   for (int i = 0; i < 4; i++) pg.beta[i] = gamma[i];
+  // every column set's factors in one launch, then their grand products side by side,
+  // chained (set c starts where set c - 1 closed)
   const uint32_t sets = (NCOL + chunk_len - 1) / chunk_len;
-  for (uint32_t c = 0; c < sets; c++) {
-    const uint32_t j0 = c * chunk_len, j1 = j0 + chunk_len < (uint32_t)NCOL ? j0 + chunk_len : NCOL;
-    hipLaunchKernelGGL(pm_factor_kernel<F>, dim3((uint32_t)((usable + 255) / 256)), dim3(256), 0, s, I,
-                       d_pool, d_advice, total_rows, row0, usable, j0, j1, m.BL, m.OH, pg, m.num,
-                       m.den);
-    hipError_t e = gp::run<F>(1, usable, mont, d_z + (uint64_t)c * out_rows * 4, 0, m.num, m.den,
-                              m.zs, c ? m.seed + c : nullptr, m.seed + c + 1, s);
-    if (e != hipSuccess) return e;
-  }
+  hipLaunchKernelGGL(pm_factor_kernel<F>, dim3((uint32_t)((usable + 255) / 256), sets), dim3(256), 0, s,
+                     I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, pg, m.num,
+                     m.den);
+  hipError_t e = gp::run<F>(sets, usable, mont, d_z, out_rows * 4, m.num, m.den, m.zs, nullptr,
+                            nullptr, s, m.seed);
+  if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 
