@@ -781,6 +781,10 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
     Ctx c = ctx_of(t, raw_desc(t));
     Ops P{};
     if (t < t_all) P = load_ops(c, lane, in, rec, Sg);
+    // the first tile's operands arrive before the loop: otherwise the compiler cannot prove at
+    // the loop header that P is never pending and waits for vmcnt(0) -- every store in flight
+    // -- at P's first use in every iteration
+    settle(P);
     uint4 dn = raw_desc(t + W);
     for (; t < t_all; t += W) {
       tick(-1);
