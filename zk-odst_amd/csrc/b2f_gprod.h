@@ -7,8 +7,8 @@
 // D_p^-1 = D^-1 prod_{i > p} den_i: ONE inversion per product (of the whole den product D),
 // the rest prefix and suffix products. Three passes over ZC-row chunks (one lane walks one
 // chunk):
-//   gp_chunk:  the chunk's num prefix Nloc_p staged in z[p + 1], the chunk totals of num and
-//              den (2 products per row);
+//   gp_chunk:  the chunk's num prefix Nloc_p (written over num in place), the chunk totals of
+//              num and den (2 products per row);
 //   gp_scan:   K_q = seed N_before(q) D_end(q)^-1 per chunk, the inversion, and the closing
 //              value seed N / D (= z[usable]) for a next product. Up to SCAN_THREADS x 4
 //              chunks one workgroup per product scans them directly; beyond, three levels over
@@ -17,8 +17,8 @@
 //              block's K), so the serial run per lane stays short at any size;
 //   gp_write:  backward over the chunk: z[p + 1] = K_q Nloc_p prod_{p < i < e} den_i
 //              (2 products per row), converted to the output form.
-// Products are independent along blockIdx.y: product y reads num/den + y * usable and writes
-// z column z_base + y * z_stride (u64 units, 4 per element).
+// Products are independent along blockIdx.y: product y reads num/den + y * elems(usable) and
+// writes z column z_base + y * z_stride (u64 units, 4 per element).
 #pragma once
 #include "b2f_field.h"
 
@@ -33,30 +33,36 @@ constexpr int SCAN_THREADS = 1024;    // one workgroup per product
 
 __host__ __device__ inline uint64_t n_chunks(uint64_t usable) { return (usable + ZC - 1) / ZC; }
 
+// num / den are stored chunk-interleaved: row p of a product at (p mod ZC) * nq + p / ZC, so
+// that the lanes of a wave (consecutive chunks) walking their chunks read consecutive
+// elements at every step -- a row-major layout put the lanes 512 bytes apart and turned each
+// 32-byte read into a 128-byte line fetch. Writers (the factor passes) place rows this way;
+// an array holds ZC * nq elements per product.
+__host__ __device__ inline uint64_t slot_of(uint64_t p, uint64_t nq) { return (p % ZC) * nq + p / ZC; }
+__host__ __device__ inline uint64_t elems(uint64_t usable) { return n_chunks(usable) * ZC; }
+
 template <class F>
 __device__ __forceinline__ Fe out_form(const Fe& a, bool mont) {
   return mont ? a : field::to_canonical<F>(a);
 }
 
 template <class F>
-__global__ __launch_bounds__(256) void gp_chunk(uint64_t usable, uint64_t* __restrict__ z_base,
-                                                uint64_t z_stride, const Fe* __restrict__ num,
+__global__ __launch_bounds__(256) void gp_chunk(uint64_t usable, Fe* __restrict__ num,
                                                 const Fe* __restrict__ den, Fe* __restrict__ zn,
                                                 Fe* __restrict__ zd) {
   const uint32_t c = blockIdx.y;
   const uint64_t nq = n_chunks(usable);
   const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (q >= nq) return;
-  const Fe* nm = num + (uint64_t)c * usable;
-  const Fe* dn = den + (uint64_t)c * usable;
-  uint64_t* zcol = z_base + (uint64_t)c * z_stride;
+  Fe* nm = num + (uint64_t)c * elems(usable);
+  const Fe* dn = den + (uint64_t)c * elems(usable);
   const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
-  Fe pn = nm[b], pd = dn[b];
-  field::store(zcol + 4 * (b + 1), pn);
+  Fe pn = nm[q], pd = dn[q];  // row b (slot 0 of chunk q)
   for (uint64_t p = b + 1; p < e; p++) {
-    pn = field::mul<F>(pn, nm[p]);
-    pd = field::mul<F>(pd, dn[p]);
-    field::store(zcol + 4 * (p + 1), pn);
+    const uint64_t k = slot_of(p, nq);
+    pn = field::mul<F>(pn, nm[k]);
+    pd = field::mul<F>(pd, dn[k]);
+    nm[k] = pn;
   }
   zn[(uint64_t)c * nq + q] = pn;
   zd[(uint64_t)c * nq + q] = pd;
@@ -176,7 +182,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void gp_block_down(uint64_t nq, Fe* _
 
 template <class F>
 __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint64_t* __restrict__ z_base,
-                                                uint64_t z_stride, const Fe* __restrict__ den,
+                                                uint64_t z_stride, const Fe* __restrict__ num,
+                                                const Fe* __restrict__ den,
                                                 const Fe* __restrict__ zn,
                                                 const Fe* __restrict__ seed,
                                                 const Fe* __restrict__ post) {
@@ -184,7 +191,8 @@ __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint
   const uint64_t nq = n_chunks(usable);
   const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (q >= nq) return;
-  const Fe* dn = den + (uint64_t)c * usable;
+  const Fe* nm = num + (uint64_t)c * elems(usable);  // Nloc, from gp_chunk
+  const Fe* dn = den + (uint64_t)c * elems(usable);
   uint64_t* zcol = z_base + (uint64_t)c * z_stride;
   const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
   // post: a factor applied here rather than in the scan (chained products: the seed of
@@ -194,8 +202,9 @@ __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint
   Fe k = zn[(uint64_t)c * nq + q];
   if (post) k = field::mul<F>(k, post[c]);
   for (uint64_t p = e; p-- > b;) {
-    field::store(zcol + 4 * (p + 1), out_form<F>(field::mul<F>(field::load(zcol + 4 * (p + 1)), k), mont));
-    if (p > b) k = field::mul<F>(k, dn[p]);
+    const uint64_t sl = slot_of(p, nq);
+    field::store(zcol + 4 * (p + 1), out_form<F>(field::mul<F>(nm[sl], k), mont));
+    if (p > b) k = field::mul<F>(k, dn[sl]);
   }
 }
 
@@ -224,7 +233,7 @@ __host__ __device__ inline uint64_t scratch_elems(uint64_t usable) {
 // run in parallel, the seeds are applied in gp_write.
 template <class F>
 hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_t z_stride,
-               const Fe* num, const Fe* den, Fe* zs, const Fe* seed, Fe* closing, hipStream_t s,
+               Fe* num, const Fe* den, Fe* zs, const Fe* seed, Fe* closing, hipStream_t s,
                Fe* chain = nullptr) {
   Fe* post = nullptr;
   if (chain) {
@@ -238,8 +247,7 @@ hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_
   Fe* tn = zd + (uint64_t)g * nq;
   Fe* td = tn + (uint64_t)g * nb;
   const uint32_t zq = (uint32_t)((nq + 255) / 256);
-  hipLaunchKernelGGL(gp_chunk<F>, dim3(zq, g), dim3(256), 0, s, usable, z_base, z_stride, num, den,
-                     zn, zd);
+  hipLaunchKernelGGL(gp_chunk<F>, dim3(zq, g), dim3(256), 0, s, usable, num, den, zn, zd);
   if (nq <= 4ull * SCAN_THREADS) {
     hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, seed, closing);
   } else {
@@ -249,8 +257,8 @@ hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_
     hipLaunchKernelGGL(gp_block_down<F>, dim3((uint32_t)nb, g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, tn);
   }
   if (chain) hipLaunchKernelGGL(gp_chain_seeds<F>, dim3(1), dim3(64), 0, s, chain, post, g);
-  hipLaunchKernelGGL(gp_write<F>, dim3(zq, g), dim3(256), 0, s, usable, mont, z_base, z_stride, den,
-                     zn, seed, post);
+  hipLaunchKernelGGL(gp_write<F>, dim3(zq, g), dim3(256), 0, s, usable, mont, z_base, z_stride, num,
+                     den, zn, seed, post);
   return hipGetLastError();
 }
 

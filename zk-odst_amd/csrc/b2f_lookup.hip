@@ -227,8 +227,9 @@ __global__ __launch_bounds__(256) void lk_permute_kernel(
   const uint32_t c = blockIdx.y;
   const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
   const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
-  Fe* nm = num + (uint64_t)c * usable;
-  Fe* dn = den + (uint64_t)c * usable;
+  Fe* nm = num + (uint64_t)c * gp::elems(usable);
+  Fe* dn = den + (uint64_t)c * gp::elems(usable);
+  const uint64_t nq = gp::n_chunks(usable);
   const Circ k = circ(row_begin, total_rows, usable, c0 + c);
   const uint32_t* P = pos + (uint64_t)c * TROWS;
   const uint32_t* D = dcnt + (uint64_t)c * TROWS;
@@ -265,8 +266,8 @@ __global__ __launch_bounds__(256) void lk_permute_kernel(
     store(o + (2 * out_rows + p) * 4, out_form<F>(ap, mont));
     store(o + (3 * out_rows + p) * 4, out_form<F>(sp, mont));
     // the grand product's factors (A + beta)(S + gamma) / ((A' + beta)(S' + gamma))
-    nm[p] = field::mul<F>(field::add<F>(a, beta), field::add<F>(sv, gamma));
-    dn[p] = field::mul<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma));
+    nm[gp::slot_of(p, nq)] = field::mul<F>(field::add<F>(a, beta), field::add<F>(sv, gamma));
+    dn[gp::slot_of(p, nq)] = field::mul<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma));
   }
 }
 
@@ -321,8 +322,8 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.dcnt = (uint32_t*)take(4ull * TROWS * group);
   k.lp = (uint32_t*)take(4ull * TROWS * group);
   k.samp = (uint32_t*)take(8ull * SAMPLE * group);
-  k.num = (Fe*)take(sizeof(Fe) * usable * group);
-  k.den = (Fe*)take(sizeof(Fe) * usable * group);
+  k.num = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);  // chunk-interleaved (b2f_gprod.h)
+  k.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);
   k.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * group);
   k.sort_bytes = sort_temp_bytes();
   k.sort_tmp = take(k.sort_bytes);

@@ -141,8 +141,8 @@ __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* 
   if (r >= usable) return;
   const uint32_t set = blockIdx.y;  // column set: columns [j0, j1)
   const uint32_t j0 = set * chunk_len, j1 = j0 + chunk_len < (uint32_t)NCOL ? j0 + chunk_len : NCOL;
-  num += (uint64_t)set * usable;
-  den += (uint64_t)set * usable;
+  num += (uint64_t)set * gp::elems(usable);
+  den += (uint64_t)set * gp::elems(usable);
   const Fe gamma = field::to_mont<F>(field::load_words(prm_gamma.beta));  // gamma rides in .beta
   const uint32_t ii = inst_of(I.start, I.n, r);
   const uint64_t used = I.start[I.n];
@@ -158,8 +158,9 @@ __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* 
     n = field::mul<F>(n, field::add<F>(vg, dw<F>(BL, OH, j, r)));
     d = field::mul<F>(d, field::add<F>(vg, dw<F>(BL, OH, c2, r2)));
   }
-  num[r] = n;
-  den[r] = d;
+  const uint64_t sl = gp::slot_of(r, gp::n_chunks(usable));  // chunk-interleaved (b2f_gprod.h)
+  num[sl] = n;
+  den[sl] = d;
 }
 
 struct Carve {
@@ -186,8 +187,8 @@ Carve carve(void* base, uint32_t k, uint64_t usable) {
   m.OL = (Fe*)take(sizeof(Fe) * NCOL * LO);
   m.BL = (Fe*)take(sizeof(Fe) * NCOL * LO);
   m.OH = (Fe*)take(sizeof(Fe) * n_hi);
-  m.num = (Fe*)take(sizeof(Fe) * usable * NCOL);  // one slice per column set (<= 8)
-  m.den = (Fe*)take(sizeof(Fe) * usable * NCOL);
+  m.num = (Fe*)take(sizeof(Fe) * gp::elems(usable) * NCOL);  // one slice per column set (<= 8)
+  m.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * NCOL);
   m.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * NCOL);
   m.seed = (Fe*)take(sizeof(Fe) * 2 * NCOL);
   m.total = off;
