@@ -155,14 +155,28 @@ __global__ __launch_bounds__(1024) void lk_scan_kernel(const uint32_t* __restric
                                                        uint32_t* __restrict__ samp) {
   const uint32_t c = blockIdx.x, t = threadIdx.x;
   const uint32_t* cnt = count + (uint64_t)c * TROWS;
+  // this thread's 64 consecutive ranks: the rank order read as 16-byte vectors, the counts
+  // gathered once into registers (and the one rank holding x = 0 remembered)
+  uint32_t nv[64];
+  int iz = -1;
+  const uint4* pv = reinterpret_cast<const uint4*>(perm + t * 64);
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint4 x = pv[i];
+    nv[4 * i] = cnt[x.x];
+    nv[4 * i + 1] = cnt[x.y];
+    nv[4 * i + 2] = cnt[x.z];
+    nv[4 * i + 3] = cnt[x.w];
+    iz = x.x == 0 ? 4 * i : x.y == 0 ? 4 * i + 1 : x.z == 0 ? 4 * i + 2 : x.w == 0 ? 4 * i + 3 : iz;
+  }
+  const uint32_t mult0 = (uint32_t)(usable - TROWS + 1);  // table row 0 fills the rest
   uint32_t sc = 0, sd = 0, sl = 0;
+#pragma unroll
   for (int i = 0; i < 64; i++) {
-    const uint32_t x = perm[t * 64 + i];
-    const uint32_t n = cnt[x];
-    const uint32_t mult = x == 0 ? (uint32_t)(usable - TROWS + 1) : 1u;
+    const uint32_t n = nv[i];
     sc += n;
     sd += n ? 1u : 0u;
-    sl += mult - (n ? 1u : 0u);
+    sl += (i == iz ? mult0 : 1u) - (n ? 1u : 0u);
   }
   __shared__ uint32_t s[3][1024];
   s[0][t] = sc; s[1][t] = sd; s[2][t] = sl;
@@ -175,24 +189,30 @@ __global__ __launch_bounds__(1024) void lk_scan_kernel(const uint32_t* __restric
     __syncthreads();
   }
   uint32_t ec = s[0][t] - sc, ed = s[1][t] - sd, el = s[2][t] - sl;  // exclusive
-  uint32_t* P = pos + (uint64_t)c * TROWS;
-  uint32_t* D = dcnt + (uint64_t)c * TROWS;
-  uint32_t* L = lp + (uint64_t)c * TROWS;
-  for (int i = 0; i < 64; i++) {
-    const uint32_t r = t * 64 + i;
-    const uint32_t x = perm[r];
-    const uint32_t n = cnt[x];
-    const uint32_t mult = x == 0 ? (uint32_t)(usable - TROWS + 1) : 1u;
-    P[r] = ec;
-    ed += n ? 1u : 0u;
-    D[r] = ed;
-    L[r] = el;
-    if ((r & 15u) == 0) {
-      samp[(uint64_t)c * 2 * SAMPLE + (r >> 4)] = ec;
-      samp[(uint64_t)c * 2 * SAMPLE + SAMPLE + (r >> 4)] = el;
+  uint4* P4 = reinterpret_cast<uint4*>(pos + (uint64_t)c * TROWS + t * 64);
+  uint4* D4 = reinterpret_cast<uint4*>(dcnt + (uint64_t)c * TROWS + t * 64);
+  uint4* L4 = reinterpret_cast<uint4*>(lp + (uint64_t)c * TROWS + t * 64);
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    uint32_t pq[4], dq[4], lq[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t n = nv[4 * i + j];
+      pq[j] = ec;
+      ed += n ? 1u : 0u;
+      dq[j] = ed;
+      lq[j] = el;
+      ec += n;
+      el += (4 * i + j == iz ? mult0 : 1u) - (n ? 1u : 0u);
     }
-    ec += n;
-    el += mult - (n ? 1u : 0u);
+    P4[i] = make_uint4(pq[0], pq[1], pq[2], pq[3]);
+    D4[i] = make_uint4(dq[0], dq[1], dq[2], dq[3]);
+    L4[i] = make_uint4(lq[0], lq[1], lq[2], lq[3]);
+    if ((i & 3) == 0) {  // rank t * 64 + 4 i is a multiple of 16: a search sample
+      const uint32_t r = t * 64 + 4 * i;
+      samp[(uint64_t)c * 2 * SAMPLE + (r >> 4)] = pq[0];
+      samp[(uint64_t)c * 2 * SAMPLE + SAMPLE + (r >> 4)] = lq[0];
+    }
   }
 }
 
