@@ -31,8 +31,9 @@ def main():
     os.environ["B2F_DIAG_FUSED" if args.fused else "B2F_DIAG_EVAL"] = str(args.fused) if args.fused else "23"
     if args.fused:
         global PHASES
-        PHASES = ["ctx+loads", "producers", "assign+stage", "msgcopy", "settle", "stores",
-                  "lkp+fixed+gates", "copies/other"]
+        # fused_hr_kernel (the half-round launch, second form) tick points
+        PHASES = ["load+words", "chains+publish", "operands+cells", "stage-wait", "stores",
+                  "fast-checks", "exact+end", "vmcnt"]
     run(eng, s)
     eng.sync(s)
     out = (ctypes.c_uint64 * 32)()

@@ -605,12 +605,12 @@ __device__ __forceinline__ void edge_tile(uint32_t* S, uint32_t* accw, const uin
 // every G, lanes 0..31
 template <int MODE, bool REC>
 __device__ __forceinline__ void hr_msg_copies(Fails<REC>& F, const WaveTile& T, uint32_t lane,
-                                              const Ctx& c, const Ops& P, const uint8_t* Sg,
+                                              const Ctx& c, uint64_t mw, const uint8_t* Sg,
                                               const Inject& inj) {
   if ((MODE & FZ_COPIES) && lane < 32) {
     const uint32_t mg = lane >> 3, which = (lane >> 2) & 1u, k = lane & 3u;
     const uint32_t dr = 52 * mg + (which ? 28u : 0u) + k;
-    uint32_t sv = limb(P.w[6], k);
+    uint32_t sv = limb(mw, k);
     if (MODE & FZ_INJECT) {
       const uint32_t g = mg + 4 * (c.hr & 1u);
       const uint32_t mj = Sg[16 * ((c.hr >> 1) % 10) + 2 * g + which];
@@ -620,10 +620,12 @@ __device__ __forceinline__ void hr_msg_copies(Fails<REC>& F, const WaveTile& T, 
   }
 }
 
-// lookups, the fixed column, the canonical gate passes and the copies of a half-round tile
-template <int MODE, bool REC>
+// lookups, the fixed column, the canonical gate passes and the copies of a half-round tile.
+// `ct`: the HrChecks entries of the tile's parity; `state(w, k, spread)`: limb k of state word w
+// as its producer assigned it (dense or spread).
+template <int MODE, bool REC, class StateLimb>
 __device__ __forceinline__ void hr_checks(Fails<REC>& F, const WaveTile& T, uint32_t lane,
-                                          const Ctx& c, const uint32_t* L, const uint64_t* prod,
+                                          const Ctx& c, const uint32_t* ct, const StateLimb& state,
                                           const Inject& inj, uint64_t* defer, uint32_t defer_cap) {
   const uint32_t nq = c.nq;
   const bool qlane = lane < nq;
@@ -691,7 +693,6 @@ __device__ __forceinline__ void hr_checks(Fails<REC>& F, const WaveTile& T, uint
     }
   }
   if (MODE & FZ_COPIES) {
-    const uint32_t* ct = L + L_CT + (c.hr & 1u) * HR_CHECKS;
 #pragma unroll
     for (int it = 0; it < HR_CHECKS / FW; it++) {
       const uint32_t e = ct[it * FW + lane];
@@ -702,8 +703,7 @@ __device__ __forceinline__ void hr_checks(Fails<REC>& F, const WaveTile& T, uint
         sv = T.at(wcol((e >> 19) & 3u), (e >> 11) & 255u);
       } else {
         const uint32_t w = (e >> 11) & 15u, k = (e >> 15) & 3u, sp = (e >> 17) & 1u;
-        const uint32_t lv = limb(prod[w], k);
-        sv = sp ? spread16(lv) : lv;
+        sv = state(w, k, sp);
         if (MODE & FZ_INJECT) {
           uint32_t col = 0;
           const uint32_t sr = state_src(w, k, sp, c.hr, col);
@@ -808,18 +808,23 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staging is complete
         __builtin_amdgcn_wave_barrier();
         Fails<false> F{A, false};
-        hr_msg_copies<MODE, false>(F, T, lane, c, P, Sg, inj);
+        hr_msg_copies<MODE, false>(F, T, lane, c, P.w[6], Sg, inj);
         tick(3);  // staging visible, message copies
         settle(Pn);
         tick(4);  // the next tile's operands arrived
         store_staged<MODE>(S, lane, nq, c.row0, adv, fixed, total_rows);
         tick(5);  // stores issued
-        hr_checks<MODE, false>(F, T, lane, c, L, prod, inj, defer, defer_cap);
+        const uint32_t* ct = L + L_CT + (c.hr & 1u) * HR_CHECKS;
+        auto state = [&](uint32_t w, uint32_t k, uint32_t sp) {
+          const uint32_t lv = limb(prod[w], k);
+          return sp ? spread16(lv) : lv;
+        };
+        hr_checks<MODE, false>(F, T, lane, c, ct, state, inj, defer, defer_cap);
         tick(6);  // lookups, fixed column, gates, copies
         if (__builtin_amdgcn_ballot_w64(F.bad)) {  // rare: a failure in this tile, record it exactly
           Fails<true> R{A, false};
-          hr_msg_copies<MODE, true>(R, T, lane, c, P, Sg, inj);
-          hr_checks<MODE, true>(R, T, lane, c, L, prod, inj, defer, defer_cap);
+          hr_msg_copies<MODE, true>(R, T, lane, c, P.w[6], Sg, inj);
+          hr_checks<MODE, true>(R, T, lane, c, ct, state, inj, defer, defer_cap);
         }
       } else if (PART == PART_EDGE && (c.kind == T_INIT || c.kind == T_FINAL)) {
         settle(Pn);
@@ -880,6 +885,593 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
   flush_report(A, rep, tid);
 }
 
+// ============================================================================================
+// The half-round launch (PART_HR), second form: a lane's quad position p inside its G never
+// changes from tile to tile, so everything that depends on p alone -- which bytes of which
+// operand word land in every cell, which cells every check reads -- is resolved once per lane
+// before the tile loop (v_perm_b32 byte selectors and LDS byte addresses in registers). Per tile:
+//   1. each lane loads ONE 8-byte word (the tile's 16 state words and 8 message words in G
+//      order, the previous half-round's 16 state words and 8 message words for the producers)
+//      and writes it to the wave's LDS;
+//   2. every lane runs the G chain of its G; one lane per G publishes the chain
+//      (a d c b a1 d1 c1 b1 a2 d2 c2 mx my 0), so a quad's operands X = s[step], Y = s[step+3]
+//      and M are three LDS reads instead of select chains; the four producer lanes publish the
+//      previous half-round's G outputs (the state words' producer values), and every lane
+//      builds one (word, limb) entry of the limb table the copy checks read (dense and spread);
+//   3. cells: a_1 rows and every operand slot by v_perm byte selection, spreads and tags, staged;
+//   4. stores (as the first form);
+//   5. fast checks, every one a 32-bit bitwise accumulation (acc |= lhs ^ rhs): lookups, the
+//      fixed column, all XOR/XOR24/XOR63 limb identities in ONE pass (64 lanes = 64 limb items),
+//      the 16 additions as carry chains, the 256 + 32 copies as pure LDS compares. They assume
+//      what the other checks of the same pass establish (every checked cell in its range); a
+//      cell out of range fails its own check, so a clean pass proves a clean tile, and a flagged
+//      tile is re-checked exactly (hr_checks<REC = true>, the eval kernel's bookkeeping).
+// The staging columns a_9 and fixed are written last in a tile, so their rows hold the tile's
+// transient words (steps 1-2) until then.
+namespace hr2 {
+constexpr uint32_t PZ = 0x0c0c0c0cu;  // v_perm_b32 selector: four zero bytes
+constexpr uint32_t psel(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+  return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+}
+constexpr uint32_t limb_sel(uint32_t k) { return psel(2 * k, 2 * k + 1, 12, 12); }  // on (hi, lo)
+
+// Per quad position p: the byte selectors of every cell of the quad (LAYOUT.md §4, the same
+// recipes as make_rows / quad_round).
+struct QuadProg {
+  uint32_t selL[4], selH[4];  // a_1 of row j = perm(O_lo, T_lo, selL) | perm(O_hi, T_hi, selH)
+  uint32_t slot[4];           // a_3..a_8 of row j = perm(slot B, slot A, slot) (ADD: limb j of (hi, lo))
+  uint32_t slA, slB;          // limb selectors of the operand slots on (hi, lo)
+  uint32_t flags;             // bit 0 ADD, 1 XOR63, 2 XOR24 | XOR63 (w cells), 3 XOR24
+  uint32_t fx0;               // fixed cell of row 0 (keygen selectors; rows 1-3 are 0)
+};
+struct QuadProgs {
+  QuadProg q[G_QUADS];
+};
+constexpr QuadProgs make_qprogs() {
+  QuadProgs P{};
+  const RowTable R = make_rows();
+  for (uint32_t p = 0; p < G_QUADS; p++) {
+    QuadProg& g = P.q[p];
+    const uint32_t st = step_of_quad(p);
+    const bool add = st % 2 == 0, x24 = st == 3, x63 = st == 7;
+    for (uint32_t j = 0; j < 4; j++) {
+      const uint32_t e = R.r[p][j];
+      const uint32_t k = e & 3u, src = (e >> 2) & 3u, sh8 = (e >> 4) & 1u, mcode = (e >> 5) & 3u;
+      const uint32_t b0 = 2 * k + sh8, half = b0 >> 2, bb = b0 & 3u, so = src == 2 ? 4u : 0u;
+      const uint32_t sel = psel(bb + so, mcode == 1 ? 12u : bb + 1 + so, 12, 12);
+      g.selL[j] = half == 0 ? sel : PZ;
+      g.selH[j] = half == 1 ? sel : PZ;
+    }
+    const uint32_t sd = R.slot[p];
+    const uint32_t jA = sd & 3u, kA = (sd >> 2) & 3u, vA = (sd >> 4) & 1u;
+    const uint32_t jB = (sd >> 5) & 3u, kB = (sd >> 7) & 3u, vB = (sd >> 9) & 1u;
+    g.slA = limb_sel(kA);
+    g.slB = limb_sel(kB);
+    for (uint32_t j = 0; j < 4; j++)
+      g.slot[j] = add ? limb_sel(j) : (vA && jA == j) ? 0x03020100u : (vB && jB == j) ? 0x07060504u : PZ;
+    g.flags = (add ? 1u : 0u) | (x63 ? 2u : 0u) | ((x24 || x63) ? 4u : 0u) | (x24 ? 8u : 0u);
+    g.fx0 = expected_sel(p);
+  }
+  return P;
+}
+// The recipes the selectors assume: a_1 sources are S (ADD), Z / O (XOR family); 0x7fff
+// masks only on XOR63's Z rows (applied to T), 0xff fields only in XOR24; no field crosses a
+// 32-bit half.
+constexpr bool qprogs_ok() {
+  const RowTable R = make_rows();
+  for (uint32_t p = 0; p < G_QUADS; p++) {
+    const uint32_t st = step_of_quad(p);
+    for (uint32_t j = 0; j < 4; j++) {
+      const uint32_t e = R.r[p][j], src = (e >> 2) & 3u, mcode = (e >> 5) & 3u;
+      if (st % 2 == 0 && src != 0) return false;
+      if (st % 2 == 1 && src == 0) return false;
+      if (mcode == 2 && !(st == 7 && src == 1)) return false;
+      if (st == 7 && src == 1 && mcode != 2) return false;
+      if (mcode == 1 && st != 3) return false;
+      if (mcode == 3) return false;
+    }
+  }
+  return true;
+}
+static_assert(qprogs_ok(), "quad programs match the row recipes");
+__constant__ QuadProgs c_qprogs = make_qprogs();
+
+// wave LDS (words): staging [11][STR]; limb table LT: [0, 64) dense, [64, 128) spread limb k of
+// state word w at 4 w + k; MW: the tile's 8 message words (u64, 2 gg + i).
+constexpr int H_LT = NSTAGE * STR;
+constexpr int H_MW = H_LT + 128;
+constexpr int HW_WORDS = H_MW + 16;
+// transient, inside staging columns a_9 and fixed: WD 56 u64 ([0, 16) state words of the tile
+// in G order, [16, 24) the producers' message words, [24, 40) previous state words in G order,
+// [40, 56) scratch), GS 4 x 16 u64 (the published chains), PG 16 u64 (producer outputs, G order)
+constexpr int T_WD = A9 * STR;
+constexpr int T_GS = T_WD + 112;
+constexpr int T_PG = T_GS + 128;
+static_assert(T_PG + 32 <= NSTAGE * STR, "transient words inside columns a_9 and fixed");
+// workgroup LDS (words)
+constexpr int H_ACC = 0, H_IV = 24, H_SG = H_IV + 16, H_WAVE = H_SG + 40;
+constexpr int H_WORDS = H_WAVE + WAVES * HW_WORDS;
+static_assert(H_WAVE % 4 == 0 && HW_WORDS % 4 == 0 && T_WD % 4 == 0 && T_GS % 4 == 0 && T_PG % 4 == 0,
+              "16-byte aligned carve");
+static_assert(H_WORDS * 4 * 4 <= 160 * 1024, "four workgroups per CU");
+static_assert(4 * H_WORDS < 65536, "LDS byte addresses fit 16 bits");
+
+// LDS accesses by byte address (a VGPR holding the address, the offset immediates folded in)
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) uint32_t l32;
+typedef __attribute__((address_space(3))) uint16_t l16;
+typedef __attribute__((address_space(3))) uint64_t l64;
+typedef __attribute__((address_space(3))) u32x4_t l128;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wint-to-pointer-cast"
+__device__ __forceinline__ uint32_t lds_byte(const uint32_t* p) {
+  return (uint32_t)(uintptr_t)(const l32*)p;
+}
+__device__ __forceinline__ uint32_t ld32(uint32_t a) { return *(const l32*)a; }
+__device__ __forceinline__ uint32_t ld16(uint32_t a) { return *(const l16*)a; }
+__device__ __forceinline__ uint64_t ld64(uint32_t a) { return *(const l64*)a; }
+__device__ __forceinline__ uint4 ld128(uint32_t a) {
+  const u32x4_t v = *(const l128*)a;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st32(uint32_t a, uint32_t v) { *(l32*)a = v; }
+__device__ __forceinline__ void st64(uint32_t a, uint64_t v) { *(l64*)a = v; }
+__device__ __forceinline__ void st128(uint32_t a, uint4 v) {
+  const u32x4_t w = {v.x, v.y, v.z, v.w};
+  *(l128*)a = w;
+}
+#pragma clang diagnostic pop
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+__device__ __forceinline__ uint32_t lo32(uint64_t v) { return (uint32_t)v; }
+__device__ __forceinline__ uint32_t hi32(uint64_t v) { return (uint32_t)(v >> 32); }
+__device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
+// tag of a 16-bit value (0: < 2^8, 1: < 2^15, 2: otherwise), branch-free
+__device__ __forceinline__ uint32_t tag_of(uint32_t x) { return ((x + 0xff00u) >> 16) + (x >> 15); }
+__device__ __forceinline__ uint32_t sel32(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+
+// A tile as the wave sees it (wave-uniform).
+struct HCtx {
+  uint32_t inst, rounds, hr, st;
+  uint64_t off, row0;
+};
+__device__ __forceinline__ HCtx hctx(const uint4& raw) {
+  HCtx c;
+  c.inst = __builtin_amdgcn_readfirstlane(raw.x);
+  const uint32_t j = __builtin_amdgcn_readfirstlane(raw.y);
+  c.rounds = __builtin_amdgcn_readfirstlane(raw.z);
+  c.st = __builtin_amdgcn_readfirstlane(raw.w);
+  c.hr = j ? j - 1 : 0;  // past the last tile: a valid in-bounds context (its loads are never used)
+  c.off = 20ull * c.inst + 208ull * c.st;
+  c.row0 = c.off + INIT_ROWS + 208ull * c.hr;
+  return c;
+}
+
+// The one word lane `lane` loads for tile c (see the WD layout; lanes 16-23 fill MW).
+__device__ __forceinline__ uint64_t load_word(const HCtx& c, uint32_t lane, const b2f_input* __restrict__ in,
+                                              const uint64_t* __restrict__ rec, const uint8_t* Sg) {
+  const b2f_input* x = in + c.inst;
+  const uint64_t* fw = reinterpret_cast<const uint64_t*>(&x->rounds);  // rounds | f << 32
+  const uint32_t h = c.hr, hp = h ? h - 1 : 0;
+  const uint32_t grp = lane >> 3, gl = (lane >> 2) & 3u, role = lane & 3u;
+  const uint32_t gm = (lane >> 1) & 3u, i = lane & 1u;
+  // message lanes: this tile's (16-23) or the producers' half-round (24-31)
+  const bool pm = grp == 3;
+  const uint32_t mh = pm ? hp : h;
+  const uint32_t sidx = Sg[16 * ((mh >> 1) % 10) + 2 * (gm + 4 * (mh & 1u)) + i];
+  // state lanes: the tile's half-round (0-15) or the previous one (32-47)
+  const bool ps = grp >= 4;
+  const uint32_t sh = ps ? hp : h;
+  const uint32_t word = 4 * role + ((gl + role * (sh & 1u)) & 3u);
+  const uint64_t* p = fw;
+  if (grp < 2 || (ps && grp < 6 && h != 0)) p = rec + 16ull * (c.st + sh) + word;
+  else if (grp == 2 || (pm && h != 0)) p = x->m + sidx;
+  else if (ps && grp < 6) p = role == 0 ? x->h + gl : role == 1 ? x->h + gl + 4 : (role == 3 && gl < 2) ? x->t + gl : fw;
+  return *p;
+}
+
+// The per-lane constants of the tile loop (resolved once).
+struct Lane {
+  // assignment
+  uint32_t selL[4], selH[4], slot[4], slA, slB;
+  uint32_t madd, mzm, mhz, mhw, mswap, rsh, fx0;
+  uint32_t aWD, aAB, aMX, aGS, aXY, aM, aPG, aLTs, aLTd, ltsh;
+  // checks
+  uint32_t aQ;                        // the lane's quad, column a_0 (lanes >= 52: quad 0..11 again)
+  uint32_t gb, ge, gf, gsel, gm24, gm63, gnl, grs, gsF, gsH;  // XOR-family limb item
+  uint32_t ar, m3;                    // ADD block
+  uint32_t ce[2][4], cm;              // copies (dst | src << 16), message copy
+};
+
+__device__ __forceinline__ Lane make_lane(uint32_t lane, uint32_t Sb) {
+  Lane L;
+  const uint32_t lq = lane < HR_Q ? lane : lane - HR_Q;
+  const uint32_t gg = lq / G_QUADS, p = lq - G_QUADS * gg;
+  const QuadProg& Q = c_qprogs.q[p];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    L.selL[j] = Q.selL[j];
+    L.selH[j] = Q.selH[j];
+    L.slot[j] = Q.slot[j];
+  }
+  L.slA = Q.slA;
+  L.slB = Q.slB;
+  const uint32_t fl = Q.flags;
+  L.madd = (fl & 1u) ? ~0u : 0u;
+  L.mzm = (fl & 2u) ? 0x7fff7fffu : ~0u;
+  L.mhz = (fl & 2u) ? ~0u : 0u;
+  L.mhw = (fl & 4u) ? ~0u : 0u;
+  L.mswap = (fl & 2u) ? ~0u : 0u;
+  L.rsh = (fl & 2u) ? 31u : 24u;
+  L.fx0 = Q.fx0;
+  const uint32_t st = step_of_quad(p), mi = st == 0 ? 11u : st == 4 ? 12u : 13u;
+  // gathers
+  L.aWD = lane < 16 ? Sb + 4 * T_WD + 8 * lane : lane < 24 ? Sb + 4 * H_MW + 8 * (lane - 16)
+                                                            : Sb + 4 * T_WD + 8 * (lane - 8);
+  if (lane < HR_Q) {
+    L.aAB = Sb + 4 * T_WD + 32 * gg;
+    L.aMX = Sb + 4 * H_MW + 16 * gg;
+  } else if (lane < HR_Q + 4) {
+    const uint32_t pg = lane - HR_Q;
+    L.aAB = Sb + 4 * T_WD + 8 * (24 + 4 * pg);
+    L.aMX = Sb + 4 * T_WD + 8 * (16 + 2 * pg);
+  } else {
+    L.aAB = Sb + 4 * T_WD + 8 * 40;
+    L.aMX = Sb + 4 * T_WD + 8 * 40;
+  }
+  L.aGS = Sb + 4 * T_GS + 128 * gg;
+  L.aXY = L.aGS + 8 * st;
+  L.aM = Sb + 4 * T_GS + 128 * gg + 8 * mi;
+  L.aPG = Sb + 4 * T_PG + 32 * (lane - HR_Q);  // producer lanes only
+  {  // limb table entry lane = 4 w + k, read from the producer outputs in G order (parity 0 / 1)
+    const uint32_t w = lane >> 2, k = lane & 3u, role = w >> 2, pos = w & 3u;
+    const uint32_t i0 = 4 * pos + role, i1 = 4 * ((pos - role) & 3u) + role;
+    const uint32_t a0 = Sb + 4 * T_PG + 8 * i0 + 4 * (k >> 1), a1 = Sb + 4 * T_PG + 8 * i1 + 4 * (k >> 1);
+    L.aLTs = a0 | (a1 << 16);
+    L.ltsh = 16 * (k & 1u);
+    L.aLTd = Sb + 4 * H_LT + 4 * lane;
+  }
+  L.aQ = Sb + 16 * lq;
+  {  // XOR-family limb item `lane`: 0-31 XOR (d1 at +4, d2 at +32), 32-47 XOR24, 48-63 XOR63
+    const uint32_t k = lane & 3u;
+    uint32_t b, E, F, kind;
+    if (lane < 32) {
+      const uint32_t blk = lane >> 2, r = 52 * (blk >> 1) + ((blk & 1u) ? 32u : 4u);
+      b = r + 2 * k;
+      E = A1 * STR + b;
+      F = A1 * STR + b;
+      kind = 0;
+    } else if (lane < 48) {
+      const uint32_t r = 52 * ((lane - 32) >> 2) + 16;
+      b = r + 3 * k;
+      E = A1 * STR + r + 3 * ((k + 1) & 3u) + 1;
+      F = A1 * STR + r + 3 * ((k + 2) & 3u);
+      kind = 1;
+    } else {
+      const uint32_t r = 52 * ((lane - 48) >> 2) + 44;
+      b = r + 2 * k;
+      E = A6 * STR + r + 2 * ((k + 3) & 3u);
+      F = A1 * STR + b;
+      kind = 2;
+    }
+    L.gb = Sb + 4 * b;
+    L.ge = Sb + 4 * E;
+    L.gf = Sb + 4 * F;
+    L.gsel = kind == 1 ? psel(12, 12, 0, 1) : PZ;  // XOR24: s2[b+1] << 16
+    L.gm24 = kind == 1 ? ~0u : 0u;
+    L.gm63 = kind == 2 ? ~0u : 0u;
+    L.gnl = kind == 1 ? ~0u : kind == 2 ? ~1u : 0u;  // side cells: XOR24 == 0, XOR63 <= 1
+    L.grs = kind ? ~0u : 0u;
+    L.gsF = kind == 1 ? 8u : 1u;
+    L.gsH = kind == 1 ? 16u : 2u;
+  }
+  {  // ADD block lane & 15: a1 +0, c1 +12, a2 +28, c2 +40 of G (lane >> 2) & 3
+    const uint32_t w4 = lane & 3u, r = 52 * ((lane >> 2) & 3u) + (w4 == 0 ? 0u : w4 == 1 ? 12u : w4 == 2 ? 28u : 40u);
+    L.ar = Sb + 4 * r;
+    L.m3 = (w4 & 1u) ? 0u : ~0u;  // ADD3: a_5 is an operand
+  }
+#pragma unroll
+  for (int par = 0; par < 2; par++)
+#pragma unroll
+    for (int it = 0; it < HR_CHECKS / FW; it++) {
+      const uint32_t e = c_hr_checks.e[par][it * FW + lane];
+      const uint32_t dr = e & 255u, dc = (e >> 8) & 3u;
+      const uint32_t dst = Sb + 4 * ((A3 + dc) * STR + dr);
+      uint32_t src;
+      if (!((e >> 10) & 1u)) {
+        src = Sb + 4 * (wcol((e >> 19) & 3u) * STR + ((e >> 11) & 255u));
+      } else {
+        const uint32_t w = (e >> 11) & 15u, k = (e >> 15) & 3u, sp = (e >> 17) & 1u;
+        src = Sb + 4 * (H_LT + 64 * sp + 4 * w + k);
+      }
+      L.ce[par][it] = dst | (src << 16);
+    }
+  {  // message copy (lanes 32-63 repeat lanes 0-31)
+    const uint32_t l = lane & 31u, mg = l >> 3, which = (l >> 2) & 1u, k = l & 3u;
+    const uint32_t dr = 52 * mg + (which ? 28u : 0u) + k;
+    L.cm = (Sb + 4 * (A5 * STR + dr)) | ((Sb + 4 * H_MW + 8 * (2 * mg + which) + 2 * k) << 16);
+  }
+  return L;
+}
+
+}  // namespace hr2
+
+template <int MODE>
+__global__ void __launch_bounds__(FW * WAVES, B2F_FUSED_WAVES)
+fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
+                uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
+                uint32_t* __restrict__ fixed, const TileDesc* __restrict__ desc,
+                b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
+                uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk) {
+  using namespace hr2;
+  __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS];
+  uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
+  auto tick = [&](int k) {
+    if (MODE & FZ_CLOCK) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      if (k >= 0) ck[k] += now - tp;
+      tp = now;
+    }
+  };
+  const int tid = threadIdx.x;
+  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
+  if (tid < 22) L[H_ACC + tid] = 0;
+  if (tid == 22) *reinterpret_cast<uint64_t*>(L + H_ACC + 20) = ~0ull;
+  if (tid < 16) L[H_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
+  if (tid < 40) L[H_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
+  __syncthreads();
+  EvalAcc A{L + H_ACC};
+  const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + H_IV);
+  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + H_SG);
+  uint32_t* S = L + H_WAVE + wv * HW_WORDS;  // this wave's staging
+  const uint32_t Sb = lds_byte(S);
+  const Lane K = make_lane(lane, Sb);
+  const bool qlane = lane < HR_Q, p0 = qlane && (lane % G_QUADS) == 0;
+  const bool plane = lane >= HR_Q && lane < HR_Q + 4;
+  const uint32_t pg = lane - HR_Q;
+
+  if (*status == 0) {  // the record kernel accepted the layout
+    const uint64_t used_rows = off[n];
+    const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
+    const uint64_t W = (uint64_t)gridDim.x * WAVES;
+    uint64_t t = (uint64_t)blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(wv);
+    auto raw_desc = [&](uint64_t tt) -> uint4 {
+      const uint64_t ti = tt < n_hr ? tt : 0;
+      const uint4 v = desc[ti].v;
+      return tt < n_hr ? v : make_uint4(0, 0, 0, 0);
+    };
+    HCtx c = hctx(raw_desc(t));
+    uint64_t P = 0;
+    if (t < n_hr) P = load_word(c, lane, in, rec, Sg);
+    asm volatile("" ::"v"(P));  // settled before the loop (see the first form)
+#ifdef B2F_HR_PF2  // the word two tiles ahead in flight: the settle waits only for stores two tiles old
+    HCtx cn = hctx(raw_desc(t + W));
+    uint64_t Pn = load_word(cn, lane, in, rec, Sg);
+    uint4 dn = raw_desc(t + 2 * W);
+#else
+    uint4 dn = raw_desc(t + W);
+#endif
+    for (; t < n_hr; t += W) {
+      tick(-1);
+#ifdef B2F_HR_PF2
+      const HCtx cnn = hctx(dn);
+      const uint64_t Pnn = load_word(cnn, lane, in, rec, Sg);  // past the end: a harmless load
+#else
+      const HCtx cn = hctx(dn);
+      const uint64_t Pn = load_word(cn, lane, in, rec, Sg);  // past the end: a harmless load
+#endif
+      // ---- 1. the tile's words into the wave's LDS
+      st64(K.aWD, P);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      tick(0);
+      // ---- 2. chains: quad lanes their G of half-round hr, producer lanes G pg of hr - 1
+      const uint4 ab = ld128(K.aAB), cd = ld128(K.aAB + 16), mm = ld128(K.aMX);
+      const uint64_t a = mk64(ab.x, ab.y), b = mk64(ab.z, ab.w), cc = mk64(cd.x, cd.y), d = mk64(cd.z, cd.w);
+      const uint64_t mx = mk64(mm.x, mm.y), my = mk64(mm.z, mm.w);
+      const uint64_t a1 = a + b + mx;
+      const uint64_t d1 = rotr64(d ^ a1, 32);
+      const uint64_t c1 = cc + d1;
+      const uint64_t b1 = rotr64(b ^ c1, 24);
+      const uint64_t a2 = a1 + b1 + my;
+      const uint64_t d2 = rotr64(d1 ^ a2, 16);
+      const uint64_t c2 = c1 + d2;
+      if (p0) {
+        const uint32_t g = K.aGS;  // this G's chain record
+        st128(g, make_uint4(lo32(a), hi32(a), lo32(d), hi32(d)));
+        st128(g + 16, make_uint4(lo32(cc), hi32(cc), lo32(b), hi32(b)));
+        st128(g + 32, make_uint4(lo32(a1), hi32(a1), lo32(d1), hi32(d1)));
+        st128(g + 48, make_uint4(lo32(c1), hi32(c1), lo32(b1), hi32(b1)));
+        st128(g + 64, make_uint4(lo32(a2), hi32(a2), lo32(d2), hi32(d2)));
+        st128(g + 80, make_uint4(lo32(c2), hi32(c2), lo32(mx), hi32(mx)));
+        st128(g + 96, make_uint4(lo32(my), hi32(my), 0u, 0u));
+      }
+      if (plane) {
+        uint64_t o0, o1, o2, o3;
+        if (c.hr == 0) {  // the initial work vector: h, IV, v12..v14 = IV ^ (t0, t1, fmask)
+          o0 = a;
+          o1 = b;
+          o2 = IV[pg];
+          const uint64_t tw = pg < 2 ? d : (pg == 2 ? ((d >> 32) ? ~0ull : 0ull) : 0ull);
+          o3 = IV[pg + 4] ^ tw;
+        } else {
+          o0 = a2;
+          o1 = rotr64(b1 ^ c2, 63);
+          o2 = c2;
+          o3 = d2;
+        }
+        st128(K.aPG, make_uint4(lo32(o0), hi32(o0), lo32(o1), hi32(o1)));
+        st128(K.aPG + 16, make_uint4(lo32(o2), hi32(o2), lo32(o3), hi32(o3)));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+#ifdef B2F_HR_PF2
+      dn = raw_desc(t + 3 * W);  // scalar load; retires during the assignment
+#else
+      dn = raw_desc(t + 2 * W);  // scalar load; retires during the assignment
+#endif
+      tick(1);
+      // ---- 3. operands of the lane's quad, the lane's limb-table entry
+      const uint64_t X = ld64(K.aXY), Y = ld64(K.aXY + 24), M = ld64(K.aM);
+      const uint32_t par = c.hr ? ((c.hr & 1u) ^ 1u) : 0u;  // G order of the producer outputs
+      const uint32_t pv = ld32(par ? K.aLTs >> 16 : K.aLTs & 0xffffu);
+      const uint32_t lv = (pv >> K.ltsh) & 0xffffu;
+      st32(K.aLTd, lv);
+      st32(K.aLTd + 256, spread16(lv));
+      // ---- 4. the cells
+      const uint64_t s1 = X + Y, Sm = s1 + M;
+      const uint32_t carry = (uint32_t)(s1 < X) + (uint32_t)(Sm < s1);
+      const uint64_t Z = X ^ Y, O = X & Y;
+      const uint32_t Tl = sel32(K.madd, lo32(Sm), lo32(Z) & K.mzm), Th = sel32(K.madd, hi32(Sm), hi32(Z) & K.mzm);
+      const uint32_t Ol = lo32(O), Oh = hi32(O);
+      // w = rotr(z, 24) (XOR24) or rotr(z, 63) (XOR63)
+      const uint32_t zu = sel32(K.mswap, lo32(Z), hi32(Z)), zv = sel32(K.mswap, hi32(Z), lo32(Z));
+      const uint32_t Wl = __builtin_amdgcn_alignbit(zu, zv, K.rsh), Wh = __builtin_amdgcn_alignbit(zv, zu, K.rsh);
+      uint32_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[j] = perm(Ol, Tl, K.selL[j]) | perm(Oh, Th, K.selH[j]);
+      // operand slots
+      const uint32_t xA = perm(hi32(X), lo32(X), K.slA), xB = perm(hi32(X), lo32(X), K.slB);
+      const uint32_t yA = perm(hi32(Y), lo32(Y), K.slA), yB = perm(hi32(Y), lo32(Y), K.slB);
+      const uint32_t wA = perm(Wh, Wl, K.slA) & K.mhw, wB = perm(Wh, Wl, K.slB) & K.mhw;
+      const uint32_t zA = (perm(hi32(Z), lo32(Z), K.slA) >> 15) & K.mhz;
+      const uint32_t zB = (perm(hi32(Z), lo32(Z), K.slB) >> 15) & K.mhz;
+      const uint32_t P3 = sel32(K.madd, hi32(X), spread16(xB)), Q3 = sel32(K.madd, lo32(X), spread16(xA));
+      const uint32_t P4 = sel32(K.madd, hi32(Y), spread16(yB)), Q4 = sel32(K.madd, lo32(Y), spread16(yA));
+      const uint32_t swA = spread16(wA), swB = spread16(wB);
+      if (qlane) {
+        const uint64_t qrow = c.row0 + 4ull * lane;
+        emit<MODE>(S, A0, lane, qrow, tag_of(v[0]), tag_of(v[1]), tag_of(v[2]), tag_of(v[3]), adv, fixed, total_rows, inj, true);
+        emit<MODE>(S, A1, lane, qrow, v[0], v[1], v[2], v[3], adv, fixed, total_rows, inj, true);
+        emit<MODE>(S, A2, lane, qrow, spread16(v[0]), spread16(v[1]), spread16(v[2]), spread16(v[3]), adv, fixed, total_rows, inj, true);
+        emit<MODE>(S, A3, lane, qrow, perm(P3, Q3, K.slot[0]), perm(P3, Q3, K.slot[1]), perm(P3, Q3, K.slot[2]),
+                   perm(P3, Q3, K.slot[3]), adv, fixed, total_rows, inj, true);
+        emit<MODE>(S, A4, lane, qrow, perm(P4, Q4, K.slot[0]), perm(P4, Q4, K.slot[1]), perm(P4, Q4, K.slot[2]),
+                   perm(P4, Q4, K.slot[3]), adv, fixed, total_rows, inj, true);
+        emit<MODE>(S, A5, lane, qrow, perm(hi32(M), lo32(M), limb_sel(0)), perm(hi32(M), lo32(M), limb_sel(1)),
+                   perm(hi32(M), lo32(M), limb_sel(2)), perm(hi32(M), lo32(M), limb_sel(3)), adv, fixed, total_rows, inj, true);
+        emit<MODE>(S, A6, lane, qrow, perm(zB, zA, K.slot[0]), perm(zB, zA, K.slot[1]), perm(zB, zA, K.slot[2]),
+                   perm(zB, zA, K.slot[3]), adv, fixed, total_rows, inj, true);
+        emit<MODE>(S, A7, lane, qrow, perm(wB, wA, K.slot[0]), perm(wB, wA, K.slot[1]), perm(wB, wA, K.slot[2]),
+                   perm(wB, wA, K.slot[3]), adv, fixed, total_rows, inj, true);
+        emit<MODE>(S, A8, lane, qrow, perm(swB, swA, K.slot[0]), perm(swB, swA, K.slot[1]), perm(swB, swA, K.slot[2]),
+                   perm(swB, swA, K.slot[3]), adv, fixed, total_rows, inj, true);
+        // last: these two columns hold the transient words until here
+        emit<MODE>(S, A9, lane, qrow, carry & K.madd, 0u, 0u, 0u, adv, fixed, total_rows, inj, true);
+        emit<MODE>(S, FXC, lane, qrow, K.fx0, 0u, 0u, 0u, adv, fixed, total_rows, inj, true);
+      }
+      tick(2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staging is complete
+      __builtin_amdgcn_wave_barrier();
+#ifdef B2F_HR_SETTLE_EARLY  // diagnostics: the first form's placement (waits for the previous stores)
+      asm volatile("" ::"v"(Pn));
+#endif
+      // ---- 5. stores, then the wait for the next tile's word: vmcnt counts loads and stores
+      // in issue order, so placed after this tile's 11 stores it is vmcnt(11) -- the load and
+      // the PREVIOUS tile's stores, issued a tile ago -- never a wait for these stores
+      tick(3);
+      store_staged<MODE>(S, lane, HR_Q, c.row0, adv, fixed, total_rows);
+      tick(4);
+#ifndef B2F_HR_SETTLE_EARLY
+      asm volatile("" ::"v"(Pn));
+#endif
+      tick(7);
+      // ---- 6. fast checks: acc |= (every identity's lhs ^ rhs)
+      uint32_t acc = 0;
+      if (MODE & (FZ_LOOKUP | FZ_GATES)) {
+        const uint4 q0 = ld128(K.aQ + 4 * A0 * STR), q1 = ld128(K.aQ + 4 * A1 * STR), q2 = ld128(K.aQ + 4 * A2 * STR);
+        const uint4 fx = ld128(K.aQ + 4 * FXC * STR);
+        if (MODE & FZ_LOOKUP) {
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const uint32_t de = comp(q1, j);
+            acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(q0, j)) | (spread16(de) ^ comp(q2, j));
+          }
+        }
+        if (MODE & FZ_GATES) acc |= (fx.x ^ K.fx0) | fx.y | fx.z | fx.w;
+      }
+      if (MODE & FZ_GATES) {
+        {  // XOR / XOR24 / XOR63 limb item
+          const uint32_t gb = K.gb;
+          const uint32_t x3 = ld32(gb + 4 * A3 * STR), x4 = ld32(gb + 4 * A4 * STR);
+          const uint32_t s0 = ld32(gb + 4 * A2 * STR), s1v = ld32(gb + 4 * (A2 * STR + 1)), s2v = ld32(gb + 4 * (A2 * STR + 2));
+          const uint32_t z6 = ld32(gb + 4 * A6 * STR), t0 = ld32(gb), t1 = ld32(gb + 4);
+          const uint32_t w7 = ld32(gb + 4 * A7 * STR), w8 = ld32(gb + 4 * A8 * STR);
+          const uint32_t E = ld32(K.ge), E2 = ld32(K.ge + 4 * (A2 - A1) * STR);
+          const uint32_t F = ld32(K.gf), H = ld32(K.gf + 4 * (A2 - A1) * STR);
+          const uint32_t R = s0 + perm(0u, s1v, K.gsel) + ((z6 << 30) & K.gm63) + 2 * sel32(K.gm24, s2v, s1v);
+          acc |= (x3 + x4) ^ R;
+          acc |= (t0 | (t1 & K.gm24) | (z6 & K.gm63)) & K.gnl;
+          const uint32_t G = sel32(K.gm24, E2, E);
+          acc |= (((E + (F << K.gsF)) ^ w7) | ((G + (H << K.gsH)) ^ w8)) & K.grs;
+        }
+        {  // ADD block (lanes 16-63 repeat lanes 0-15)
+          const uint4 s = ld128(K.ar + 4 * A1 * STR), x = ld128(K.ar + 4 * A3 * STR);
+          const uint4 y = ld128(K.ar + 4 * A4 * STR), z = ld128(K.ar + 4 * A5 * STR);
+          const uint32_t a9 = ld32(K.ar + 4 * A9 * STR);
+          int32_t cy = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            cy += (int32_t)(comp(x, k) + comp(y, k) + (comp(z, k) & K.m3) - comp(s, k));
+            acc |= (uint32_t)cy & 0xffffu;
+            cy >>= 16;
+          }
+          acc |= (uint32_t)cy ^ a9;
+        }
+      }
+      if (MODE & FZ_COPIES) {
+        const bool odd = c.hr & 1u;
+#pragma unroll
+        for (int it = 0; it < HR_CHECKS / FW; it++) {
+          const uint32_t e = odd ? K.ce[1][it] : K.ce[0][it];
+          acc |= ld32(e & 0xffffu) ^ ld32(e >> 16);
+        }
+        acc |= ld32(K.cm & 0xffffu) ^ ld16(K.cm >> 16);
+      }
+      bool bad = acc != 0;
+      if (MODE & FZ_INJECT)  // the test hook: its instance is checked exactly
+        bad |= inj.row >= c.off && inj.row < c.off + FIXED_ROWS + (uint64_t)ROUND_ROWS * c.rounds;
+      tick(5);
+      if (__builtin_amdgcn_ballot_w64(bad)) {  // rare: a failure in this tile, record it exactly
+        Ctx c1;
+        c1.kind = T_HR;
+        c1.inst = c.inst;
+        c1.rounds = c.rounds;
+        c1.hr = c.hr;
+        c1.nq = HR_Q;
+        c1.off = c.off;
+        c1.st = c.st;
+        c1.row0 = c.row0;
+        const WaveTile T{S};
+        const uint32_t* LT = S + H_LT;
+        const uint64_t* MW = reinterpret_cast<const uint64_t*>(S + H_MW);
+        auto state = [&](uint32_t w, uint32_t k, uint32_t sp) { return LT[64 * sp + 4 * w + k]; };
+        Fails<true> Rf{A, false};
+        hr_msg_copies<MODE, true>(Rf, T, lane, c1, MW[2 * ((lane >> 3) & 3u) + ((lane >> 2) & 1u)], Sg, inj);
+        hr_checks<MODE, true>(Rf, T, lane, c1, &c_hr_checks.e[c.hr & 1u][0], state, inj, defer, defer_cap);
+      }
+      // the staging is rewritten by the next tile: keep the compiler from hoisting those writes
+      // above this tile's reads (the wave's LDS operations execute in order)
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      tick(6);
+      c = cn;
+      P = Pn;
+#ifdef B2F_HR_PF2
+      cn = cnn;
+      Pn = Pnn;
+#endif
+    }
+  }
+  if ((MODE & FZ_CLOCK) && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) atomicAdd(&clk[8 * wv + k], (unsigned long long)ck[k]);
+  }
+  __syncthreads();
+  flush_report(A, rep, tid);
+}
+
 // Per-tile descriptors {instance, tile index inside it, rounds, first state index}: thread per
 // instance, 2 rounds + 2 tiles each (init, half-rounds, final).
 __global__ void tile_desc_kernel(const uint64_t* __restrict__ off, const b2f_input* __restrict__ in,
@@ -921,6 +1513,13 @@ __global__ void deferred_gates_kernel(const uint32_t* __restrict__ adv, const ui
 
 constexpr uint32_t DEFER_CAP = 4096;
 
+// the half-round launch: the second form (fused_hr_kernel); -DB2F_FUSED_V1 builds the first
+#ifdef B2F_FUSED_V1
+#define B2F_HR_KERNEL(M) (fused_kernel<M, PART_HR>)
+#else
+#define B2F_HR_KERNEL(M) (fused_hr_kernel<M>)
+#endif
+
 }  // namespace
 
 namespace b2f {
@@ -958,7 +1557,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   static int per_cu[2] = {0, 0};
   if (!per_cu[0]) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fused_kernel<FZ_FULL, PART_HR>, FW * WAVES, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, B2F_HR_KERNEL(FZ_FULL), FW * WAVES, 0) !=
             hipSuccess || nb < 1)
       nb = 2;
     per_cu[0] = nb;
@@ -976,7 +1575,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   switch (mode) {
 #define B2F_FUSED(M)                                                                               \
   case M:                                                                                          \
-    hipLaunchKernelGGL((fused_kernel<M, PART_HR>), dim3(grid), dim3(FW * WAVES), 0, s, d_in, n,     \
+    hipLaunchKernelGGL(B2F_HR_KERNEL(M), dim3(grid), dim3(FW * WAVES), 0, s, d_in, n,              \
                        d_off, total_rows, rec, d_adv, d_fixed, desc, d_rep, d_status, inj, defer,  \
                        DEFER_CAP, clk);                                                            \
     hipLaunchKernelGGL((fused_kernel<M, PART_EDGE>), dim3(grid_e), dim3(FW * WAVES), 0, s, d_in, n, \
