@@ -1068,7 +1068,11 @@ __device__ __forceinline__ uint64_t load_word(const HCtx& c, uint32_t lane, cons
   if (grp < 2 || (ps && grp < 6 && h != 0)) p = rec + 16ull * (c.st + sh) + word;
   else if (grp == 2 || (pm && h != 0)) p = x->m + sidx;
   else if (ps && grp < 6) p = role == 0 ? x->h + gl : role == 1 ? x->h + gl + 4 : (role == 3 && gl < 2) ? x->t + gl : fw;
+#ifdef B2F_FZ_NOLOAD  // diagnostics: the word without memory traffic (wrong trace)
+  return reinterpret_cast<uint64_t>(p) * 0x9E3779B97F4A7C15ull;
+#else
   return *p;
+#endif
 }
 
 // The per-lane constants of the tile loop (resolved once).
