@@ -27,7 +27,7 @@ def per_kernel(d, counter):
             k = r["Kernel_Name"]
             kind = ("fill" if "fill_kernel" in k else "eval" if "eval_kernel" in k
                     else "fill_eval_edge" if "fused_kernel<27, 2>" in k
-                    else "fill_eval" if "fused_kernel" in k else None)
+                    else "fill_eval" if ("fused_kernel" in k or "fused_hr_kernel" in k) else None)
             if kind is None:
                 continue
             per_dispatch[r["Dispatch_Id"]] += float(r["Counter_Value"])
