@@ -188,6 +188,39 @@ __global__ void __launch_bounds__(256) wave_rr_nostore(uint32_t* adv, uint64_t t
   if (h == 0x12345678u) adv[lane] = h;
 }
 
+// the same order with LDS-latency-bound work in front of the stores: `work` dependent LDS round
+// trips per tile (write, wait, read a neighbour lane's word), the shape of a tile whose phases
+// hand data between lanes through LDS; NOSTORE: the work alone
+template <int STEP, bool NOSTORE>
+__global__ void __launch_bounds__(256) wave_rr_ldswork(uint32_t* adv, uint64_t total_rows, int work) {
+  __shared__ uint32_t L[256];
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t* S = L + (threadIdx.x & ~63u);
+  const uint64_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  const uint64_t total_quads = total_rows >> 2;
+  const uint64_t n_t = (total_quads + STEP - 1) / STEP;
+  uint32_t h = lane;
+  for (uint64_t t = wid; t < n_t; t += nw) {
+    const uint64_t q = t * STEP + lane;
+    h ^= (uint32_t)q;
+    for (int k = 0; k < work; k++) {
+      S[lane] = h;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      h = S[(lane + 7u) & 63u] * 0x9E3779B1u + (uint32_t)k;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!NOSTORE && lane < STEP && q < total_quads) {
+#pragma unroll
+      for (int c = 0; c < 11; c++)
+        __builtin_nontemporal_store(u32x4{h + c, h ^ c, h * c, h - c},
+                                    reinterpret_cast<u32x4*>(adv + (uint64_t)c * total_rows + 4 * q));
+    }
+  }
+  if (NOSTORE && h == 0x12345678u) adv[lane] = h;
+}
+
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? atoi(argv[1]) : (1u << 18);
   const uint32_t rows_per = 228 + 416 * 12;
@@ -219,6 +252,23 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
   const uint64_t nt = (total + 1023) / 1024;
+  if (argc > 2 && argv[2][0] == 'l') {  // LDS-latency work vs VALU work, with and without stores
+    for (int work : {120}) {
+      char nm[96];
+      snprintf(nm, sizeof nm, "work%d_nostore", work);
+      run(nm, [&] { hipLaunchKernelGGL(wave_rr_nostore<52>, dim3(cus * 4), dim3(256), 0, 0, adv, total, work); });
+      snprintf(nm, sizeof nm, "work%d_burst", work);
+      run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<52, false, false>), dim3(cus * 4), dim3(256), 0, 0, adv, total, work); });
+    }
+    for (int work : {4, 8, 16}) {
+      char nm[96];
+      snprintf(nm, sizeof nm, "ldswork%d_nostore", work);
+      run(nm, [&] { hipLaunchKernelGGL((wave_rr_ldswork<52, true>), dim3(cus * 4), dim3(256), 0, 0, adv, total, work); });
+      snprintf(nm, sizeof nm, "ldswork%d_burst", work);
+      run(nm, [&] { hipLaunchKernelGGL((wave_rr_ldswork<52, false>), dim3(cus * 4), dim3(256), 0, 0, adv, total, work); });
+    }
+    return 0;
+  }
   for (int w : {8, 4}) {
     char nm[64];
     snprintf(nm, sizeof nm, "tile_rr_%dwg", w);
