@@ -170,7 +170,7 @@ struct Ctx {
   uint64_t off, st, row0;  // instance offset, its first state index, first row of the tile
 };
 
-__device__ __forceinline__ Ctx make_ctx(uint64_t t, uint64_t t_inst, const uint4& raw,
+[[maybe_unused]] __device__ __forceinline__ Ctx make_ctx(uint64_t t, uint64_t t_inst, const uint4& raw,
                                         uint64_t used_rows, uint64_t total_rows) {
   Ctx c;
   c.inst = __builtin_amdgcn_readfirstlane(raw.x);
@@ -1476,6 +1476,471 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
   flush_report(A, rep, tid);
 }
 
+// ============================================================================================
+// The edge launch (PART_EDGE), second form: ONE wave tile per instance holds both of its edge
+// regions -- the init region on lanes 0-40 (INW h / m / t, FMASK, CONST IV, XOR v12..v14) and the
+// final region on lanes 41-56 (XOR3 + digest), so the init region's h cells (the XOR3 H operands'
+// copy sources) are staged in the same tile; lanes 57-60 recompute the final state from the last
+// half-round (the XOR3 V / U operands' producer values). The zero rows past the last instance
+// follow as 64-quad tiles. Fast 32-bit checks as in the half-round launch; a flagged tile is done
+// again, region by region, by the first form's edge path (assignment, stores, exact checks).
+namespace edge2 {
+constexpr uint32_t NQ_I = INIT_Q, NQ_F = FINAL_Q, NQ = INIT_Q + FINAL_Q;  // 41, 16, 57
+constexpr int STR_E = 232;  // staged rows per column: init rows 0-163, final rows 164-227
+static_assert(4 * NQ_I == INIT_ROWS && 4 * NQ <= (uint32_t)STR_E && STR_E % 4 == 0, "lane = quad, rows 4 lane");
+enum : uint32_t { E_INW = 1, E_FMASK = 2, E_CONST = 4, E_XOR = 8, E_XOR3 = 16 };
+struct EdgeProg {
+  uint32_t selL[4], selH[4];  // a_1 of row j = perm(O_lo, T_lo, selL) | perm(O_hi, T_hi, selH)
+  uint32_t kind, qq, a;       // block kind, quad inside an XOR / XOR3 block, word index
+};
+struct EdgeProgs {
+  EdgeProg e[NQ];
+};
+constexpr EdgeProgs make_edge_progs() {
+  EdgeProgs P{};
+  for (uint32_t l = 0; l < NQ; l++) {
+    EdgeProg& g = P.e[l];
+    uint32_t kind = 0, qq = 0, a = 0;
+    if (l < 26) {
+      kind = E_INW;
+      a = l;
+    } else if (l == 26) {
+      kind = E_FMASK;
+    } else if (l < 35) {
+      kind = E_CONST;
+      a = l - 27;
+    } else if (l < NQ_I) {
+      kind = E_XOR;
+      a = (l - 35) >> 1;
+      qq = (l - 35) & 1u;
+    } else {
+      kind = E_XOR3;
+      a = (l - NQ_I) >> 1;
+      qq = (l - NQ_I) & 1u;
+    }
+    g.kind = kind;
+    g.qq = qq;
+    g.a = a;
+    for (uint32_t j = 0; j < 4; j++) {
+      const bool xr = kind & (E_XOR | E_XOR3);
+      const uint32_t k = xr ? 2 * qq + (j >> 1) : j, so = (xr && (j & 1u)) ? 4u : 0u;  // XOR: rows 2h z/e, 2h+1 o/maj
+      const uint32_t half = k >> 1, bb = 2 * (k & 1u);
+      const uint32_t sel = hr2::psel(bb + so, bb + 1 + so, 12, 12);
+      g.selL[j] = half == 0 ? sel : hr2::PZ;
+      g.selH[j] = half == 1 ? sel : hr2::PZ;
+    }
+  }
+  return P;
+}
+__constant__ EdgeProgs c_eprogs = make_edge_progs();
+
+// Copy checks of an edge tile (120): the init XORs' operands (IV_4..6 from the CONST blocks, t0 /
+// t1 / fmask from their INW / FMASK blocks) and the XOR3 operands (H from the INW h blocks, V and
+// U from the final state's producer values). Entry: dst row (bits 0-7), dst column a_3 + c
+// (8-9), source kind (10: 0 staged a_2 cell at row bits 11-18, 1 limb-table entry bits 11-16).
+constexpr int E_CHECKS = 120;
+struct EdgeChecks {
+  uint32_t e[128];
+};
+constexpr EdgeChecks make_edge_checks() {
+  EdgeChecks T{};
+  uint32_t n = 0;
+  for (uint32_t a = 0; a < 3; a++)
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t row = 140 + 8 * a + 2 * k;
+      T.e[n++] = row | (0u << 8) | ((108 + 4 * (4 + a) + k) << 11);
+      T.e[n++] = row | (1u << 8) | ((a < 2 ? 96 + 4 * a + k : 104 + k) << 11);
+    }
+  for (uint32_t i = 0; i < 8; i++)
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t row = INIT_ROWS + 8 * i + 2 * k;
+      T.e[n++] = row | (0u << 8) | ((4 * i + k) << 11);
+      T.e[n++] = row | (1u << 8) | (1u << 10) | ((4 * i + k) << 11);
+      T.e[n++] = row | (2u << 8) | (1u << 10) | ((4 * (i + 8) + k) << 11);
+    }
+  for (uint32_t i = n; i < 128; i++) T.e[i] = T.e[i - n];  // duplicates fill the last lanes
+  if (n != E_CHECKS) T.e[0] = 0xffffffffu;
+  return T;
+}
+static_assert(make_edge_checks().e[0] != 0xffffffffu, "120 edge copy checks");
+__constant__ EdgeChecks c_echecks = make_edge_checks();
+
+// wave LDS (words): staging [11][STR_E], limb table (spread limbs of the final state, 4 w + k),
+// producer outputs (16 u64 by word). The first form's edge path reuses the same words with its own
+// carve (staging [11][208], prod, canonical flags), inside this one.
+constexpr int E_LT = NSTAGE * STR_E;
+constexpr int E_PROD = E_LT + 64;
+constexpr int EW_WORDS = E_PROD + 32;
+static_assert(EW_WORDS >= WAVE_WORDS, "the first form's edge carve fits");
+constexpr int E_ACC = 0, E_IV = 24, E_SG = E_IV + 16, E_WAVE = E_SG + 40;
+constexpr int E_WORDS = E_WAVE + WAVES * EW_WORDS;
+static_assert(E_WAVE % 4 == 0 && EW_WORDS % 4 == 0 && E_PROD % 2 == 0, "aligned carve");
+static_assert(4 * E_WORDS < 65536, "LDS byte addresses fit 16 bits");
+
+// store of one region of an edge tile: lane `lane` writes quad lane - q0 of the region
+__device__ __forceinline__ void region_store(uint32_t* base, uint32_t nq, uint32_t lane, uint32_t q0, uint4 v) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const i32x4 rsrc = {(int32_t)(uint32_t)a, (int32_t)(uint32_t)(a >> 32), (int32_t)(nq * 16u), 0x00020000};
+  b2f_raw_buffer_store_v4(i32x4{(int32_t)v.x, (int32_t)v.y, (int32_t)v.z, (int32_t)v.w}, rsrc,
+                          (int)(16u * (lane - q0)), 0, BUF_NT);  // lanes outside: past the range
+}
+
+struct ECtx {
+  uint32_t inst, rounds;
+  uint64_t off, st;
+};
+}  // namespace edge2
+
+// One column of an edge tile's quad into the staging (STR_E rows per column), the test-only
+// injection applied as emit applies it.
+template <int MODE>
+__device__ __forceinline__ void stage_e(uint32_t* S, int col, uint32_t lane, uint64_t qrow, uint32_t v0,
+                                        uint32_t v1, uint32_t v2, uint32_t v3, const Inject& inj) {
+  if (MODE & FZ_INJECT) {
+    if ((inj.row >> 2) == (qrow >> 2) && inj.col == (uint32_t)col) {
+      const uint32_t j = (uint32_t)inj.row & 3u;
+      v0 ^= j == 0 ? inj.mask : 0u;
+      v1 ^= j == 1 ? inj.mask : 0u;
+      v2 ^= j == 2 ? inj.mask : 0u;
+      v3 ^= j == 3 ? inj.mask : 0u;
+    }
+  }
+  *reinterpret_cast<uint4*>(S + col * edge2::STR_E + 4 * lane) = make_uint4(v0, v1, v2, v3);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(FW * WAVES, 3)
+fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
+                  uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
+                  uint32_t* __restrict__ fixed, uint32_t* __restrict__ redo,
+                  b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
+                  uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk) {
+  using namespace hr2;
+  using namespace edge2;
+  (void)clk;
+  __shared__ __attribute__((aligned(16))) uint32_t L[E_WORDS];
+  const int tid = threadIdx.x;
+  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
+  if (tid < 22) L[E_ACC + tid] = 0;
+  if (tid == 22) *reinterpret_cast<uint64_t*>(L + E_ACC + 20) = ~0ull;
+  if (tid < 16) L[E_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
+  if (tid < 40) L[E_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
+  __syncthreads();
+  EvalAcc A{L + E_ACC};
+  const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + E_IV);
+  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + E_SG);
+  uint32_t* S = L + E_WAVE + wv * EW_WORDS;
+  const uint32_t Sb = lds_byte(S);
+  uint64_t* prod = reinterpret_cast<uint64_t*>(S + E_PROD);
+
+  // per-lane constants
+  const uint32_t lq = lane < NQ ? lane : lane - NQ;  // the quad a lane checks (>= 57: a repeat)
+  const EdgeProg& G = c_eprogs.e[lq];
+  uint32_t selL[4], selH[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    selL[j] = G.selL[j];
+    selH[j] = G.selH[j];
+  }
+  const uint32_t kind = G.kind, qq = G.qq, wa = G.a;
+  const uint32_t mINW = kind == E_INW ? ~0u : 0u, mFM = kind == E_FMASK ? ~0u : 0u;
+  const uint32_t mCONST = kind == E_CONST ? ~0u : 0u, mX3 = kind == E_XOR3 ? ~0u : 0u;
+  const uint32_t mXOR = (kind & (E_XOR | E_XOR3)) ? ~0u : 0u;
+  const uint32_t m78 = mINW | (qq == 0 ? mX3 : 0u), mDG = qq == 0 ? mX3 : 0u;
+  uint4 fxq = make_uint4(0, 0, 0, 0);  // the keygen fixed cells of the lane's quad
+  if (kind == E_INW) fxq.x = 1u << S_ABCD;
+  if (kind == E_FMASK) fxq.x = 1u << S_FMASK;
+  if (kind == E_XOR && qq == 0) fxq.x = 1u << S_XOR;
+  if (kind == E_XOR3 && qq == 0) fxq.x = (1u << S_XOR3) | (1u << S_DIGEST);
+  if (kind == E_CONST) {
+    const uint64_t w = IV[wa];
+    fxq = make_uint4((1u << S_CONST) | ((uint32_t)(w & 0xffffu) << 16), (1u << S_CONST) | ((uint32_t)((w >> 16) & 0xffffu) << 16),
+                     (1u << S_CONST) | ((uint32_t)((w >> 32) & 0xffffu) << 16), (1u << S_CONST) | ((uint32_t)(w >> 48) << 16));
+  }
+  const uint32_t aQ = Sb + 16 * lq, aQn = Sb + 16 * (lq + 1);
+  uint32_t ce[2];
+#pragma unroll
+  for (int it = 0; it < 2; it++) {
+    const uint32_t e = c_echecks.e[it * FW + lane];
+    const uint32_t dst = Sb + 4 * ((A3 + ((e >> 8) & 3u)) * STR_E + (e & 255u));
+    const uint32_t src = (e >> 10) & 1u ? Sb + 4 * (E_LT + ((e >> 11) & 63u)) : Sb + 4 * (A2 * STR_E + ((e >> 11) & 255u));
+    ce[it] = dst | (src << 16);
+  }
+  const bool plane = lane >= NQ && lane < NQ + 4;
+  const uint32_t pg = lane - NQ;
+
+  if (*status == 0) {
+    const uint64_t used_rows = off[n];
+    const uint64_t n_pad = ((total_rows - used_rows) / 4 + PAD_Q - 1) / PAD_Q;
+    const uint64_t t_all = (uint64_t)n + n_pad;
+    const uint64_t W = (uint64_t)gridDim.x * WAVES;
+    uint64_t t = (uint64_t)blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(wv);
+    auto ectx = [&](uint64_t tt) {
+      ECtx c;
+      const uint32_t i = tt < n ? (uint32_t)tt : 0u;
+      c.inst = i;
+      c.off = off[i];
+      c.rounds = in[i].rounds;
+      c.st = 2 * ((c.off - (uint64_t)FIXED_ROWS * i) / ROUND_ROWS) + i;
+      return c;
+    };
+    // the words of one tile: init lanes their block's word, final lanes h_i and the final state's
+    // v_i, v_{i+8}; producer lanes the last half-round's G operands (or the initial words at 0 rounds)
+    auto words = [&](const ECtx& c) {
+      const b2f_input* x = in + c.inst;
+      const uint64_t* fw = reinterpret_cast<const uint64_t*>(&x->rounds);  // rounds | f << 32
+      const uint64_t* p[6] = {fw, fw, fw, fw, fw, fw};
+      if (lane < 26) {
+        p[0] = lane < 8 ? x->h + lane : lane < 24 ? x->m + (lane - 8) : x->t + (lane - 24);
+      } else if (lane >= 35 && lane < NQ_I) {
+        const uint32_t a = (lane - 35) >> 1;
+        p[0] = a < 2 ? x->t + a : fw;
+      } else if (lane >= NQ_I && lane < NQ) {
+        const uint32_t i = (lane - NQ_I) >> 1;
+        const uint64_t* fin = rec + 16ull * (c.st + 2ull * c.rounds);
+        p[0] = x->h + i;
+        p[1] = fin + i;
+        p[2] = fin + i + 8;
+      } else if (plane) {
+        if (c.rounds == 0) {
+          p[0] = x->h + pg;
+          p[1] = x->h + pg + 4;
+          p[3] = pg < 2 ? x->t + pg : fw;
+        } else {
+          const uint32_t hp = 2 * c.rounds - 1, g = pg + 4;  // the last half-round: diagonal G's
+          const uint64_t* s = rec + 16ull * (c.st + hp);
+          const uint32_t gi = gidx_word(g);
+          const uint8_t* sg = Sg + 16 * ((hp >> 1) % 10) + 2 * g;
+          p[0] = s + (gi & 15u);
+          p[1] = s + ((gi >> 8) & 15u);
+          p[2] = s + ((gi >> 16) & 15u);
+          p[3] = s + ((gi >> 24) & 15u);
+          p[4] = x->m + sg[0];
+          p[5] = x->m + sg[1];
+        }
+      }
+      Ops o;
+#pragma unroll
+      for (int k = 0; k < 6; k++) o.w[k] = *p[k];
+      o.w[6] = 0;
+      return o;
+    };
+    ECtx c = ectx(t);
+    Ops P = words(c);  // past the instances: instance 0's words (harmless, unused)
+    settle(P);
+    ECtx cn = ectx(t + W);
+    for (; t < t_all; t += W) {
+      const ECtx cnn = ectx(t + 2 * W);  // scalar loads, two tiles ahead
+      const Ops Pn = words(cn);         // unconditional: the compiler counts vmcnt exactly
+      if (t < n) {
+        // ---- one instance's init + final regions
+        const uint64_t row_i = c.off, row_f = c.off + INIT_ROWS + (uint64_t)ROUND_ROWS * c.rounds;
+        const uint64_t qrow = lane < NQ_I ? row_i + 4ull * lane : row_f + 4ull * (lane - NQ_I);
+        const uint64_t w0 = P.w[0];
+        const bool fbit = (w0 >> 32) != 0;
+        uint64_t X = 0, Y = 0, U = 0, T, O = 0;
+        if (kind == E_CONST) {
+          T = IV[wa];
+        } else if (kind == E_FMASK) {
+          T = fbit ? ~0ull : 0ull;
+        } else if (kind == E_XOR) {
+          X = IV[4 + wa];
+          Y = wa < 2 ? w0 : (fbit ? ~0ull : 0ull);
+          T = X ^ Y;
+          O = X & Y;
+        } else if (kind == E_XOR3) {
+          X = w0;
+          Y = P.w[1];
+          U = P.w[2];
+          T = X ^ Y ^ U;
+          O = (X & Y) | (X & U) | (Y & U);
+        } else {
+          T = w0;
+        }
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = perm(lo32(O), lo32(T), selL[j]) | perm(hi32(O), hi32(T), selH[j]);
+        const uint32_t sl0 = limb_sel(2 * qq), sl1 = limb_sel(2 * qq + 1);
+        const uint32_t sx0 = spread16(perm(hi32(X), lo32(X), sl0)) & mXOR, sx1 = spread16(perm(hi32(X), lo32(X), sl1)) & mXOR;
+        const uint32_t sy0 = spread16(perm(hi32(Y), lo32(Y), sl0)) & mXOR, sy1 = spread16(perm(hi32(Y), lo32(Y), sl1)) & mXOR;
+        const uint32_t su0 = spread16(perm(hi32(U), lo32(U), sl0)) & mX3, su1 = spread16(perm(hi32(U), lo32(U), sl1)) & mX3;
+        const uint32_t a5r0 = (su0 & mX3) | ((fbit ? 1u : 0u) & mFM);
+        if (lane < NQ) {
+          stage_e<MODE>(S, A0, lane, qrow, tag_of(v[0]), tag_of(v[1]), tag_of(v[2]), tag_of(v[3]), inj);
+          stage_e<MODE>(S, A1, lane, qrow, v[0], v[1], v[2], v[3], inj);
+          stage_e<MODE>(S, A2, lane, qrow, spread16(v[0]), spread16(v[1]), spread16(v[2]), spread16(v[3]), inj);
+          stage_e<MODE>(S, A3, lane, qrow, sx0, 0u, sx1, 0u, inj);
+          stage_e<MODE>(S, A4, lane, qrow, sy0, 0u, sy1, 0u, inj);
+          stage_e<MODE>(S, A5, lane, qrow, a5r0, 0u, su1, 0u, inj);
+          stage_e<MODE>(S, A6, lane, qrow, 0u, 0u, 0u, 0u, inj);
+          stage_e<MODE>(S, A7, lane, qrow, lo32(T) & m78, 0u, 0u, 0u, inj);
+          stage_e<MODE>(S, A8, lane, qrow, hi32(T) & m78, 0u, 0u, 0u, inj);
+          stage_e<MODE>(S, A9, lane, qrow, 0u, 0u, 0u, 0u, inj);
+          stage_e<MODE>(S, FXC, lane, qrow, fxq.x, fxq.y, fxq.z, fxq.w, inj);
+        }
+        if (plane) producer_words(prod, P, pg, c.rounds == 0, 2 * c.rounds - 1, IV);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        {  // limb table: spread limb (lane & 3) of final state word lane >> 2
+          const uint32_t lv = limb(prod[lane >> 2], lane & 3u);
+          S[E_LT + lane] = spread16(lv);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        // ---- stores: the init region (lanes 0-40) and the final region (lanes 41-56)
+        if (MODE & FZ_STORE) {
+          const uint32_t l = lane < NQ ? lane : 0;
+#pragma unroll
+          for (int col = 0; col < NSTAGE; col++) {
+            const uint4 cv = *reinterpret_cast<const uint4*>(S + col * STR_E + 4 * l);
+            uint32_t* base = col < 10 ? adv + (uint64_t)col * total_rows : fixed;
+            region_store(base + row_i, NQ_I, lane, 0, cv);
+            region_store(base + row_f, NQ_F, lane, NQ_I, cv);
+          }
+        }
+        asm volatile("" ::"v"(Pn.w[0]), "v"(Pn.w[1]), "v"(Pn.w[2]), "v"(Pn.w[3]), "v"(Pn.w[4]), "v"(Pn.w[5]));
+        // ---- fast checks
+        uint32_t acc = 0;
+        {
+          const uint4 q0 = ld128(aQ + 4 * A0 * STR_E), q1 = ld128(aQ + 4 * A1 * STR_E), q2 = ld128(aQ + 4 * A2 * STR_E);
+          const uint4 q3 = ld128(aQ + 4 * A3 * STR_E), q4 = ld128(aQ + 4 * A4 * STR_E), q5 = ld128(aQ + 4 * A5 * STR_E);
+          const uint4 q7 = ld128(aQ + 4 * A7 * STR_E), q8 = ld128(aQ + 4 * A8 * STR_E), fx = ld128(aQ + 4 * FXC * STR_E);
+          const uint4 n1 = ld128(aQn + 4 * A1 * STR_E);
+          if (MODE & FZ_LOOKUP) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              const uint32_t de = comp(q1, j);
+              acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(q0, j)) | (spread16(de) ^ comp(q2, j));
+            }
+          }
+          if (MODE & FZ_GATES) {
+            acc |= (fx.x ^ fxq.x) | (fx.y ^ fxq.y) | (fx.z ^ fxq.z) | (fx.w ^ fxq.w);
+            // INW: a_7 = a_1@0 + 2^16 a_1@1, a_8 = a_1@2 + 2^16 a_1@3
+            acc |= ((q7.x ^ (q1.x + (q1.y << 16))) | (q8.x ^ (q1.z + (q1.w << 16)))) & mINW;
+            // FMASK: a_5 in {0, 1}, a_1@k = 65535 a_5
+            const uint32_t fm = (0u - q5.x) & 0xffffu;
+            acc |= ((q5.x >> 1) | (q1.x ^ fm) | (q1.y ^ fm) | (q1.z ^ fm) | (q1.w ^ fm)) & mFM;
+            // CONST: a_1 = k_0 on every row
+            acc |= ((q1.x ^ (fx.x >> 16)) | (q1.y ^ (fx.y >> 16)) | (q1.z ^ (fx.z >> 16)) | (q1.w ^ (fx.w >> 16))) & mCONST;
+            // XOR / XOR3 limbs of the quad (rows 0 and 2)
+            acc |= (((q3.x + q4.x + (q5.x & mX3)) ^ (q2.x + 2 * q2.y)) | ((q3.z + q4.z + (q5.z & mX3)) ^ (q2.z + 2 * q2.w))) & mXOR;
+            // digest: a_7 = a_1@0 + 2^16 a_1@2, a_8 = a_1@4 + 2^16 a_1@6 (the next quad's rows 0, 2)
+            acc |= ((q7.x ^ (q1.x + (q1.z << 16))) | (q8.x ^ (n1.x + (n1.z << 16)))) & mDG;
+          }
+        }
+        if (MODE & FZ_COPIES) {
+#pragma unroll
+          for (int it = 0; it < 2; it++) acc |= ld32(ce[it] & 0xffffu) ^ ld32(ce[it] >> 16);
+        }
+        bool bad = acc != 0;
+        if (MODE & FZ_INJECT)  // the test hook: its instance is checked exactly
+          bad |= inj.row >= c.off && inj.row < c.off + FIXED_ROWS + (uint64_t)ROUND_ROWS * c.rounds;
+        // rare: the instance goes to the redo list (edge_redo_kernel: the first form's edge path,
+        // exact bookkeeping); a list slot per instance, so it cannot overflow
+        if (__builtin_amdgcn_ballot_w64(bad) && lane == 0) {
+          const uint32_t slot = atomicAdd(redo, 1u);
+          redo[1 + slot] = c.inst;
+        }
+      } else {
+        // ---- the zero rows past the last instance: written and checked from registers (a
+        // selector here can only come from the test hook, and its gate is deferred)
+        const uint64_t row0 = used_rows + (uint64_t)PAD_Q * 4 * (t - n);
+        const uint64_t left = row0 < total_rows ? (total_rows - row0) >> 2 : 0;
+        const uint32_t nq = (uint32_t)(left < PAD_Q ? left : PAD_Q);
+        const uint64_t qrow = row0 + 4ull * lane;
+        Quad Q;
+        zero(Q);
+        if (MODE & FZ_INJECT) {
+          if ((inj.row >> 2) == (qrow >> 2)) {
+            const uint32_t j = (uint32_t)inj.row & 3u;
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+#pragma unroll
+              for (int cc = 0; cc < 10; cc++)
+                if ((uint32_t)cc == inj.col && (uint32_t)jj == j) Q.c[cc][jj] ^= inj.mask;
+              if (inj.col == 10 && (uint32_t)jj == j) Q.fx[jj] ^= inj.mask;
+            }
+          }
+        }
+        if (MODE & FZ_STORE) {
+#pragma unroll
+          for (int cc = 0; cc < 11; cc++)
+            tile_store((cc < 10 ? adv + (uint64_t)cc * total_rows : fixed) + row0, nq, lane,
+                       cc < 10 ? make_uint4(Q.c[cc][0], Q.c[cc][1], Q.c[cc][2], Q.c[cc][3])
+                               : make_uint4(Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]));
+        }
+        asm volatile("" ::"v"(Pn.w[0]), "v"(Pn.w[1]), "v"(Pn.w[2]), "v"(Pn.w[3]), "v"(Pn.w[4]), "v"(Pn.w[5]));
+        if (lane < nq) {
+          const uint4 fx = make_uint4(Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]);
+          if (MODE & FZ_LOOKUP)
+            check_lookups(A, make_uint4(Q.c[A0][0], Q.c[A0][1], Q.c[A0][2], Q.c[A0][3]),
+                          make_uint4(Q.c[A1][0], Q.c[A1][1], Q.c[A1][2], Q.c[A1][3]),
+                          make_uint4(Q.c[A2][0], Q.c[A2][1], Q.c[A2][2], Q.c[A2][3]), qrow);
+          if (MODE & FZ_GATES) {
+            check_fixed(A, fx, make_uint4(0, 0, 0, 0), qrow);
+            defer_rows(fx, qrow, defer, defer_cap);
+          }
+        }
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      c = cn;
+      cn = cnn;
+      P = Pn;
+    }
+  }
+  __syncthreads();
+  flush_report(A, rep, tid);
+}
+
+// The edge regions of the instances the edge launch flagged, done again by the first form's
+// edge path (assignment and stores repeated with the same values, every check recorded exactly).
+template <int MODE>
+__global__ void __launch_bounds__(FW * WAVES)
+edge_redo_kernel(const b2f_input* __restrict__ in, const uint64_t* __restrict__ off,
+                 uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
+                 uint32_t* __restrict__ fixed, const uint32_t* __restrict__ redo,
+                 b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
+                 uint64_t* __restrict__ defer, uint32_t defer_cap) {
+  __shared__ __attribute__((aligned(16))) uint32_t L[L_WAVE + WAVES * WAVE_WORDS];
+  const int tid = threadIdx.x;
+  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
+  if (tid < 22) L[L_ACC + tid] = 0;
+  if (tid == 22) *reinterpret_cast<uint64_t*>(L + L_ACC + 20) = ~0ull;
+  if (tid < 16) L[L_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
+  if (tid < 40) L[L_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
+  __syncthreads();
+  const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + L_IV);
+  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + L_SG);
+  uint32_t* S = L + L_WAVE + wv * WAVE_WORDS;
+  if (*status == 0) {
+    const uint32_t cnt = redo[0];
+    for (uint32_t k = blockIdx.x * WAVES + wv; k < cnt; k += gridDim.x * WAVES) {
+      const uint32_t i = __builtin_amdgcn_readfirstlane(redo[1 + k]);
+#pragma unroll 1
+      for (int part = 0; part < 2; part++) {
+        Ctx c;
+        c.inst = i;
+        c.rounds = in[i].rounds;
+        c.off = off[i];
+        c.st = 2 * ((c.off - (uint64_t)FIXED_ROWS * i) / ROUND_ROWS) + i;
+        c.kind = part ? T_FINAL : T_INIT;
+        c.hr = 0;
+        c.nq = part ? FINAL_Q : INIT_Q;
+        c.row0 = part ? c.off + INIT_ROWS + (uint64_t)ROUND_ROWS * c.rounds : c.off;
+        const Ops P = load_ops(c, lane, in, rec, Sg);
+        settle(P);
+        edge_tile<MODE>(S, L + L_ACC, IV, inj, adv, fixed, total_rows, defer, defer_cap, c, P, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+  __syncthreads();
+  EvalAcc A{L + L_ACC};
+  flush_report(A, rep, tid);
+}
+
 // Per-tile descriptors {instance, tile index inside it, rounds, first state index}: thread per
 // instance, 2 rounds + 2 tiles each (init, half-rounds, final).
 __global__ void tile_desc_kernel(const uint64_t* __restrict__ off, const b2f_input* __restrict__ in,
@@ -1518,10 +1983,23 @@ __global__ void deferred_gates_kernel(const uint32_t* __restrict__ adv, const ui
 constexpr uint32_t DEFER_CAP = 4096;
 
 // the half-round launch: the second form (fused_hr_kernel); -DB2F_FUSED_V1 builds the first
+// (-DB2F_EDGE_V1: the second-form half-round launch with the first-form edge launch)
 #ifdef B2F_FUSED_V1
 #define B2F_HR_KERNEL(M) (fused_kernel<M, PART_HR>)
 #else
 #define B2F_HR_KERNEL(M) (fused_hr_kernel<M>)
+#endif
+#if defined(B2F_FUSED_V1) || defined(B2F_EDGE_V1)
+#define B2F_EDGE_FIRST_FORM 1
+#define B2F_EDGE_KERNEL(M) (fused_kernel<M, PART_EDGE>)
+#define B2F_EDGE_ARG desc
+#define B2F_EDGE_REDO(M)
+#else
+#define B2F_EDGE_KERNEL(M) (fused_edge_kernel<M>)
+#define B2F_EDGE_ARG redo
+#define B2F_EDGE_REDO(M)                                                                          \
+  hipLaunchKernelGGL(edge_redo_kernel<M>, dim3(cu_count), dim3(FW * WAVES), 0, s, d_in, d_off,     \
+                     total_rows, rec, d_adv, d_fixed, redo, d_rep, d_status, inj, defer, DEFER_CAP);
 #endif
 
 }  // namespace
@@ -1530,7 +2008,10 @@ namespace b2f {
 
 // Scratch of the fused path: tile descriptors for `tiles` instance tiles and the deferred row
 // list (count + DEFER_CAP rows).
-size_t fused_scratch_bytes(uint64_t tiles) { return tiles * sizeof(TileDesc) + 8 * (1 + DEFER_CAP); }
+// + the edge launch's redo list (count + one slot per instance; tiles >= instances)
+size_t fused_scratch_bytes(uint64_t tiles) {
+  return tiles * sizeof(TileDesc) + 8 * (1 + DEFER_CAP) + 4 * (2 + tiles);
+}
 // Instance tiles of a batch of n instances in at most total_rows rows (an upper bound).
 uint64_t fused_instance_tiles(uint64_t total_rows, uint64_t n) {
   return (total_rows - (uint64_t)FIXED_ROWS * n) / 208 + 2 * n;
@@ -1546,7 +2027,10 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                             unsigned long long* clk, hipStream_t s) {
   TileDesc* desc = reinterpret_cast<TileDesc*>(scratch);
   uint64_t* defer = reinterpret_cast<uint64_t*>(desc + tiles);
+  uint32_t* redo = reinterpret_cast<uint32_t*>(defer + 1 + DEFER_CAP);
   hipError_t e = hipMemsetAsync(defer, 0, 8, s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(redo, 0, 4, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(tile_desc_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d_off, d_in, n, desc, d_status);
   Inject inj;
@@ -1565,26 +2049,31 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
             hipSuccess || nb < 1)
       nb = 2;
     per_cu[0] = nb;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fused_kernel<FZ_FULL, PART_EDGE>, FW * WAVES, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, B2F_EDGE_KERNEL(FZ_FULL), FW * WAVES, 0) !=
             hipSuccess || nb < 1)
       nb = 2;
     per_cu[1] = nb;
   }
-  // the edge tiles: 2 per instance plus the zero rows; no more workgroups than they fill
+  // the edge tiles (first form: 2 per instance, second form: 1) plus the zero rows; no more
+  // workgroups than they fill (the zero-row count here is an upper bound)
+#ifdef B2F_EDGE_FIRST_FORM
   const uint64_t edge_tiles = 2ull * n + ((total_rows / 4) + PAD_Q - 1) / PAD_Q;
+#else
+  const uint64_t edge_tiles = (uint64_t)n + ((total_rows / 4) + PAD_Q - 1) / PAD_Q;
+#endif
   const uint64_t edge_wgs = (edge_tiles + WAVES - 1) / WAVES;
   const uint32_t grid = (uint32_t)(cu_count * per_cu[0]);
   const uint32_t grid_e = (uint32_t)(edge_wgs < (uint64_t)cu_count * per_cu[1] ? edge_wgs : (uint64_t)cu_count * per_cu[1]);
-  const TileDesc* desc_e = desc;  // the kernels offset the edge list themselves (n_hr is on the device)
   switch (mode) {
 #define B2F_FUSED(M)                                                                               \
   case M:                                                                                          \
     hipLaunchKernelGGL(B2F_HR_KERNEL(M), dim3(grid), dim3(FW * WAVES), 0, s, d_in, n,              \
                        d_off, total_rows, rec, d_adv, d_fixed, desc, d_rep, d_status, inj, defer,  \
                        DEFER_CAP, clk);                                                            \
-    hipLaunchKernelGGL((fused_kernel<M, PART_EDGE>), dim3(grid_e), dim3(FW * WAVES), 0, s, d_in, n, \
-                       d_off, total_rows, rec, d_adv, d_fixed, desc_e, d_rep, d_status, inj, defer, \
-                       DEFER_CAP, clk);                                                            \
+    hipLaunchKernelGGL(B2F_EDGE_KERNEL(M), dim3(grid_e), dim3(FW * WAVES), 0, s, d_in, n,           \
+                       d_off, total_rows, rec, d_adv, d_fixed, B2F_EDGE_ARG, d_rep, d_status, inj,  \
+                       defer, DEFER_CAP, clk);                                                     \
+    B2F_EDGE_REDO(M)                                                                               \
     break;
 #ifdef B2F_DIAG
     B2F_FUSED(0) B2F_FUSED(2) B2F_FUSED(3) B2F_FUSED(10) B2F_FUSED(18) B2F_FUSED(8) B2F_FUSED(16)
