@@ -885,6 +885,18 @@ fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __res
   flush_report(A, rep, tid);
 }
 
+// The first tile of wave wv of workgroup b in a persistent grid of `grid` workgroups that takes
+// WAVES * grid consecutive tiles per round. XCD-aware: workgroups are dispatched to the 8 XCDs
+// round-robin (b % 8), so XCD x takes the x-th eighth of every round as one contiguous run --
+// neighbouring tiles (which share boundary cache lines, the previous half-round's state cells and
+// the instance's message rows) sit behind the same L2.
+__device__ __forceinline__ uint64_t first_tile(uint32_t b, uint32_t wv, uint32_t grid) {
+#ifndef B2F_NO_XCD_DEAL
+  if (grid % 8 == 0) return ((uint64_t)(b % 8) * (grid / 8) + b / 8) * WAVES + wv;
+#endif
+  return (uint64_t)b * WAVES + wv;
+}
+
 // ============================================================================================
 // The half-round launch (PART_HR), second form: a lane's quad position p inside its G never
 // changes from tile to tile, so everything that depends on p alone -- which bytes of which
@@ -1201,6 +1213,68 @@ __device__ __forceinline__ Lane make_lane(uint32_t lane, uint32_t Sb) {
 
 }  // namespace hr2
 
+// The fast checks of a staged half-round tile (see the second form's comment): lookups, the fixed
+// column, every canonical gate block, the 256 state-word / in-tile copies (sources: the staging
+// and the limb table), the lane's message copy against `msrc` (the message limb its producer or
+// the trace holds, read where it is used). Returns the OR of every identity's lhs ^ rhs: 0 iff all hold (given the
+// ranges the other checks of the pass establish).
+template <int MODE, class MsgSrc>
+__device__ __forceinline__ uint32_t hr_fast_checks(const hr2::Lane& K, uint32_t hr, const MsgSrc& msrc) {
+  using namespace hr2;
+  uint32_t acc = 0;
+  if (MODE & (FZ_LOOKUP | FZ_GATES)) {
+    const uint4 q0 = ld128(K.aQ + 4 * A0 * STR), q1 = ld128(K.aQ + 4 * A1 * STR), q2 = ld128(K.aQ + 4 * A2 * STR);
+    const uint4 fx = ld128(K.aQ + 4 * FXC * STR);
+    if (MODE & FZ_LOOKUP) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t de = comp(q1, j);
+        acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(q0, j)) | (spread16(de) ^ comp(q2, j));
+      }
+    }
+    if (MODE & FZ_GATES) acc |= (fx.x ^ K.fx0) | fx.y | fx.z | fx.w;
+  }
+  if (MODE & FZ_GATES) {
+    {  // XOR / XOR24 / XOR63 limb item
+      const uint32_t gb = K.gb;
+      const uint32_t x3 = ld32(gb + 4 * A3 * STR), x4 = ld32(gb + 4 * A4 * STR);
+      const uint32_t s0 = ld32(gb + 4 * A2 * STR), s1v = ld32(gb + 4 * (A2 * STR + 1)), s2v = ld32(gb + 4 * (A2 * STR + 2));
+      const uint32_t z6 = ld32(gb + 4 * A6 * STR), t0 = ld32(gb), t1 = ld32(gb + 4);
+      const uint32_t w7 = ld32(gb + 4 * A7 * STR), w8 = ld32(gb + 4 * A8 * STR);
+      const uint32_t E = ld32(K.ge), E2 = ld32(K.ge + 4 * (A2 - A1) * STR);
+      const uint32_t F = ld32(K.gf), H = ld32(K.gf + 4 * (A2 - A1) * STR);
+      const uint32_t R = s0 + perm(0u, s1v, K.gsel) + ((z6 << 30) & K.gm63) + 2 * sel32(K.gm24, s2v, s1v);
+      acc |= (x3 + x4) ^ R;
+      acc |= (t0 | (t1 & K.gm24) | (z6 & K.gm63)) & K.gnl;
+      const uint32_t G = sel32(K.gm24, E2, E);
+      acc |= (((E + (F << K.gsF)) ^ w7) | ((G + (H << K.gsH)) ^ w8)) & K.grs;
+    }
+    {  // ADD block (lanes 16-63 repeat lanes 0-15)
+      const uint4 s = ld128(K.ar + 4 * A1 * STR), x = ld128(K.ar + 4 * A3 * STR);
+      const uint4 y = ld128(K.ar + 4 * A4 * STR), z = ld128(K.ar + 4 * A5 * STR);
+      const uint32_t a9 = ld32(K.ar + 4 * A9 * STR);
+      int32_t cy = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        cy += (int32_t)(comp(x, k) + comp(y, k) + (comp(z, k) & K.m3) - comp(s, k));
+        acc |= (uint32_t)cy & 0xffffu;
+        cy >>= 16;
+      }
+      acc |= (uint32_t)cy ^ a9;
+    }
+  }
+  if (MODE & FZ_COPIES) {
+    const bool odd = hr & 1u;
+#pragma unroll
+    for (int it = 0; it < HR_CHECKS / FW; it++) {
+      const uint32_t e = odd ? K.ce[1][it] : K.ce[0][it];
+      acc |= ld32(e & 0xffffu) ^ ld32(e >> 16);
+    }
+    acc |= ld32(K.cm & 0xffffu) ^ msrc();
+  }
+  return acc;
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES, B2F_FUSED_WAVES)
 fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
@@ -1239,7 +1313,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
     const uint64_t used_rows = off[n];
     const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
     const uint64_t W = (uint64_t)gridDim.x * WAVES;
-    uint64_t t = (uint64_t)blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(wv);
+    uint64_t t = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
     auto raw_desc = [&](uint64_t tt) -> uint4 {
       const uint64_t ti = tt < n_hr ? tt : 0;
       const uint4 v = desc[ti].v;
@@ -1381,7 +1455,8 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       asm volatile("" ::"v"(Pn));
 #endif
       tick(7);
-      // ---- 6. fast checks: acc |= (every identity's lhs ^ rhs)
+      // ---- 6. fast checks: acc |= (every identity's lhs ^ rhs) -- hr_fast_checks, kept inline
+      // here: called as a function it moved the register allocation (hot-loop spill reloads)
       uint32_t acc = 0;
       if (MODE & (FZ_LOOKUP | FZ_GATES)) {
         const uint4 q0 = ld128(K.aQ + 4 * A0 * STR), q1 = ld128(K.aQ + 4 * A1 * STR), q2 = ld128(K.aQ + 4 * A2 * STR);
@@ -1608,6 +1683,102 @@ __device__ __forceinline__ void stage_e(uint32_t* S, int col, uint32_t lane, uin
   *reinterpret_cast<uint4*>(S + col * edge2::STR_E + 4 * lane) = make_uint4(v0, v1, v2, v3);
 }
 
+
+// Per-lane constants of an edge tile (lane = quad of the init region 0-40 / final region 41-56;
+// lanes >= 57 check a repeat of quads 0-6).
+struct ELane {
+  uint32_t selL[4], selH[4];
+  uint32_t kind, qq, a;
+  uint32_t mINW, mFM, mCONST, mX3, mXOR, m78, mDG;
+  uint4 fxq;          // the keygen fixed cells of the quad
+  uint32_t aQ, aQn;   // the quad's and the next quad's staged rows (column a_0)
+  uint32_t ce[2];     // copy checks (dst | src << 16)
+};
+__device__ __forceinline__ ELane make_elane(uint32_t lane, uint32_t Sb, const uint64_t* IV) {
+  using namespace edge2;
+  ELane E;
+  const uint32_t lq = lane < NQ ? lane : lane - NQ;
+  const EdgeProg& G = c_eprogs.e[lq];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    E.selL[j] = G.selL[j];
+    E.selH[j] = G.selH[j];
+  }
+  E.kind = G.kind;
+  E.qq = G.qq;
+  E.a = G.a;
+  const uint32_t kind = G.kind, qq = G.qq;
+  E.mINW = kind == E_INW ? ~0u : 0u;
+  E.mFM = kind == E_FMASK ? ~0u : 0u;
+  E.mCONST = kind == E_CONST ? ~0u : 0u;
+  E.mX3 = kind == E_XOR3 ? ~0u : 0u;
+  E.mXOR = (kind & (E_XOR | E_XOR3)) ? ~0u : 0u;
+  E.m78 = E.mINW | (qq == 0 ? E.mX3 : 0u);
+  E.mDG = qq == 0 ? E.mX3 : 0u;
+  uint4 fxq = make_uint4(0, 0, 0, 0);
+  if (kind == E_INW) fxq.x = 1u << S_ABCD;
+  if (kind == E_FMASK) fxq.x = 1u << S_FMASK;
+  if (kind == E_XOR && qq == 0) fxq.x = 1u << S_XOR;
+  if (kind == E_XOR3 && qq == 0) fxq.x = (1u << S_XOR3) | (1u << S_DIGEST);
+  if (kind == E_CONST) {
+    const uint64_t w = IV[G.a];
+    fxq = make_uint4((1u << S_CONST) | ((uint32_t)(w & 0xffffu) << 16), (1u << S_CONST) | ((uint32_t)((w >> 16) & 0xffffu) << 16),
+                     (1u << S_CONST) | ((uint32_t)((w >> 32) & 0xffffu) << 16), (1u << S_CONST) | ((uint32_t)(w >> 48) << 16));
+  }
+  E.fxq = fxq;
+  E.aQ = Sb + 16 * lq;
+  E.aQn = Sb + 16 * (lq + 1);
+#pragma unroll
+  for (int it = 0; it < 2; it++) {
+    const uint32_t e = c_echecks.e[it * FW + lane];
+    const uint32_t dst = Sb + 4 * ((A3 + ((e >> 8) & 3u)) * STR_E + (e & 255u));
+    const uint32_t src = (e >> 10) & 1u ? Sb + 4 * (E_LT + ((e >> 11) & 63u)) : Sb + 4 * (A2 * STR_E + ((e >> 11) & 255u));
+    E.ce[it] = dst | (src << 16);
+  }
+  return E;
+}
+
+// The fast checks of a staged edge tile: lookups, the fixed column, the INW / FMASK / CONST /
+// XOR / XOR3 / digest identities of each lane's quad, the 120 copies (staging and limb table).
+template <int MODE>
+__device__ __forceinline__ uint32_t edge_fast_checks(const ELane& E) {
+  using namespace hr2;
+  using namespace edge2;
+  uint32_t acc = 0;
+  {
+    const uint4 q0 = ld128(E.aQ + 4 * A0 * STR_E), q1 = ld128(E.aQ + 4 * A1 * STR_E), q2 = ld128(E.aQ + 4 * A2 * STR_E);
+    const uint4 q3 = ld128(E.aQ + 4 * A3 * STR_E), q4 = ld128(E.aQ + 4 * A4 * STR_E), q5 = ld128(E.aQ + 4 * A5 * STR_E);
+    const uint4 q7 = ld128(E.aQ + 4 * A7 * STR_E), q8 = ld128(E.aQ + 4 * A8 * STR_E), fx = ld128(E.aQ + 4 * FXC * STR_E);
+    const uint4 n1 = ld128(E.aQn + 4 * A1 * STR_E);
+    if (MODE & FZ_LOOKUP) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t de = comp(q1, j);
+        acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(q0, j)) | (spread16(de) ^ comp(q2, j));
+      }
+    }
+    if (MODE & FZ_GATES) {
+      acc |= (fx.x ^ E.fxq.x) | (fx.y ^ E.fxq.y) | (fx.z ^ E.fxq.z) | (fx.w ^ E.fxq.w);
+      // INW: a_7 = a_1@0 + 2^16 a_1@1, a_8 = a_1@2 + 2^16 a_1@3
+      acc |= ((q7.x ^ (q1.x + (q1.y << 16))) | (q8.x ^ (q1.z + (q1.w << 16)))) & E.mINW;
+      // FMASK: a_5 in {0, 1}, a_1@k = 65535 a_5
+      const uint32_t fm = (0u - q5.x) & 0xffffu;
+      acc |= ((q5.x >> 1) | (q1.x ^ fm) | (q1.y ^ fm) | (q1.z ^ fm) | (q1.w ^ fm)) & E.mFM;
+      // CONST: a_1 = k_0 on every row
+      acc |= ((q1.x ^ (fx.x >> 16)) | (q1.y ^ (fx.y >> 16)) | (q1.z ^ (fx.z >> 16)) | (q1.w ^ (fx.w >> 16))) & E.mCONST;
+      // XOR / XOR3 limbs of the quad (rows 0 and 2)
+      acc |= (((q3.x + q4.x + (q5.x & E.mX3)) ^ (q2.x + 2 * q2.y)) | ((q3.z + q4.z + (q5.z & E.mX3)) ^ (q2.z + 2 * q2.w))) & E.mXOR;
+      // digest: a_7 = a_1@0 + 2^16 a_1@2, a_8 = a_1@4 + 2^16 a_1@6 (the next quad's rows 0, 2)
+      acc |= ((q7.x ^ (q1.x + (q1.z << 16))) | (q8.x ^ (n1.x + (n1.z << 16)))) & E.mDG;
+    }
+  }
+  if (MODE & FZ_COPIES) {
+#pragma unroll
+    for (int it = 0; it < 2; it++) acc |= ld32(E.ce[it] & 0xffffu) ^ ld32(E.ce[it] >> 16);
+  }
+  return acc;
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES, 3)
 fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
@@ -1634,38 +1805,10 @@ fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* 
   uint64_t* prod = reinterpret_cast<uint64_t*>(S + E_PROD);
 
   // per-lane constants
-  const uint32_t lq = lane < NQ ? lane : lane - NQ;  // the quad a lane checks (>= 57: a repeat)
-  const EdgeProg& G = c_eprogs.e[lq];
-  uint32_t selL[4], selH[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    selL[j] = G.selL[j];
-    selH[j] = G.selH[j];
-  }
-  const uint32_t kind = G.kind, qq = G.qq, wa = G.a;
-  const uint32_t mINW = kind == E_INW ? ~0u : 0u, mFM = kind == E_FMASK ? ~0u : 0u;
-  const uint32_t mCONST = kind == E_CONST ? ~0u : 0u, mX3 = kind == E_XOR3 ? ~0u : 0u;
-  const uint32_t mXOR = (kind & (E_XOR | E_XOR3)) ? ~0u : 0u;
-  const uint32_t m78 = mINW | (qq == 0 ? mX3 : 0u), mDG = qq == 0 ? mX3 : 0u;
-  uint4 fxq = make_uint4(0, 0, 0, 0);  // the keygen fixed cells of the lane's quad
-  if (kind == E_INW) fxq.x = 1u << S_ABCD;
-  if (kind == E_FMASK) fxq.x = 1u << S_FMASK;
-  if (kind == E_XOR && qq == 0) fxq.x = 1u << S_XOR;
-  if (kind == E_XOR3 && qq == 0) fxq.x = (1u << S_XOR3) | (1u << S_DIGEST);
-  if (kind == E_CONST) {
-    const uint64_t w = IV[wa];
-    fxq = make_uint4((1u << S_CONST) | ((uint32_t)(w & 0xffffu) << 16), (1u << S_CONST) | ((uint32_t)((w >> 16) & 0xffffu) << 16),
-                     (1u << S_CONST) | ((uint32_t)((w >> 32) & 0xffffu) << 16), (1u << S_CONST) | ((uint32_t)(w >> 48) << 16));
-  }
-  const uint32_t aQ = Sb + 16 * lq, aQn = Sb + 16 * (lq + 1);
-  uint32_t ce[2];
-#pragma unroll
-  for (int it = 0; it < 2; it++) {
-    const uint32_t e = c_echecks.e[it * FW + lane];
-    const uint32_t dst = Sb + 4 * ((A3 + ((e >> 8) & 3u)) * STR_E + (e & 255u));
-    const uint32_t src = (e >> 10) & 1u ? Sb + 4 * (E_LT + ((e >> 11) & 63u)) : Sb + 4 * (A2 * STR_E + ((e >> 11) & 255u));
-    ce[it] = dst | (src << 16);
-  }
+  const ELane E = make_elane(lane, Sb, IV);
+  const uint32_t kind = E.kind, qq = E.qq, wa = E.a;
+  const uint32_t mFM = E.mFM, mX3 = E.mX3, mXOR = E.mXOR, m78 = E.m78;
+  const uint4 fxq = E.fxq;
   const bool plane = lane >= NQ && lane < NQ + 4;
   const uint32_t pg = lane - NQ;
 
@@ -1674,7 +1817,7 @@ fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* 
     const uint64_t n_pad = ((total_rows - used_rows) / 4 + PAD_Q - 1) / PAD_Q;
     const uint64_t t_all = (uint64_t)n + n_pad;
     const uint64_t W = (uint64_t)gridDim.x * WAVES;
-    uint64_t t = (uint64_t)blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(wv);
+    uint64_t t = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
     auto ectx = [&](uint64_t tt) {
       ECtx c;
       const uint32_t i = tt < n ? (uint32_t)tt : 0u;
@@ -1759,7 +1902,7 @@ fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* 
         }
         uint32_t v[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) v[j] = perm(lo32(O), lo32(T), selL[j]) | perm(hi32(O), hi32(T), selH[j]);
+        for (int j = 0; j < 4; j++) v[j] = perm(lo32(O), lo32(T), E.selL[j]) | perm(hi32(O), hi32(T), E.selH[j]);
         const uint32_t sl0 = limb_sel(2 * qq), sl1 = limb_sel(2 * qq + 1);
         const uint32_t sx0 = spread16(perm(hi32(X), lo32(X), sl0)) & mXOR, sx1 = spread16(perm(hi32(X), lo32(X), sl1)) & mXOR;
         const uint32_t sy0 = spread16(perm(hi32(Y), lo32(Y), sl0)) & mXOR, sy1 = spread16(perm(hi32(Y), lo32(Y), sl1)) & mXOR;
@@ -1800,38 +1943,7 @@ fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* 
         }
         asm volatile("" ::"v"(Pn.w[0]), "v"(Pn.w[1]), "v"(Pn.w[2]), "v"(Pn.w[3]), "v"(Pn.w[4]), "v"(Pn.w[5]));
         // ---- fast checks
-        uint32_t acc = 0;
-        {
-          const uint4 q0 = ld128(aQ + 4 * A0 * STR_E), q1 = ld128(aQ + 4 * A1 * STR_E), q2 = ld128(aQ + 4 * A2 * STR_E);
-          const uint4 q3 = ld128(aQ + 4 * A3 * STR_E), q4 = ld128(aQ + 4 * A4 * STR_E), q5 = ld128(aQ + 4 * A5 * STR_E);
-          const uint4 q7 = ld128(aQ + 4 * A7 * STR_E), q8 = ld128(aQ + 4 * A8 * STR_E), fx = ld128(aQ + 4 * FXC * STR_E);
-          const uint4 n1 = ld128(aQn + 4 * A1 * STR_E);
-          if (MODE & FZ_LOOKUP) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-              const uint32_t de = comp(q1, j);
-              acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(q0, j)) | (spread16(de) ^ comp(q2, j));
-            }
-          }
-          if (MODE & FZ_GATES) {
-            acc |= (fx.x ^ fxq.x) | (fx.y ^ fxq.y) | (fx.z ^ fxq.z) | (fx.w ^ fxq.w);
-            // INW: a_7 = a_1@0 + 2^16 a_1@1, a_8 = a_1@2 + 2^16 a_1@3
-            acc |= ((q7.x ^ (q1.x + (q1.y << 16))) | (q8.x ^ (q1.z + (q1.w << 16)))) & mINW;
-            // FMASK: a_5 in {0, 1}, a_1@k = 65535 a_5
-            const uint32_t fm = (0u - q5.x) & 0xffffu;
-            acc |= ((q5.x >> 1) | (q1.x ^ fm) | (q1.y ^ fm) | (q1.z ^ fm) | (q1.w ^ fm)) & mFM;
-            // CONST: a_1 = k_0 on every row
-            acc |= ((q1.x ^ (fx.x >> 16)) | (q1.y ^ (fx.y >> 16)) | (q1.z ^ (fx.z >> 16)) | (q1.w ^ (fx.w >> 16))) & mCONST;
-            // XOR / XOR3 limbs of the quad (rows 0 and 2)
-            acc |= (((q3.x + q4.x + (q5.x & mX3)) ^ (q2.x + 2 * q2.y)) | ((q3.z + q4.z + (q5.z & mX3)) ^ (q2.z + 2 * q2.w))) & mXOR;
-            // digest: a_7 = a_1@0 + 2^16 a_1@2, a_8 = a_1@4 + 2^16 a_1@6 (the next quad's rows 0, 2)
-            acc |= ((q7.x ^ (q1.x + (q1.z << 16))) | (q8.x ^ (n1.x + (n1.z << 16)))) & mDG;
-          }
-        }
-        if (MODE & FZ_COPIES) {
-#pragma unroll
-          for (int it = 0; it < 2; it++) acc |= ld32(ce[it] & 0xffffu) ^ ld32(ce[it] >> 16);
-        }
+        const uint32_t acc = edge_fast_checks<MODE>(E);
         bool bad = acc != 0;
         if (MODE & FZ_INJECT)  // the test hook: its instance is checked exactly
           bad |= inj.row >= c.off && inj.row < c.off + FIXED_ROWS + (uint64_t)ROUND_ROWS * c.rounds;
@@ -1941,6 +2053,195 @@ edge_redo_kernel(const b2f_input* __restrict__ in, const uint64_t* __restrict__ 
   flush_report(A, rep, tid);
 }
 
+// ============================================================================================
+// The eval's fast clean-check pass (b2f_eval_dev): the same wave tiles, lane programs and fast
+// checks as the fused path, on a GIVEN trace -- the tile's cells are loaded instead of assigned,
+// and every copy source is the source cell in the trace (the state words' canonical cells at the
+// half-round start, the message words' INW cells, the final state's canonical cells), gathered
+// into the limb table. A pass that finds nothing proves the trace clean: the report
+// report_init_kernel wrote is the verdict. Anything it flags (a failure, or a range a check
+// assumes) sets `dirty`, and the exact eval kernel then evaluates the whole trace and writes the
+// report (MockProver's counters and first failing row).
+
+// half-round tile descriptors from the row map alone (the eval has no input records)
+__global__ void eval_desc_kernel(const uint64_t* __restrict__ off, uint32_t n, TileDesc* __restrict__ desc,
+                                 const int* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || *status) return;
+  const uint64_t o = off[i];
+  const uint32_t rounds = (uint32_t)((off[i + 1] - o - FIXED_ROWS) / ROUND_ROWS);
+  const uint64_t st = 2 * ((o - (uint64_t)FIXED_ROWS * i) / ROUND_ROWS) + i;
+  for (uint32_t j = 1; j <= 2 * rounds; j++) desc[st - i + j - 1].v = make_uint4(i, j, rounds, (uint32_t)st);
+}
+
+// The loads of one eval tile (see eval_hr_kernel): the tile's 11 cells of the lane's quad, the
+// lane's limb-table entry (dense, spread) and its message-copy source. Named members, no array:
+// a register array carried across the tile loop was kept in scratch by the compiler.
+struct EvCells {
+  uint4 c0, c1, c2, c3, c4, c5, c6, c7, c8, c9, c10;
+  uint32_t d, sp, mc;
+};
+__device__ __forceinline__ EvCells ev_load(const hr2::HCtx& c, uint32_t lane, uint32_t lq, uint32_t mg, uint32_t mwh,
+                                           uint32_t mk, const uint32_t* __restrict__ adv,
+                                           const uint32_t* __restrict__ fixed, uint64_t total_rows, const uint8_t* Sg) {
+  EvCells v;
+  const uint32_t* p = adv + c.row0 + 4 * lq;
+  v.c0 = *reinterpret_cast<const uint4*>(p);
+  v.c1 = *reinterpret_cast<const uint4*>(p + total_rows);
+  v.c2 = *reinterpret_cast<const uint4*>(p + 2 * total_rows);
+  v.c3 = *reinterpret_cast<const uint4*>(p + 3 * total_rows);
+  v.c4 = *reinterpret_cast<const uint4*>(p + 4 * total_rows);
+  v.c5 = *reinterpret_cast<const uint4*>(p + 5 * total_rows);
+  v.c6 = *reinterpret_cast<const uint4*>(p + 6 * total_rows);
+  v.c7 = *reinterpret_cast<const uint4*>(p + 7 * total_rows);
+  v.c8 = *reinterpret_cast<const uint4*>(p + 8 * total_rows);
+  v.c9 = *reinterpret_cast<const uint4*>(p + 9 * total_rows);
+  v.c10 = *reinterpret_cast<const uint4*>(fixed + c.row0 + 4 * lq);
+  const Canon cs = canon_state(lane >> 2, c.hr);
+  const uint64_t r = c.off + cs.row(lane & 3u);
+  v.d = adv[(uint64_t)cs.dcol * total_rows + r];
+  v.sp = adv[(uint64_t)cs.scol * total_rows + r];
+  const uint32_t j = Sg[16 * ((c.hr >> 1) % 10) + 2 * (mg + 4 * (c.hr & 1u)) + mwh];
+  v.mc = adv[(uint64_t)A1 * total_rows + c.off + 32 + 4 * j + mk];
+  return v;
+}
+
+#ifndef B2F_EVAL_WAVES_HR
+#define B2F_EVAL_WAVES_HR 3  // waves per SIMD of the eval fast pass (the prefetched tile's registers)
+#endif
+template <int MODE>
+__global__ void __launch_bounds__(FW * WAVES, B2F_EVAL_WAVES_HR)
+eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fixed, uint32_t n,
+               const uint64_t* __restrict__ off, uint64_t total_rows, const TileDesc* __restrict__ desc,
+               uint32_t* __restrict__ dirty, const int* __restrict__ status) {
+  using namespace hr2;
+  __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS];
+  const int tid = threadIdx.x;
+  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
+  if (tid < 40) L[H_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
+  __syncthreads();
+  if (*status) return;  // a rejected row map: the eval kernel reports it
+  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + H_SG);
+  uint32_t* S = L + H_WAVE + wv * HW_WORDS;
+  const Lane K = make_lane(lane, lds_byte(S));
+  const bool qlane = lane < HR_Q;
+  const uint32_t lq = qlane ? lane : 0;
+  const uint32_t m32 = lane & 31u, mg = m32 >> 3, mwh = (m32 >> 2) & 1u, mk = m32 & 3u;
+  const uint64_t used_rows = off[n];
+  const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
+  const uint64_t W = (uint64_t)gridDim.x * WAVES;
+  uint64_t t = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
+  auto raw_desc = [&](uint64_t tt) -> uint4 { return desc[tt].v; };
+  // per tile: its cells (lane = quad), its limb-table entry (the canonical dense / spread cell of
+  // state word lane / 4, limb lane % 4, as the half-round starts) and its message-copy source
+  // (message word SIGMA[..] limb, a_1 of its INW block), loaded one tile ahead
+#ifndef B2F_EVAL_NOPF
+  HCtx c = hctx(raw_desc(t < n_hr ? t : 0));
+  EvCells cur = ev_load(c, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg);
+  for (; t < n_hr; t += W) {
+    const HCtx cn = hctx(raw_desc(t + W < n_hr ? t + W : 0));
+    const EvCells nxt = ev_load(cn, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg);  // in flight
+#else
+  for (; t < n_hr; t += W) {
+    const HCtx c = hctx(raw_desc(t));
+    const EvCells cur = ev_load(c, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg);
+#endif
+    if (qlane) {
+      uint4* q = reinterpret_cast<uint4*>(S + 4 * lane);
+      q[0 * STR / 4] = cur.c0;
+      q[1 * STR / 4] = cur.c1;
+      q[2 * STR / 4] = cur.c2;
+      q[3 * STR / 4] = cur.c3;
+      q[4 * STR / 4] = cur.c4;
+      q[5 * STR / 4] = cur.c5;
+      q[6 * STR / 4] = cur.c6;
+      q[7 * STR / 4] = cur.c7;
+      q[8 * STR / 4] = cur.c8;
+      q[9 * STR / 4] = cur.c9;
+      q[10 * STR / 4] = cur.c10;
+    }
+    S[H_LT + lane] = cur.d;
+    S[H_LT + 64 + lane] = cur.sp;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t mc = cur.mc;
+    const uint32_t acc = hr_fast_checks<MODE>(K, c.hr, [&] { return mc; });
+    if (__builtin_amdgcn_ballot_w64(acc != 0) && lane == 0) *dirty = 1u;
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#ifndef B2F_EVAL_NOPF
+    c = cn;
+    cur = nxt;
+#endif
+  }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(FW * WAVES, 3)
+eval_edge_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fixed, uint32_t n,
+                 const uint64_t* __restrict__ off, uint64_t total_rows, uint32_t* __restrict__ dirty,
+                 const int* __restrict__ status) {
+  using namespace hr2;
+  using namespace edge2;
+  __shared__ __attribute__((aligned(16))) uint32_t L[E_WORDS];
+  const int tid = threadIdx.x;
+  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
+  if (tid < 16) L[E_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
+  __syncthreads();
+  if (*status) return;
+  const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + E_IV);
+  uint32_t* S = L + E_WAVE + wv * EW_WORDS;
+  const ELane E = make_elane(lane, lds_byte(S), IV);
+  const uint64_t used_rows = off[n];
+  const uint64_t n_pad = ((total_rows - used_rows) / 4 + PAD_Q - 1) / PAD_Q;
+  const uint64_t t_all = (uint64_t)n + n_pad;
+  const uint64_t W = (uint64_t)gridDim.x * WAVES;
+  bool bad = false;
+  for (uint64_t t = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x); t < t_all; t += W) {
+    if (t < n) {
+      const uint32_t i = (uint32_t)t;
+      const uint64_t o = off[i];
+      const uint32_t rounds = (uint32_t)((off[i + 1] - o - FIXED_ROWS) / ROUND_ROWS);
+      const uint64_t row_f = o + INIT_ROWS + (uint64_t)ROUND_ROWS * rounds;
+      const uint64_t row = lane < NQ_I ? o + 4 * lane : lane < NQ ? row_f + 4 * (lane - NQ_I) : o;
+      uint4 cv[NSTAGE];
+#pragma unroll
+      for (int col = 0; col < NSTAGE; col++)
+        cv[col] = *reinterpret_cast<const uint4*>((col < 10 ? adv + (uint64_t)col * total_rows : fixed) + row);
+      // limb table: the spread canonical cell of final state word lane / 4, limb lane % 4
+      const Canon cs = canon_state(lane >> 2, 2 * rounds);
+      const uint32_t sp = adv[(uint64_t)cs.scol * total_rows + o + cs.row(lane & 3u)];
+      if (lane < NQ) {
+#pragma unroll
+        for (int col = 0; col < NSTAGE; col++) *reinterpret_cast<uint4*>(S + col * STR_E + 4 * lane) = cv[col];
+      }
+      S[E_LT + lane] = sp;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      bad |= edge_fast_checks<MODE>(E) != 0;
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+    } else {  // the zero rows: valid lookups, no selector
+      const uint64_t row0 = used_rows + (uint64_t)PAD_Q * 4 * (t - n);
+      const uint64_t left = row0 < total_rows ? (total_rows - row0) >> 2 : 0;
+      const uint32_t nq = (uint32_t)(left < PAD_Q ? left : PAD_Q);
+      if (lane < nq) {
+        const uint64_t r = row0 + 4ull * lane;
+        const uint4 q0 = *reinterpret_cast<const uint4*>(adv + r), q1 = *reinterpret_cast<const uint4*>(adv + total_rows + r);
+        const uint4 q2 = *reinterpret_cast<const uint4*>(adv + 2 * total_rows + r), fx = *reinterpret_cast<const uint4*>(fixed + r);
+        uint32_t acc = fx.x | fx.y | fx.z | fx.w;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t de = comp(q1, j);
+          acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(q0, j)) | (spread16(de) ^ comp(q2, j));
+        }
+        bad |= acc != 0;
+      }
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(bad) && lane == 0) *dirty = 1u;
+}
+
 // Per-tile descriptors {instance, tile index inside it, rounds, first state index}: thread per
 // instance, 2 rounds + 2 tiles each (init, half-rounds, final).
 __global__ void tile_desc_kernel(const uint64_t* __restrict__ off, const b2f_input* __restrict__ in,
@@ -2010,7 +2311,49 @@ namespace b2f {
 // list (count + DEFER_CAP rows).
 // + the edge launch's redo list (count + one slot per instance; tiles >= instances)
 size_t fused_scratch_bytes(uint64_t tiles) {
-  return tiles * sizeof(TileDesc) + 8 * (1 + DEFER_CAP) + 4 * (2 + tiles);
+  return tiles * sizeof(TileDesc) + 8 * (1 + DEFER_CAP) + 4 * (2 + tiles) + 8;  // + the eval's dirty word
+}
+
+// The eval's fast clean-check pass (see eval_hr_kernel) into the fused scratch; returns the
+// device word the exact eval kernel is gated on (0: clean, the report stands).
+hipError_t launch_eval_fast(const uint32_t* d_adv, const uint32_t* d_fixed, const uint64_t* d_off, uint32_t n,
+                            uint64_t total_rows, void* scratch, uint64_t tiles, const int* d_status,
+                            int cu_count, hipStream_t s, const uint32_t** gate, int mode) {
+#ifndef B2F_DIAG
+  mode = FZ_FULL;  // the product library runs the full pass only
+#endif
+  TileDesc* desc = reinterpret_cast<TileDesc*>(scratch);
+  uint32_t* dirty = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + fused_scratch_bytes(tiles) - 8);
+  hipError_t e = hipMemsetAsync(dirty, 0, 4, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(eval_desc_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d_off, n, desc, d_status);
+  static int per_cu[2] = {0, 0};
+  if (!per_cu[0]) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, eval_hr_kernel<FZ_FULL>, FW * WAVES, 0) != hipSuccess || nb < 1) nb = 2;
+    per_cu[0] = nb;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, eval_edge_kernel<FZ_FULL>, FW * WAVES, 0) != hipSuccess || nb < 1) nb = 2;
+    per_cu[1] = nb;
+  }
+  const uint64_t edge_tiles = (uint64_t)n + ((total_rows / 4) + PAD_Q - 1) / PAD_Q;
+  const uint64_t edge_wgs = (edge_tiles + WAVES - 1) / WAVES;
+  const uint32_t grid_e = (uint32_t)(edge_wgs < (uint64_t)cu_count * per_cu[1] ? edge_wgs : (uint64_t)cu_count * per_cu[1]);
+  switch (mode) {
+#define B2F_EVFAST(M)                                                                              \
+  case M:                                                                                          \
+    hipLaunchKernelGGL(eval_hr_kernel<M>, dim3(cu_count * per_cu[0]), dim3(FW * WAVES), 0, s, d_adv, d_fixed, n, \
+                       d_off, total_rows, desc, dirty, d_status);                                  \
+    hipLaunchKernelGGL(eval_edge_kernel<M>, dim3(grid_e), dim3(FW * WAVES), 0, s, d_adv, d_fixed, n, d_off, \
+                       total_rows, dirty, d_status);                                               \
+    break;
+#ifdef B2F_DIAG
+    B2F_EVFAST(0) B2F_EVFAST(1) B2F_EVFAST(8) B2F_EVFAST(16)
+#endif
+    default: B2F_EVFAST(FZ_FULL)
+#undef B2F_EVFAST
+  }
+  *gate = dirty;
+  return hipGetLastError();
 }
 // Instance tiles of a batch of n instances in at most total_rows rows (an upper bound).
 uint64_t fused_instance_tiles(uint64_t total_rows, uint64_t n) {

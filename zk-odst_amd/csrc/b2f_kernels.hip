@@ -53,6 +53,9 @@ hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint6
                             int cu_count, hipStream_t s);  // b2f_export.hip
 size_t fused_scratch_bytes(uint64_t tiles);
 uint64_t fused_instance_tiles(uint64_t total_rows, uint64_t n);
+hipError_t launch_eval_fast(const uint32_t* d_adv, const uint32_t* d_fixed, const uint64_t* d_off, uint32_t n,
+                            uint64_t total_rows, void* scratch, uint64_t tiles, const int* d_status,
+                            int cu_count, hipStream_t s, const uint32_t** gate, int mode);  // b2f_fused.hip
 hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d_off,
                             uint64_t total_rows, const uint64_t* rec, uint32_t* d_adv,
                             uint32_t* d_fixed, void* scratch, uint64_t tiles,
@@ -438,7 +441,11 @@ __global__ void __launch_bounds__(BLOCK, B2F_EVAL_WAVES) eval_kernel(const uint3
                                                     b2f_eval_report* __restrict__ rep,
                                                     int* __restrict__ status,
                                                     int* __restrict__ sticky,
-                                                    unsigned long long* __restrict__ clk) {
+                                                    unsigned long long* __restrict__ clk,
+                                                    const uint32_t* __restrict__ gate) {
+  // gate: the fast clean-check pass (launch_eval_fast) found nothing to record -- the report
+  // report_init_kernel wrote is already the verdict (an accepted layout only)
+  if (gate && *gate == 0 && *status == 0) return;
   __shared__ __attribute__((aligned(16))) uint32_t L[LDS_WORDS];
   uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
   auto tick = [&](int k) {
@@ -1118,6 +1125,20 @@ B2F_API int b2f_fill_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const ui
   return B2F_OK;
 }
 
+// The fused path's scratch (tile descriptors, deferred rows, redo list, the eval's dirty word),
+// grown on demand.
+static int ensure_fused_scratch(b2f_ctx* ctx, size_t need, hipStream_t s) {
+  if (need > ctx->fz_cap) {
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    if (ctx->d_fz) HIPCHK(ctx, hipFree(ctx->d_fz));
+    ctx->d_fz = nullptr;
+    ctx->fz_cap = 0;
+    HIPCHK(ctx, hipMalloc(&ctx->d_fz, need));
+    ctx->fz_cap = need;
+  }
+  return B2F_OK;
+}
+
 B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
                               const uint64_t* d_offsets, uint64_t total_rows, uint32_t* d_advice,
                               uint32_t* d_fixed, uint64_t* d_h_out, b2f_eval_report* d_report,
@@ -1128,15 +1149,8 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
   int rc = fill_prologue(ctx, d_in, n, d_offsets, total_rows, d_advice, d_fixed, d_h_out, d_report, s);
   if (rc) return rc;
   const uint64_t tiles = fused_instance_tiles(total_rows, n);
-  const size_t need = fused_scratch_bytes(tiles);
-  if (need > ctx->fz_cap) {
-    HIPCHK(ctx, hipStreamSynchronize(s));
-    if (ctx->d_fz) HIPCHK(ctx, hipFree(ctx->d_fz));
-    ctx->d_fz = nullptr;
-    ctx->fz_cap = 0;
-    HIPCHK(ctx, hipMalloc(&ctx->d_fz, need));
-    ctx->fz_cap = need;
-  }
+  rc = ensure_fused_scratch(ctx, fused_scratch_bytes(tiles), s);
+  if (rc) return rc;
   const int fmode = fused_mode();
   if ((fmode & 128) && !ctx->d_clock) {
     HIPCHK(ctx, hipMalloc(&ctx->d_clock, 32 * sizeof(unsigned long long)));
@@ -1200,13 +1214,31 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
     HIPCHK(ctx, hipMalloc(&ctx->d_clock, 32 * sizeof(unsigned long long)));
     HIPCHK(ctx, hipMemset(ctx->d_clock, 0, 32 * sizeof(unsigned long long)));
   }
+  // the product path: the fast clean-check pass first; the exact eval kernel runs only if it
+  // flagged something (device-side gate). Diagnostic modes run the exact kernel alone.
+  const uint32_t* gate = nullptr;
+  // (diagnostics: B2F_DIAG_EVALFAST = the fast pass's check mode, the exact kernel then skipped)
+  const int fmode = diag_mode("B2F_DIAG_EVALFAST", 27);
+  const bool fast = (emode == EVAL_FULL || fmode != 27) && total_rows >= (uint64_t)FIXED_ROWS * n;
+  if (fast) {
+    rc = ensure_fused_scratch(ctx, fused_scratch_bytes(fused_instance_tiles(total_rows, n)), s);
+    if (rc) return rc;
+  }
   int tk = timed_begin(ctx, B2F_KERNEL_EVAL, s);
+  if (fast)
+    HIPCHK(ctx, launch_eval_fast(d_advice, d_fixed, d_offsets, (uint32_t)n, total_rows, ctx->d_fz,
+                                 fused_instance_tiles(total_rows, n), ctx->d_status + 1, ctx->cu_count, s, &gate,
+                                 fmode));
+  if (fmode != 27) {  // diagnostics: the fast pass alone
+    timed_end(ctx, tk, s);
+    return B2F_OK;
+  }
   switch (emode) {
 #define B2F_EVAL(M)                                                                             \
   case M:                                                                                       \
     hipLaunchKernelGGL(eval_kernel<M>, dim3(wgs), dim3(BLOCK), 0, s, d_advice, d_fixed,         \
                        d_offsets, (uint32_t)n, total_rows, ctx->d_tiles, nt, d_report,          \
-                       ctx->d_status + 1, ctx->d_status + 2, ctx->d_clock);                     \
+                       ctx->d_status + 1, ctx->d_status + 2, ctx->d_clock, gate);               \
     break;
 #ifdef B2F_DIAG
     B2F_EVAL(1) B2F_EVAL(2) B2F_EVAL(3) B2F_EVAL(4) B2F_EVAL(5) B2F_EVAL(6) B2F_EVAL(8)
