@@ -25,8 +25,11 @@ def per_kernel(d, counter):
             if r["Counter_Name"] != counter:
                 continue
             k = r["Kernel_Name"]
-            kind = ("fill" if "fill_kernel" in k else "eval" if "eval_kernel" in k
-                    else "fill_eval_edge" if "fused_kernel<27, 2>" in k
+            # the fused path is two launches per step (half-round tiles, then the edge regions);
+            # the eval is the fast pass (half-round + edge launches) and the gated exact kernel
+            kind = ("fill" if "fill_kernel" in k
+                    else "eval_part" if ("eval_hr_kernel" in k or "eval_edge_kernel" in k) else "eval" if "eval_kernel" in k
+                    else "fill_eval_edge" if ("fused_kernel<27, 2>" in k or "fused_edge_kernel" in k)
                     else "fill_eval" if ("fused_kernel" in k or "fused_hr_kernel" in k) else None)
             if kind is None:
                 continue
@@ -46,6 +49,8 @@ def main():
     for d in (fetch, write):
         if "fill_eval_edge" in d:
             d["fill_eval"] = d.get("fill_eval", 0.0) + d.pop("fill_eval_edge")
+        if "eval_part" in d:  # per launch; two launches (half-round, edge) per eval call
+            d["eval"] = d.get("eval", 0.0) + 2 * d.pop("eval_part")
     res = json.load(open(out)) if os.path.exists(out) else {}
     for kind in ("fill", "eval", "fill_eval"):
         if kind not in fetch or kind not in write:
