@@ -9,10 +9,12 @@ agg = collections.OrderedDict()
 for f in sorted(glob.glob(root + "/*/p_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "fill_kernel" not in k and "eval_kernel" not in k and "fused_kernel" not in k:
+        if not any(t in k for t in ("fill_kernel", "eval_kernel", "eval_hr_kernel", "eval_edge_kernel",
+                                    "fused_kernel", "fused_hr_kernel", "fused_edge_kernel")):
             continue
-        name = k.split("(")[0].split("::")[-1]
-        mode = k.split("<")[1].split(">")[0] if "<" in k else ""
+        name = k.split("(anonymous namespace)::")[1].split("<")[0].split("(")[0]
+        head = k.split("(anonymous namespace)::")[1].split("(")[0]
+        mode = head.split("<")[1].split(">")[0] if "<" in head else ""
         key = (name + "<" + mode + ">", f.split("/")[-2], r["Dispatch_Id"])
         agg.setdefault(key, {})[r["Counter_Name"]] = agg.get(key, {}).get(r["Counter_Name"], 0) + float(r["Counter_Value"])
 for (name, run, disp), c in agg.items():
