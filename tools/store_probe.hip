@@ -221,6 +221,74 @@ __global__ void __launch_bounds__(256) wave_rr_ldswork(uint32_t* adv, uint64_t t
   if (NOSTORE && h == 0x12345678u) adv[lane] = h;
 }
 
+
+// wave-specialised: NC compute waves per workgroup produce tiles (the work120 hash, 11 columns x
+// 52 quads) into NSLOT LDS slots each; one store wave per workgroup drains the slots in tile
+// order and issues the 11 column stores. Slot handshake by LDS counters: compute waits for the
+// slot's drain count, fills it, bumps its fill count; the store wave waits for the fill count,
+// reads the slot into registers, bumps the drain count, stores. NOSTORE: drain without storing.
+template <int NC, int NSLOT, bool NOSTORE>
+__global__ void __launch_bounds__((NC + 1) * 64) wave_spec(uint32_t* adv, uint64_t total_rows, int work) {
+  constexpr int STEP = 52, SW = 11 * STEP * 4;
+  __shared__ __attribute__((aligned(16))) uint32_t L[NC * NSLOT * SW];
+  __shared__ uint32_t Fc[NC * NSLOT], Dc[NC * NSLOT];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint64_t total_quads = total_rows >> 2;
+  const uint64_t n_t = (total_quads + STEP - 1) / STEP;
+  const uint64_t ncw = (uint64_t)gridDim.x * NC;
+  if (threadIdx.x < NC * NSLOT) {
+    Fc[threadIdx.x] = 0;
+    Dc[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  volatile uint32_t* vF = Fc;
+  volatile uint32_t* vD = Dc;
+  if (w < NC) {
+    uint32_t h = lane;
+    uint32_t r = 0;
+    for (uint64_t t = (uint64_t)blockIdx.x * NC + w; t < n_t; t += ncw, r++) {
+      const uint64_t q = t * STEP + lane;
+      h ^= (uint32_t)q;
+      for (int k = 0; k < work; k++) h = (h ^ (h >> 7)) * 0x9E3779B1u + (uint32_t)k;
+      const uint32_t sl = w * NSLOT + r % NSLOT, seq = r / NSLOT;
+      while (__builtin_amdgcn_readfirstlane(vD[sl]) != seq) __builtin_amdgcn_s_sleep(1);
+      uint32_t* S = L + sl * SW;
+      if (lane < STEP) {
+#pragma unroll
+        for (int c = 0; c < 11; c++)
+          *reinterpret_cast<u32x4*>(S + c * STEP * 4 + 4 * lane) = u32x4{h + c, h ^ c, h * c, h - c};
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) vF[sl] = seq + 1;
+    }
+  } else {
+    for (uint32_t r = 0;; r++) {
+      const uint64_t t0 = (uint64_t)blockIdx.x * NC + (uint64_t)r * ncw;
+      if (t0 >= n_t) break;
+      for (int cw = 0; cw < NC; cw++) {
+        const uint64_t t = t0 + cw;
+        if (t >= n_t) break;
+        const uint32_t sl = cw * NSLOT + r % NSLOT, seq = r / NSLOT;
+        while (__builtin_amdgcn_readfirstlane(vF[sl]) != seq + 1) __builtin_amdgcn_s_sleep(1);
+        const uint32_t* S = L + sl * SW;
+        u32x4 v[11];
+#pragma unroll
+        for (int c = 0; c < 11; c++) v[c] = *reinterpret_cast<const u32x4*>(S + c * STEP * 4 + 4 * (lane < STEP ? lane : 0));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) vD[sl] = seq + 1;
+        const uint64_t q = t * STEP + lane;
+        if (!NOSTORE && lane < STEP && q < total_quads) {
+#pragma unroll
+          for (int c = 0; c < 11; c++)
+            __builtin_nontemporal_store(v[c], reinterpret_cast<u32x4*>(adv + (uint64_t)c * total_rows + 4 * q));
+        } else if (NOSTORE && v[3].x == 0x12345678u && v[5].y == 7u) {
+          adv[lane] = v[0].x;
+        }
+      }
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? atoi(argv[1]) : (1u << 18);
   const uint32_t rows_per = 228 + 416 * 12;
@@ -252,6 +320,27 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
   const uint64_t nt = (total + 1023) / 1024;
+  if (argc > 2 && argv[2][0] == 's') {  // wave-specialised store waves vs the burst pattern
+    for (int work : {0, 120, 240}) {
+      char nm[96];
+      snprintf(nm, sizeof nm, "work%d_burst", work);
+      run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<52, false, false>), dim3(cus * 4), dim3(256), 0, 0, adv, total, work); });
+      snprintf(nm, sizeof nm, "work%d_nostore", work);
+      run(nm, [&] { hipLaunchKernelGGL(wave_rr_nostore<52>, dim3(cus * 4), dim3(256), 0, 0, adv, total, work); });
+#define SPEC(NC, NS, WG)                                                                          \
+      snprintf(nm, sizeof nm, "work%d_spec_c%d_s%d_wg%d", work, NC, NS, WG);                     \
+      run(nm, [&] { hipLaunchKernelGGL((wave_spec<NC, NS, false>), dim3(cus * WG), dim3((NC + 1) * 64), 0, 0, adv, total, work); }); \
+      snprintf(nm, sizeof nm, "work%d_spec_c%d_s%d_wg%d_nostore", work, NC, NS, WG);             \
+      run(nm, [&] { hipLaunchKernelGGL((wave_spec<NC, NS, true>), dim3(cus * WG), dim3((NC + 1) * 64), 0, 0, adv, total, work); });
+      SPEC(4, 2, 2)
+      SPEC(2, 2, 4)
+      SPEC(3, 2, 2)
+      SPEC(7, 1, 2)
+      SPEC(4, 3, 1)
+#undef SPEC
+    }
+    return 0;
+  }
   if (argc > 2 && argv[2][0] == 'l') {  // LDS-latency work vs VALU work, with and without stores
     for (int work : {120}) {
       char nm[96];

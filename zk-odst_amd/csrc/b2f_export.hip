@@ -12,9 +12,10 @@
 // same values with a generic Montgomery multiply by R^2, oracle/b2f_oracle.c).
 // Canonical form (PrimeField::to_repr, 32-byte little endian) is simply (x, 0, 0, 0), in
 // either field.
-// BN254 Fr (halo2curves 0.3.2 bn256::Fr, r < 2^254, no such short form): mont(x) is the
-// generic Montgomery product x * R^2 / R with the one-word operand's zero words folded
-// (b2f_field.h; 8 + 64 word products).
+// BN254 Fr (halo2curves 0.3.2 bn256::Fr, r < 2^254, no such short form of r): mont(x) =
+// x * (2^256 mod r) mod r with a 32-bit quotient from a fixed-point reciprocal
+// (field::from_u32: 16 word products; the generic Montgomery product by R^2 it replaced took
+// 72 and made this kernel VALU-bound, 4.9 ms at 2^25 rows).
 //
 // HBM-bound: 4 B read, 32 B written per cell. A wave writes 64 x 16 B = 1 KiB contiguous per
 // store instruction (lane l stores 16-byte chunk l of a 1 KiB span, i.e. half l & 1 of cell
@@ -42,10 +43,19 @@ constexpr uint64_t kD1 = 0x224698fc094cf91bull;  // d, high limb
 constexpr int EXPORT_BLOCK = 256;
 constexpr int CELLS_PER_ITER = EXPORT_BLOCK / 2;  // 128 cells = 4 KiB of output per WG pass
 
-// limbs (2*half, 2*half+1) of the field element for cell value x: canonical (either field)
-// or pasta Montgomery (the closed form above)
+__device__ __forceinline__ u64x2 bn254_half(uint32_t x, uint32_t half) {
+  const field::Fe m = field::from_u32<field::Bn254>(x);
+  uint32_t o[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) o[i] = half ? m.w[4 + i] : m.w[i];  // no dynamic index (scratch)
+  return u64x2{(uint64_t)o[0] | ((uint64_t)o[1] << 32), (uint64_t)o[2] | ((uint64_t)o[3] << 32)};
+}
+
+// limbs (2*half, 2*half+1) of the field element for cell value x: canonical (either field),
+// pasta Montgomery (the closed form above) or BN254 Montgomery (FORM 3)
 template <int FORM>
 __device__ __forceinline__ u64x2 fp_half(uint32_t x, uint32_t half) {
+  if (FORM == 3) return bn254_half(x, half);
   u64x2 r;
   if (!(FORM & 1)) {  // canonical, either field
     r.x = half ? 0 : x;
@@ -116,27 +126,6 @@ __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
   }
 }
 
-// BN254 Fr Montgomery form: a generic Montgomery product per element (b2f_field.h), so one lane
-// per element (two 16-byte stores; a wave's pair covers 2 KiB contiguous), grid-stride.
-__global__ __launch_bounds__(256) void export_bn254_kernel(const uint32_t* __restrict__ advice,
-                                                           uint64_t total_rows, uint64_t row_begin,
-                                                           uint64_t nrows, uint64_t* __restrict__ out,
-                                                           uint64_t out_rows) {
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t cell = (uint64_t)blockIdx.x * 256 + threadIdx.x; cell < nrows; cell += stride) {
-#pragma unroll 2
-    for (int h = 0; h < 10; h++) {
-      const uint32_t x = advice[(uint64_t)kAofH[h] * total_rows + row_begin + cell];
-      const field::Fe m = field::from_u32<field::Bn254>(x);
-      u64x2* dst = reinterpret_cast<u64x2*>(out + ((uint64_t)h * out_rows + cell) * 4);
-      __builtin_nontemporal_store(u64x2{(uint64_t)m.w[0] | ((uint64_t)m.w[1] << 32),
-                                        (uint64_t)m.w[2] | ((uint64_t)m.w[3] << 32)}, dst);
-      __builtin_nontemporal_store(u64x2{(uint64_t)m.w[4] | ((uint64_t)m.w[5] << 32),
-                                        (uint64_t)m.w[6] | ((uint64_t)m.w[7] << 32)}, dst + 1);
-    }
-  }
-}
-
 // The spread table as the prover's three table (fixed) columns tag, dense, spread
 // (SpreadTableChip::load, spread_table.rs:470-508: row x < 2^16 holds (tag(x), x, spread(x)),
 // spread_table.rs:574-600), then the layouter's fill_from_row default -- row 0's values,
@@ -162,9 +151,7 @@ __global__ __launch_bounds__(256) void spread_table_kernel(uint64_t usable_rows,
     u64x2* dst = reinterpret_cast<u64x2*>(out + (uint64_t)c * out_rows * 4);
     u64x2 e;
     if (form == B2F_FP_BN254_MONTGOMERY) {
-      const field::Fe m = field::from_u32<field::Bn254>(v[c]);
-      const uint32_t o = 4 * half;
-      e = u64x2{(uint64_t)m.w[o] | ((uint64_t)m.w[o + 1] << 32), (uint64_t)m.w[o + 2] | ((uint64_t)m.w[o + 3] << 32)};
+      e = bn254_half(v[c], half);
     } else {
       e = form & 1u ? fp_half<1>(v[c], half) : fp_half<0>(v[c], half);
     }
@@ -187,13 +174,13 @@ hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint6
                             int cu_count, hipStream_t s) {
   // persistent grid: 4 workgroups per CU (halo2 column h -> a_i by kAofH)
   uint64_t tiles = (nrows + XT - 1) / XT;
-  uint64_t want = (uint64_t)cu_count * 4;  // 122 VGPRs: 4 waves/SIMD
+  // 122 VGPRs: 4 waves/SIMD; BN254 Montgomery 140 VGPRs: 3 (every workgroup resident at once)
+  uint64_t want = (uint64_t)cu_count * (form == B2F_FP_BN254_MONTGOMERY ? 3 : 4);
   uint32_t gx = (uint32_t)(tiles < want ? tiles : want);
   if (gx == 0) return hipSuccess;
   if (form == B2F_FP_BN254_MONTGOMERY) {
-    const uint64_t blocks = (nrows + 255) / 256, cap = (uint64_t)cu_count * 8;
-    hipLaunchKernelGGL(export_bn254_kernel, dim3((uint32_t)(blocks < cap ? blocks : cap)), dim3(256), 0, s,
-                       d_advice, total_rows, row_begin, nrows, d_out, out_rows);
+    hipLaunchKernelGGL(export_fp_kernel<3>, dim3(gx), dim3(EXPORT_BLOCK), 0, s, d_advice,
+                       total_rows, row_begin, nrows, d_out, out_rows);
   } else if (form & 1u) {
     hipLaunchKernelGGL(export_fp_kernel<1>, dim3(gx), dim3(EXPORT_BLOCK), 0, s, d_advice,
                        total_rows, row_begin, nrows, d_out, out_rows);

@@ -31,6 +31,7 @@ struct Pallas {
   static constexpr uint32_t R3[8] = {0x3a9e10f9u, 0xf185a599u, 0x6ac5b1d1u, 0xf6a68f3bu,
                                      0x353fd42cu, 0xdf8d1014u, 0x2d2d9910u, 0x2ae30922u};
   static constexpr uint32_t NP = 0xffffffffu;  // -p^-1 mod 2^32
+  static constexpr uint64_t RQ = 0xffffffffffffffffull;  // floor(R 2^64 / p), R = 2^256 mod p
 };
 
 struct Bn254 {
@@ -43,6 +44,7 @@ struct Bn254 {
   static constexpr uint32_t R3[8] = {0xb4bf0040u, 0x5e94d8e1u, 0x1cfbb6b8u, 0x2a489cbeu,
                                      0xa19fcfedu, 0x893cc664u, 0x7fcc657cu, 0x0cf8594bu};
   static constexpr uint32_t NP = 0xefffffffu;
+  static constexpr uint64_t RQ = 0x4a47462623a04a7aull;
 };
 
 static_assert(Pallas::P[7] < 0x7ffffffeu && Bn254::P[7] < 0x7ffffffeu, "no-carry CIOS needs a spare top bit");
@@ -135,12 +137,27 @@ __device__ __forceinline__ Fe add(const Fe& a, const Fe& b) {  // a + b < 2p < 2
   return reduce_once<F>(s);
 }
 
-// Montgomery form of a small integer: x R = mont(x, R^2)
+// Montgomery form of a small integer, x R mod p, without a Montgomery product: with c = R mod p
+// (F::R), x c < 2^32 p, so the quotient fits 32 bits and q' = floor(x RQ / 2^64) is q or q - 1
+// (x c / p - x RQ / 2^64 < x / 2^64 < 1). x c - q' p is in [0, 2p): computed mod 2^256 as 16
+// word products, then one conditional subtraction (the generic route, mont(x, R^2), is 72).
 template <class F>
 __device__ __forceinline__ Fe from_u32(uint32_t x) {
-  Fe a = fe_zero();
-  a.w[0] = x;
-  return mul<F>(a, fe_const<F>(F::R2));
+  const uint32_t q = (uint32_t)__umul64hi((uint64_t)x, F::RQ);
+  Fe w;
+  uint64_t ca = 0, cb = 0;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t ta = (uint64_t)x * F::R[i] + ca;
+    const uint64_t tb = (uint64_t)q * F::P[i] + cb;
+    ca = ta >> 32;
+    cb = tb >> 32;
+    const uint64_t td = (uint64_t)(uint32_t)ta - (uint32_t)tb - br;
+    w.w[i] = (uint32_t)td;
+    br = (uint32_t)(td >> 63);
+  }
+  return reduce_once<F>(w);
 }
 
 // Montgomery form of a canonical element (< p)
