@@ -147,6 +147,12 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
  * fused verdict equals b2f_eval_dev's / the oracle's on the trace actually written. */
 B2F_API int b2f_debug_inject(b2f_ctx* ctx, uint64_t row, uint32_t col, uint32_t mask);
 
+/* Test hook: which path the last b2f_eval_dev call of `ctx` took, after a device synchronize:
+ * *out = 0 the fast clean-check pass found the trace clean (its report stands), 1 the pass
+ * flagged something and the exact eval kernel wrote the report, 2 no fast pass ran (the exact
+ * kernel alone). Lets tests prove a clean trace costs the fast pass only. */
+B2F_API int b2f_debug_eval_path(b2f_ctx* ctx, uint32_t* out);
+
 /* Diagnostics: eval-kernel phase cycle totals (s_memtime deltas summed over workgroups) of
  * the EVAL_CLOCK variant since the previous call; out[8 * wave + phase], phases:
  * stage+lookups, barrier 1, prefetch issue, G-table build, gate pass, copies, per-quad paths,

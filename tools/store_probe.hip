@@ -341,6 +341,18 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (argc > 2 && argv[2][0] == 'i') {  // instance-per-wave orders vs the half-round round robin
+    for (int w : {4, 8}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "wave_rr_q52_%dwg", w);
+      run(nm, [&] { hipLaunchKernelGGL(wave_rr_store<52>, dim3(cus * w), dim3(256), 0, 0, adv, total); });
+      snprintf(nm, sizeof nm, "wave_dyn_step52_%dwg", w);
+      run(nm, [&] { hipLaunchKernelGGL((wave_store<52, true>), dim3(cus * w), dim3(256), 0, 0, adv, total, n, rows_per, ctr); });
+      snprintf(nm, sizeof nm, "wave_static_step52_%dwg", w);
+      run(nm, [&] { hipLaunchKernelGGL((wave_store<52, false>), dim3(cus * w), dim3(256), 0, 0, adv, total, n, rows_per, ctr); });
+    }
+    return 0;
+  }
   if (argc > 2 && argv[2][0] == 'l') {  // LDS-latency work vs VALU work, with and without stores
     for (int work : {120}) {
       char nm[96];
@@ -385,7 +397,7 @@ int main(int argc, char** argv) {
     snprintf(nm, sizeof nm, "wave_rr_q64_%dwg", w);
     run(nm, [&] { hipLaunchKernelGGL(wave_rr_store<64>, dim3(cus * w), dim3(256), 0, 0, adv, total); });
   }
-  for (int w : {0}) {
+  for (int w : {4, 8}) {
     char nm[64];
     snprintf(nm, sizeof nm, "wave_dyn_step52_%dwg", w);
     run(nm, [&] { hipLaunchKernelGGL((wave_store<52, true>), dim3(cus * w), dim3(256), 0, 0, adv, total, n, rows_per, ctr); });

@@ -77,6 +77,7 @@ SIGNATURES = [
     ("b2f_fill_eval_dev", I32, [P, P, SIZE, P, U64, P, P, P, P, P]),
     ("b2f_debug_inject", I32, [P, U64, ctypes.c_uint32, ctypes.c_uint32]),
     ("b2f_debug_clock", I32, [P, P]),
+    ("b2f_debug_eval_path", I32, [P, P]),
     ("b2f_fill_fixed_dev", I32, [P, P, SIZE, U64, P, P]),
     ("b2f_copy_constraints", U64, [ctypes.c_uint32, P, U64]),
     ("b2f_chain_inputs_dev", I32, [P, P, P, P, P, ctypes.c_uint32, SIZE, P, P]),

@@ -144,6 +144,14 @@ class Engine:
             int(usable_rows), lim[0], lim[1], lim[2], lim[3], int(chunk_len), int(form),
             _vp(d_sigma) if d_sigma else None, _vp(d_z), int(out_rows), _vp(stream)))
 
+    def debug_eval_path(self):
+        """Path of the last eval_dev call (device-synchronizing): 0 the fast clean-check pass
+        found the trace clean, 1 it flagged something and the exact eval kernel reported, 2 no
+        fast pass ran."""
+        out = ctypes.c_uint32(0)
+        self._check(self.lib.b2f_debug_eval_path(self.ctx, ctypes.byref(out)))
+        return int(out.value)
+
     def sync(self, stream=0):
         self._check(self.lib.b2f_sync(self.ctx, _vp(stream)))
 

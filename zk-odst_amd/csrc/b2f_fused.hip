@@ -1001,7 +1001,13 @@ constexpr int T_GS = T_WD + 112;
 constexpr int T_PG = T_GS + 128;
 static_assert(T_PG + 32 <= NSTAGE * STR, "transient words inside columns a_9 and fixed");
 // workgroup LDS (words)
-constexpr int H_ACC = 0, H_IV = 24, H_SG = H_IV + 16, H_WAVE = H_SG + 40;
+// H_SPT: the byte spread table (256 x u16, spread8(i) at byte 2 i), read by spread_t
+#ifdef B2F_HR_SPT
+constexpr int SPT_WORDS = 128;
+#else
+constexpr int SPT_WORDS = 0;
+#endif
+constexpr int H_ACC = 0, H_IV = 24, H_SG = H_IV + 16, H_SPT = H_SG + 40, H_WAVE = H_SPT + SPT_WORDS;
 constexpr int H_WORDS = H_WAVE + WAVES * HW_WORDS;
 static_assert(H_WAVE % 4 == 0 && HW_WORDS % 4 == 0 && T_WD % 4 == 0 && T_GS % 4 == 0 && T_PG % 4 == 0,
               "16-byte aligned carve");
@@ -1042,6 +1048,17 @@ __device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) { return (uin
 // tag of a 16-bit value (0: < 2^8, 1: < 2^15, 2: otherwise), branch-free
 __device__ __forceinline__ uint32_t tag_of(uint32_t x) { return ((x + 0xff00u) >> 16) + (x >> 15); }
 __device__ __forceinline__ uint32_t sel32(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+// spread16 of the low 16 bits of x by two lookups in the byte spread table at LDS byte address
+// `tb` (4 VALU + 2 LDS reads instead of 8-12 VALU for the shift/mask interleave)
+__device__ __forceinline__ uint32_t spread_t(uint32_t tb, uint32_t x) {
+#ifndef B2F_HR_SPT  // the table form measured 1 % slower in the fused kernel (more LDS traffic)
+  return spread16(x & 0xffffu);
+#else
+  const uint32_t lo = ld16(tb + ((x & 0xffu) << 1));
+  const uint32_t hi = ld16(tb + ((x >> 7) & 0x1feu));
+  return lo | (hi << 16);
+#endif
+}
 
 // A tile as the wave sees it (wave-uniform).
 struct HCtx {
@@ -1298,12 +1315,16 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
   if (tid == 22) *reinterpret_cast<uint64_t*>(L + H_ACC + 20) = ~0ull;
   if (tid < 16) L[H_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
   if (tid < 40) L[H_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
+#ifdef B2F_HR_SPT
+  reinterpret_cast<uint16_t*>(L + H_SPT)[tid & 255] = (uint16_t)spread16((uint32_t)tid & 255u);
+#endif
   __syncthreads();
   EvalAcc A{L + H_ACC};
   const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + H_IV);
   const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + H_SG);
   uint32_t* S = L + H_WAVE + wv * HW_WORDS;  // this wave's staging
   const uint32_t Sb = lds_byte(S);
+  const uint32_t TB = lds_byte(L + H_SPT);
   const Lane K = make_lane(lane, Sb);
   const bool qlane = lane < HR_Q, p0 = qlane && (lane % G_QUADS) == 0;
   const bool plane = lane >= HR_Q && lane < HR_Q + 4;
@@ -1396,7 +1417,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       const uint32_t pv = ld32(par ? K.aLTs >> 16 : K.aLTs & 0xffffu);
       const uint32_t lv = (pv >> K.ltsh) & 0xffffu;
       st32(K.aLTd, lv);
-      st32(K.aLTd + 256, spread16(lv));
+      st32(K.aLTd + 256, spread_t(TB, lv));
       // ---- 4. the cells
       const uint64_t s1 = X + Y, Sm = s1 + M;
       const uint32_t carry = (uint32_t)(s1 < X) + (uint32_t)(Sm < s1);
@@ -1415,29 +1436,32 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       const uint32_t wA = perm(Wh, Wl, K.slA) & K.mhw, wB = perm(Wh, Wl, K.slB) & K.mhw;
       const uint32_t zA = (perm(hi32(Z), lo32(Z), K.slA) >> 15) & K.mhz;
       const uint32_t zB = (perm(hi32(Z), lo32(Z), K.slB) >> 15) & K.mhz;
-      const uint32_t P3 = sel32(K.madd, hi32(X), spread16(xB)), Q3 = sel32(K.madd, lo32(X), spread16(xA));
-      const uint32_t P4 = sel32(K.madd, hi32(Y), spread16(yB)), Q4 = sel32(K.madd, lo32(Y), spread16(yA));
-      const uint32_t swA = spread16(wA), swB = spread16(wB);
+      const uint32_t P3 = sel32(K.madd, hi32(X), spread_t(TB, xB)), Q3 = sel32(K.madd, lo32(X), spread_t(TB, xA));
+      const uint32_t P4 = sel32(K.madd, hi32(Y), spread_t(TB, yB)), Q4 = sel32(K.madd, lo32(Y), spread_t(TB, yA));
+      const uint32_t swA = spread_t(TB, wA), swB = spread_t(TB, wB);
       if (qlane) {
         const uint64_t qrow = c.row0 + 4ull * lane;
-        emit<MODE>(S, A0, lane, qrow, tag_of(v[0]), tag_of(v[1]), tag_of(v[2]), tag_of(v[3]), adv, fixed, total_rows, inj, true);
-        emit<MODE>(S, A1, lane, qrow, v[0], v[1], v[2], v[3], adv, fixed, total_rows, inj, true);
-        emit<MODE>(S, A2, lane, qrow, spread16(v[0]), spread16(v[1]), spread16(v[2]), spread16(v[3]), adv, fixed, total_rows, inj, true);
-        emit<MODE>(S, A3, lane, qrow, perm(P3, Q3, K.slot[0]), perm(P3, Q3, K.slot[1]), perm(P3, Q3, K.slot[2]),
-                   perm(P3, Q3, K.slot[3]), adv, fixed, total_rows, inj, true);
-        emit<MODE>(S, A4, lane, qrow, perm(P4, Q4, K.slot[0]), perm(P4, Q4, K.slot[1]), perm(P4, Q4, K.slot[2]),
-                   perm(P4, Q4, K.slot[3]), adv, fixed, total_rows, inj, true);
-        emit<MODE>(S, A5, lane, qrow, perm(hi32(M), lo32(M), limb_sel(0)), perm(hi32(M), lo32(M), limb_sel(1)),
-                   perm(hi32(M), lo32(M), limb_sel(2)), perm(hi32(M), lo32(M), limb_sel(3)), adv, fixed, total_rows, inj, true);
-        emit<MODE>(S, A6, lane, qrow, perm(zB, zA, K.slot[0]), perm(zB, zA, K.slot[1]), perm(zB, zA, K.slot[2]),
-                   perm(zB, zA, K.slot[3]), adv, fixed, total_rows, inj, true);
-        emit<MODE>(S, A7, lane, qrow, perm(wB, wA, K.slot[0]), perm(wB, wA, K.slot[1]), perm(wB, wA, K.slot[2]),
-                   perm(wB, wA, K.slot[3]), adv, fixed, total_rows, inj, true);
-        emit<MODE>(S, A8, lane, qrow, perm(swB, swA, K.slot[0]), perm(swB, swA, K.slot[1]), perm(swB, swA, K.slot[2]),
-                   perm(swB, swA, K.slot[3]), adv, fixed, total_rows, inj, true);
+auto put = [&](int col, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
+          emit<MODE>(S, col, lane, qrow, v0, v1, v2, v3, adv, fixed, total_rows, inj, true);
+        };
+        put(A0, tag_of(v[0]), tag_of(v[1]), tag_of(v[2]), tag_of(v[3]));
+        put(A1, v[0], v[1], v[2], v[3]);
+        put(A2, spread_t(TB, v[0]), spread_t(TB, v[1]), spread_t(TB, v[2]), spread_t(TB, v[3]));
+        put(A3, perm(P3, Q3, K.slot[0]), perm(P3, Q3, K.slot[1]), perm(P3, Q3, K.slot[2]),
+            perm(P3, Q3, K.slot[3]));
+        put(A4, perm(P4, Q4, K.slot[0]), perm(P4, Q4, K.slot[1]), perm(P4, Q4, K.slot[2]),
+            perm(P4, Q4, K.slot[3]));
+        put(A5, perm(hi32(M), lo32(M), limb_sel(0)), perm(hi32(M), lo32(M), limb_sel(1)),
+            perm(hi32(M), lo32(M), limb_sel(2)), perm(hi32(M), lo32(M), limb_sel(3)));
+        put(A6, perm(zB, zA, K.slot[0]), perm(zB, zA, K.slot[1]), perm(zB, zA, K.slot[2]),
+            perm(zB, zA, K.slot[3]));
+        put(A7, perm(wB, wA, K.slot[0]), perm(wB, wA, K.slot[1]), perm(wB, wA, K.slot[2]),
+            perm(wB, wA, K.slot[3]));
+        put(A8, perm(swB, swA, K.slot[0]), perm(swB, swA, K.slot[1]), perm(swB, swA, K.slot[2]),
+            perm(swB, swA, K.slot[3]));
         // last: these two columns hold the transient words until here
-        emit<MODE>(S, A9, lane, qrow, carry & K.madd, 0u, 0u, 0u, adv, fixed, total_rows, inj, true);
-        emit<MODE>(S, FXC, lane, qrow, K.fx0, 0u, 0u, 0u, adv, fixed, total_rows, inj, true);
+        put(A9, carry & K.madd, 0u, 0u, 0u);
+        put(FXC, K.fx0, 0u, 0u, 0u);
       }
       tick(2);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staging is complete
@@ -1465,7 +1489,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
 #pragma unroll
           for (int j = 0; j < 4; j++) {
             const uint32_t de = comp(q1, j);
-            acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(q0, j)) | (spread16(de) ^ comp(q2, j));
+            acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(q0, j)) | (spread_t(TB, de) ^ comp(q2, j));
           }
         }
         if (MODE & FZ_GATES) acc |= (fx.x ^ K.fx0) | fx.y | fx.z | fx.w;
@@ -2083,7 +2107,8 @@ struct EvCells {
 };
 __device__ __forceinline__ EvCells ev_load(const hr2::HCtx& c, uint32_t lane, uint32_t lq, uint32_t mg, uint32_t mwh,
                                            uint32_t mk, const uint32_t* __restrict__ adv,
-                                           const uint32_t* __restrict__ fixed, uint64_t total_rows, const uint8_t* Sg) {
+                                           const uint32_t* __restrict__ fixed, uint64_t total_rows, const uint8_t* Sg,
+                                           bool gath) {
   EvCells v;
   const uint32_t* p = adv + c.row0 + 4 * lq;
   v.c0 = *reinterpret_cast<const uint4*>(p);
@@ -2097,10 +2122,12 @@ __device__ __forceinline__ EvCells ev_load(const hr2::HCtx& c, uint32_t lane, ui
   v.c8 = *reinterpret_cast<const uint4*>(p + 8 * total_rows);
   v.c9 = *reinterpret_cast<const uint4*>(p + 9 * total_rows);
   v.c10 = *reinterpret_cast<const uint4*>(fixed + c.row0 + 4 * lq);
+  // the limb-table gather only when the previous half-round's tile is not the wave's previous tile
+  // (otherwise a read of the tile's own first cells: lines this wave loads anyway, value unused)
   const Canon cs = canon_state(lane >> 2, c.hr);
-  const uint64_t r = c.off + cs.row(lane & 3u);
-  v.d = adv[(uint64_t)cs.dcol * total_rows + r];
-  v.sp = adv[(uint64_t)cs.scol * total_rows + r];
+  const uint64_t r = gath ? c.off + cs.row(lane & 3u) : c.row0 + 4 * lq;
+  v.d = adv[(uint64_t)(gath ? cs.dcol : (uint32_t)A1) * total_rows + r];
+  v.sp = adv[(uint64_t)(gath ? cs.scol : (uint32_t)A2) * total_rows + r];
   const uint32_t j = Sg[16 * ((c.hr >> 1) % 10) + 2 * (mg + 4 * (c.hr & 1u)) + mwh];
   v.mc = adv[(uint64_t)A1 * total_rows + c.off + 32 + 4 * j + mk];
   return v;
@@ -2109,6 +2136,18 @@ __device__ __forceinline__ EvCells ev_load(const hr2::HCtx& c, uint32_t lane, ui
 #ifndef B2F_EVAL_WAVES_HR
 #define B2F_EVAL_WAVES_HR 3  // waves per SIMD of the eval fast pass (the prefetched tile's registers)
 #endif
+#ifndef B2F_EVAL_HR_BAND
+#define B2F_EVAL_HR_BAND 24  // consecutive half-round tiles per wave visit (1: one tile, every limb table gathered)
+#endif
+constexpr uint32_t EV_BAND = B2F_EVAL_HR_BAND;
+// LDS byte addresses (dense | spread << 16) of limb k = lane % 4 of state word lane / 4 in the staged
+// PREVIOUS half-round tile, for that tile's parity `par` (0: column G's, 1: diagonal G's): where the
+// limb table of a tile comes from when the wave has just checked the instance's previous half-round
+__device__ __forceinline__ uint32_t carry_addr(uint32_t lane, uint32_t Sb, uint32_t par) {
+  const Canon cs = canon_state(lane >> 2, 1 + par);  // rows of half-round par of round 0
+  const uint32_t ri = cs.row(lane & 3u) - INIT_ROWS - 208 * par;
+  return (Sb + 4 * (cs.dcol * STR + ri)) | ((Sb + 4 * (cs.scol * STR + ri)) << 16);
+}
 template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES, B2F_EVAL_WAVES_HR)
 eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fixed, uint32_t n,
@@ -2119,6 +2158,9 @@ eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fi
   const int tid = threadIdx.x;
   const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
   if (tid < 40) L[H_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
+#ifdef B2F_HR_SPT
+  reinterpret_cast<uint16_t*>(L + H_SPT)[tid & 255] = (uint16_t)spread16((uint32_t)tid & 255u);
+#endif
   __syncthreads();
   if (*status) return;  // a rejected row map: the eval kernel reports it
   const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + H_SG);
@@ -2130,22 +2172,35 @@ eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fi
   const uint64_t used_rows = off[n];
   const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
   const uint64_t W = (uint64_t)gridDim.x * WAVES;
-  uint64_t t = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
+  // bands of EV_BAND consecutive tiles per wave visit, dealt like single tiles (first_tile)
+  uint64_t b = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
+  uint64_t t = b * EV_BAND;
+  uint32_t j = 0;
+  const uint32_t cA0 = carry_addr(lane, lds_byte(S), 0), cA1 = carry_addr(lane, lds_byte(S), 1);
   auto raw_desc = [&](uint64_t tt) -> uint4 { return desc[tt].v; };
   // per tile: its cells (lane = quad), its limb-table entry (the canonical dense / spread cell of
-  // state word lane / 4, limb lane % 4, as the half-round starts) and its message-copy source
-  // (message word SIGMA[..] limb, a_1 of its INW block), loaded one tile ahead
-#ifndef B2F_EVAL_NOPF
+  // state word lane / 4, limb lane % 4, as the half-round starts: gathered at a band's first tile
+  // and at an instance's first half-round, otherwise read from the previous tile's staging) and its
+  // message-copy source (message word SIGMA[..] limb, a_1 of its INW block), loaded one tile ahead
   HCtx c = hctx(raw_desc(t < n_hr ? t : 0));
-  EvCells cur = ev_load(c, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg);
-  for (; t < n_hr; t += W) {
-    const HCtx cn = hctx(raw_desc(t + W < n_hr ? t + W : 0));
-    const EvCells nxt = ev_load(cn, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg);  // in flight
-#else
-  for (; t < n_hr; t += W) {
-    const HCtx c = hctx(raw_desc(t));
-    const EvCells cur = ev_load(c, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg);
-#endif
+  EvCells cur = ev_load(c, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg, true);
+  while (t < n_hr) {
+    uint64_t tn = t + 1, bn = b;
+    uint32_t jn = j + 1;
+    if (jn == EV_BAND || tn >= n_hr) {
+      bn = b + W;
+      tn = bn * EV_BAND;
+      jn = 0;
+    }
+    const HCtx cn = hctx(raw_desc(tn < n_hr ? tn : 0));
+    const EvCells nxt = ev_load(cn, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg, jn == 0 || cn.hr == 0);
+    uint32_t ltd = cur.d, lts = cur.sp;
+    if (j != 0 && c.hr != 0) {  // the staging holds half-round hr - 1 of this instance
+      const uint32_t a = ((c.hr - 1) & 1u) ? cA1 : cA0;
+      ltd = ld32(a & 0xffffu);
+      lts = ld32(a >> 16);
+    }
+    asm volatile("" ::: "memory");  // read before the tile's cells overwrite the staging
     if (qlane) {
       uint4* q = reinterpret_cast<uint4*>(S + 4 * lane);
       q[0 * STR / 4] = cur.c0;
@@ -2160,8 +2215,8 @@ eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fi
       q[9 * STR / 4] = cur.c9;
       q[10 * STR / 4] = cur.c10;
     }
-    S[H_LT + lane] = cur.d;
-    S[H_LT + 64 + lane] = cur.sp;
+    S[H_LT + lane] = ltd;
+    S[H_LT + 64 + lane] = lts;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     const uint32_t mc = cur.mc;
@@ -2169,10 +2224,11 @@ eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fi
     if (__builtin_amdgcn_ballot_w64(acc != 0) && lane == 0) *dirty = 1u;
     asm volatile("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-#ifndef B2F_EVAL_NOPF
     c = cn;
     cur = nxt;
-#endif
+    t = tn;
+    j = jn;
+    b = bn;
   }
 }
 

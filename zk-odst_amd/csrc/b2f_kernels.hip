@@ -738,6 +738,7 @@ struct b2f_ctx {
   std::vector<int> kinds;        // kernel kind of pair i
   int cu_count;
   unsigned long long* d_clock;  // 32 u64: EVAL_CLOCK phase totals (diagnostics)
+  const uint32_t* d_eval_gate;  // the last eval's fast-pass word (0: the fast pass found the trace clean)
   uint64_t inj_row;    // b2f_debug_inject (UINT64_MAX: off)
   uint32_t inj_col, inj_mask;
   void* d_lk;          // lookup-column scratch (b2f_lookup.hip carve)
@@ -1176,6 +1177,18 @@ B2F_API int b2f_debug_clock(b2f_ctx* ctx, uint64_t* out) {
   return B2F_OK;
 }
 
+B2F_API int b2f_debug_eval_path(b2f_ctx* ctx, uint32_t* out) {
+  if (!ctx || !out) return B2F_ERR_ARG;
+  *out = 2;
+  if (!ctx->d_eval_gate) return B2F_OK;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipDeviceSynchronize());
+  uint32_t w = 0;
+  HIPCHK(ctx, hipMemcpy(&w, ctx->d_eval_gate, sizeof w, hipMemcpyDeviceToHost));
+  *out = w ? 1u : 0u;
+  return B2F_OK;
+}
+
 B2F_API int b2f_debug_inject(b2f_ctx* ctx, uint64_t row, uint32_t col, uint32_t mask) {
   if (!ctx) return B2F_ERR_ARG;
   if (row != UINT64_MAX && col > B2F_NUM_ADVICE)
@@ -1229,6 +1242,7 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
     HIPCHK(ctx, launch_eval_fast(d_advice, d_fixed, d_offsets, (uint32_t)n, total_rows, ctx->d_fz,
                                  fused_instance_tiles(total_rows, n), ctx->d_status + 1, ctx->cu_count, s, &gate,
                                  fmode));
+  ctx->d_eval_gate = gate;
   if (fmode != 27) {  // diagnostics: the fast pass alone
     timed_end(ctx, tk, s);
     return B2F_OK;
