@@ -124,6 +124,8 @@ def load(diag=False, path=None):
     _share_hip_runtime_with_torch()
     lib = ctypes.CDLL(path)
     for name, res, args in SIGNATURES:
+        if path != LIB_PATH and path != DIAG_LIB_PATH and not hasattr(lib, name):
+            continue  # an older A/B build (tools/) without a later entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
