@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--eval", action="store_true", help="also time each variant's eval kernel")
+    ap.add_argument("--fill", action="store_true", help="also time each variant's split fill")
     args = ap.parse_args()
     import torch
 
@@ -30,8 +31,13 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     prod = b2f.Engine(0)
     engines = [("product", prod)]
-    for p in [v for v in args.libs.split(",") if v]:
-        engines.append((os.path.basename(p)[6:-3], b2f.Engine(0, lib_path=os.path.join(ROOT, p))))
+    envs = {}
+    for spec in [v for v in args.libs.split(",") if v]:
+        # path[@K=V[;K=V]]: environment set around that variant's fused calls (diag builds)
+        p, _, env = spec.partition("@")
+        name = os.path.basename(p)[6:-3] + ("@" + env if env else "")
+        engines.append((name, b2f.Engine(0, lib_path=os.path.join(ROOT, p))))
+        envs[name] = dict(kv.split("=", 1) for kv in env.split(";") if kv)
     nbytes = batch.used_rows * 44
     batch.fill(prod, s)
     batch.evaluate(prod, s)
@@ -45,6 +51,14 @@ def main():
         kt = prod.kernel_times()
         res.setdefault("split(fill+eval)", []).append(kt["fill"][0] + kt["eval"][0] + kt["record"][0])
         for name, eng in engines:
+            for k, v in envs.get(name, {}).items():
+                os.environ[k] = v
+            if args.fill:
+                eng.set_timing(True)
+                batch.fill(eng, s)
+                kt = eng.kernel_times()
+                res.setdefault("%s/fill" % name, []).append(kt["fill"][0])
+                eng.sync(s)
             if args.eval:
                 eng.set_timing(True)
                 batch.evaluate(eng, s)
@@ -58,6 +72,8 @@ def main():
                 kt = eng.kernel_times()
                 res.setdefault("%s/fused%s" % (name, m), []).append(kt["fill_eval"][0] + kt["record"][0])
                 eng.sync(s)
+            for k in envs.get(name, {}):
+                os.environ.pop(k, None)
         os.environ.pop("B2F_DIAG_FUSED", None)
     for k, v in res.items():
         best = min(v)

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/b2f.h"
 #include "b2f_common.h"
@@ -301,6 +302,9 @@ __device__ __forceinline__ void producer_words(uint64_t* prod, const Ops& P, uin
 // MODE (diagnostics; the product launches FZ_FULL, with FZ_INJECT only under the test hook)
 #ifndef B2F_FUSED_WAVES
 #define B2F_FUSED_WAVES 4  // waves per SIMD the fused kernel is compiled for (VGPR budget)
+#endif
+#ifndef B2F_FUSED_HR_PER_CU
+#define B2F_FUSED_HR_PER_CU 2  // half-round launch: workgroups per CU (at most what fits)
 #endif
 enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16, FZ_FULL = 27,
        FZ_CLOCK = 128 };  // per-phase s_memtime totals per wave slot (diagnostics, b2f_debug_clock)
@@ -2394,10 +2398,19 @@ hipError_t launch_eval_fast(const uint32_t* d_adv, const uint32_t* d_fixed, cons
   const uint64_t edge_tiles = (uint64_t)n + ((total_rows / 4) + PAD_Q - 1) / PAD_Q;
   const uint64_t edge_wgs = (edge_tiles + WAVES - 1) / WAVES;
   const uint32_t grid_e = (uint32_t)(edge_wgs < (uint64_t)cu_count * per_cu[1] ? edge_wgs : (uint64_t)cu_count * per_cu[1]);
+  // 2 workgroups per CU: like the fused half-round launch, a narrower front of tiles in flight
+  // reads faster than every workgroup that fits (same-process A/B 9.77 vs 9.87 ms)
+  int ev_per_cu = per_cu[0] < 2 ? per_cu[0] : 2;
+#ifdef B2F_DIAG  // diagnostics: workgroups per CU of the half-round pass
+  if (const char* v = getenv("B2F_EVAL_PERCU")) {
+    const int k = atoi(v);
+    if (k >= 1 && k <= per_cu[0]) ev_per_cu = k;
+  }
+#endif
   switch (mode) {
 #define B2F_EVFAST(M)                                                                              \
   case M:                                                                                          \
-    hipLaunchKernelGGL(eval_hr_kernel<M>, dim3(cu_count * per_cu[0]), dim3(FW * WAVES), 0, s, d_adv, d_fixed, n, \
+    hipLaunchKernelGGL(eval_hr_kernel<M>, dim3(cu_count * ev_per_cu), dim3(FW * WAVES), 0, s, d_adv, d_fixed, n, \
                        d_off, total_rows, desc, dirty, d_status);                                  \
     hipLaunchKernelGGL(eval_edge_kernel<M>, dim3(grid_e), dim3(FW * WAVES), 0, s, d_adv, d_fixed, n, d_off, \
                        total_rows, dirty, d_status);                                               \
@@ -2461,8 +2474,24 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   const uint64_t edge_tiles = (uint64_t)n + ((total_rows / 4) + PAD_Q - 1) / PAD_Q;
 #endif
   const uint64_t edge_wgs = (edge_tiles + WAVES - 1) / WAVES;
-  const uint32_t grid = (uint32_t)(cu_count * per_cu[0]);
-  const uint32_t grid_e = (uint32_t)(edge_wgs < (uint64_t)cu_count * per_cu[1] ? edge_wgs : (uint64_t)cu_count * per_cu[1]);
+  // Fewer half-round workgroups than fit: 2 per CU (8 waves) write the trace faster than 4 per CU
+  // (16 waves) -- a narrower front of tiles in flight (same-process A/B 11.78 vs 12.54 ms)
+  int hr_per_cu = per_cu[0] < B2F_FUSED_HR_PER_CU ? per_cu[0] : B2F_FUSED_HR_PER_CU;
+#ifdef B2F_DIAG  // diagnostics: workgroups per CU of the half-round launch
+  if (const char* v = getenv("B2F_FUSED_PERCU")) {
+    const int k = atoi(v);
+    if (k >= 1 && k <= per_cu[0]) hr_per_cu = k;
+  }
+#endif
+  const uint32_t grid = (uint32_t)(cu_count * hr_per_cu);
+  int e_per_cu = per_cu[1];
+#ifdef B2F_DIAG  // diagnostics: workgroups per CU of the edge launch
+  if (const char* v = getenv("B2F_EDGE_PERCU")) {
+    const int k = atoi(v);
+    if (k >= 1 && k <= per_cu[1]) e_per_cu = k;
+  }
+#endif
+  const uint32_t grid_e = (uint32_t)(edge_wgs < (uint64_t)cu_count * e_per_cu ? edge_wgs : (uint64_t)cu_count * e_per_cu);
   switch (mode) {
 #define B2F_FUSED(M)                                                                               \
   case M:                                                                                          \
