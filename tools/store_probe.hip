@@ -82,6 +82,27 @@ __global__ void __launch_bounds__(256) wave_rr_store(uint32_t* adv, uint64_t tot
   }
 }
 
+// wave_rr_store with the columns `stride` words apart (stride >= total_rows): column padding
+template <int STEP>
+__global__ void __launch_bounds__(256) wave_rr_pad(uint32_t* adv, uint64_t total_rows, uint64_t stride, int work) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  const uint64_t total_quads = total_rows >> 2;
+  const uint64_t n_t = (total_quads + STEP - 1) / STEP;
+  uint32_t h = lane;
+  for (uint64_t t = wid; t < n_t; t += nw) {
+    const uint64_t q = t * STEP + lane;
+    h ^= (uint32_t)q;
+    for (int k = 0; k < work; k++) h = (h ^ (h >> 7)) * 0x9E3779B1u + (uint32_t)k;
+    if (lane < STEP && q < total_quads) {
+#pragma unroll
+      for (int c = 0; c < 11; c++)
+        __builtin_nontemporal_store(u32x4{h + c, h ^ c, h * c, h - c},
+                                    reinterpret_cast<u32x4*>(adv + (uint64_t)c * stride + 4 * q));
+    }
+  }
+}
+
 // the same order with per-tile work in front of the stores: `work` rounds of a dependent
 // integer hash per lane (~4 VALU each), optionally staged through LDS and read back (STAGE), and
 // stored with raw buffer stores (BUF) instead of global stores
@@ -338,6 +359,22 @@ int main(int argc, char** argv) {
       SPEC(7, 1, 2)
       SPEC(4, 3, 1)
 #undef SPEC
+    }
+    return 0;
+  }
+  if (argc > 2 && argv[2][0] == 'p') {  // column stride padding (words), 2 workgroups per CU
+    CHK(hipFree(adv));
+    const uint64_t maxpad = 1ull << 20;
+    CHK(hipMalloc(&adv, (total + maxpad) * 11 * 4));
+    for (int work : {0, 120}) {
+      for (uint64_t pad : {0ull, 64ull, 256ull, 1024ull, 4096ull, 16384ull, 65536ull, 3ull * 65536ull + 1024ull,
+                           1ull << 20}) {
+        for (int w : {2, 4}) {
+          char nm[96];
+          snprintf(nm, sizeof nm, "pad%llu_work%d_%dwg", (unsigned long long)pad, work, w);
+          run(nm, [&] { hipLaunchKernelGGL(wave_rr_pad<52>, dim3(cus * w), dim3(256), 0, 0, adv, total, total + pad, work); });
+        }
+      }
     }
     return 0;
   }

@@ -362,6 +362,8 @@ __device__ __forceinline__ void store_staged(const uint32_t* S, uint32_t lane, u
   if (!(MODE & FZ_STORE)) return;
 
   const uint32_t l = lane < nq ? lane : 0;
+  // one column at a time (read, store): measured faster than reading 4, 6 or all 11 columns
+  // ahead of their stores, whose burstier store stream wrote slower (same-process A/B)
 #pragma unroll
   for (int col = 0; col < NSTAGE; col++)
     tile_store((col < 10 ? adv + (uint64_t)col * total_rows : fixed) + row0, nq, lane,
