@@ -8,13 +8,15 @@
 // is a table row, so the sort is a counting sort over the 2^16 table rows in the order of
 // their compressed values:
 //   table pass (once per theta): T[x] = theta^2 tag(x) + theta x + spread(x) for x < 2^16,
-//     sorted by canonical value (four stable LSD passes of a 64-bit radix sort), giving the
-//     rank order x_of_rank[r] and Ts[r] = T[x_of_rank[r]];
+//     sorted by canonical value (one radix sort by the top 64-bit limb, ties -- about 2^-33
+//     likely -- ordered by the lower limbs), giving the rank order x_of_rank[r] and
+//     Ts[r] = T[x_of_rank[r]];
 //   count:   histogram of the dense cell (a_1) over the circuit's rows (LDS-privatised, four
 //            workgroups per circuit, a quarter of the bins each), with the row check (tag,
 //            dense, spread) in table (first failing row reported);
 //   scan:    in rank order, run starts pos[r] (exclusive prefix of counts), D[r] (runs up to
-//            and including r) and LP[r] (exclusive prefix of leftover table multiplicities);
+//            and including r) and LP[r] (exclusive prefix of leftover table multiplicities), 16
+//            workgroups per circuit (part totals, then each part's scan);
 //   permute: row p of A' is Ts[r] for the run r holding p (binary search of pos); a run
 //            start gets S'[p] = Ts[r]; the j-th repeated row gets leftover item L - 1 - j
 //            (halo2 hands leftovers out in ascending order, each to the last open repeated
@@ -81,11 +83,34 @@ __global__ __launch_bounds__(256) void lk_table_kernel(Chal ch, Fe* __restrict__
   perm[x] = x;
 }
 
-__global__ __launch_bounds__(256) void lk_gather_key_kernel(const uint64_t* __restrict__ limb,
-                                                            const uint32_t* __restrict__ perm,
-                                                            uint64_t* __restrict__ out) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  out[i] = limb[perm[i]];
+// After one radix sort by the top 64-bit limb of the canonical value: a run of equal top limbs
+// (about 2^-33 likely for 2^16 uniform values, but possible) is put in order by the three lower
+// limbs, in place, by the thread at the run's start (insertion sort). The rank order is then the
+// order of the full 256-bit values, as four LSD passes over the limbs would give.
+__global__ __launch_bounds__(256) void lk_tie_fix_kernel(const uint64_t* __restrict__ key,
+                                                         const uint64_t* __restrict__ top,
+                                                         uint32_t* __restrict__ perm) {
+  const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+  const uint64_t k = top[r];
+  if ((r > 0 && top[r - 1] == k) || r + 1 >= TROWS || top[r + 1] != k) return;
+  uint32_t e = r + 1;
+  while (e < TROWS && top[e] == k) e++;
+  auto less = [&](uint32_t a, uint32_t b) {
+    for (int l = 2; l >= 0; l--) {
+      const uint64_t x = key[(uint64_t)l * TROWS + a], y = key[(uint64_t)l * TROWS + b];
+      if (x != y) return x < y;
+    }
+    return false;
+  };
+  for (uint32_t i = r + 1; i < e; i++) {
+    const uint32_t v = perm[i];
+    uint32_t j = i;
+    while (j > r && less(v, perm[j - 1])) {
+      perm[j] = perm[j - 1];
+      j--;
+    }
+    perm[j] = v;
+  }
 }
 
 __global__ __launch_bounds__(256) void lk_rank_kernel(const Fe* __restrict__ Tx,
@@ -145,74 +170,129 @@ __global__ __launch_bounds__(CNT_THREADS) void lk_count_kernel(
   for (uint32_t i = t; i < (uint32_t)CNT_BINS; i += CNT_THREADS) cnt[i] = bins[i];
 }
 
-// one workgroup per circuit: 1024 threads x 64 ranks
+// The rank-order scan of a circuit's counts, split over SC_PARTS workgroups per circuit of
+// SC_THREADS threads x SC_PER consecutive ranks (the counts gathered into registers once per
+// pass): lk_scan_sums writes each part's totals, lk_scan_write adds the totals of the parts
+// before it and scans its own ranks. (One 1,024-thread workgroup per circuit holding 64 ranks per
+// thread kept the gathered counts in scratch and used 64 of the 256 CUs.)
 constexpr int SAMPLE = TROWS / 16;  // every 16th pos / lp entry, for the permute searches
-__global__ __launch_bounds__(1024) void lk_scan_kernel(const uint32_t* __restrict__ perm,
-                                                       const uint32_t* __restrict__ count,
-                                                       uint64_t usable, uint32_t* __restrict__ pos,
-                                                       uint32_t* __restrict__ dcnt,
-                                                       uint32_t* __restrict__ lp,
-                                                       uint32_t* __restrict__ samp) {
-  const uint32_t c = blockIdx.x, t = threadIdx.x;
-  const uint32_t* cnt = count + (uint64_t)c * TROWS;
-  // this thread's 64 consecutive ranks: the rank order read as 16-byte vectors, the counts
-  // gathered once into registers (and the one rank holding x = 0 remembered)
-  uint32_t nv[64];
-  int iz = -1;
-  const uint4* pv = reinterpret_cast<const uint4*>(perm + t * 64);
+constexpr int SC_PARTS = 16, SC_THREADS = 256, SC_PER = TROWS / (SC_PARTS * SC_THREADS);
+static_assert(SC_PER == 16, "one search sample per thread");
+
+// the counts of this thread's SC_PER ranks (rank order read as 16-byte vectors), the index of the
+// rank holding table row 0 (-1: none), and the three sums: rows, runs, leftover table multiplicity
+struct RankRun {
+  uint32_t nv[SC_PER];
+  int iz;
+  uint32_t sc, sd, sl;
+};
+__device__ __forceinline__ RankRun rank_run(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ cnt,
+                                            uint32_t r0, uint32_t mult0) {
+  RankRun R;
+  R.iz = -1;
+  const uint4* pv = reinterpret_cast<const uint4*>(perm + r0);
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
+  for (int i = 0; i < SC_PER / 4; i++) {
     const uint4 x = pv[i];
-    nv[4 * i] = cnt[x.x];
-    nv[4 * i + 1] = cnt[x.y];
-    nv[4 * i + 2] = cnt[x.z];
-    nv[4 * i + 3] = cnt[x.w];
-    iz = x.x == 0 ? 4 * i : x.y == 0 ? 4 * i + 1 : x.z == 0 ? 4 * i + 2 : x.w == 0 ? 4 * i + 3 : iz;
+    R.nv[4 * i] = cnt[x.x];
+    R.nv[4 * i + 1] = cnt[x.y];
+    R.nv[4 * i + 2] = cnt[x.z];
+    R.nv[4 * i + 3] = cnt[x.w];
+    R.iz = x.x == 0 ? 4 * i : x.y == 0 ? 4 * i + 1 : x.z == 0 ? 4 * i + 2 : x.w == 0 ? 4 * i + 3 : R.iz;
   }
+  R.sc = R.sd = R.sl = 0;
+#pragma unroll
+  for (int i = 0; i < SC_PER; i++) {
+    const uint32_t n = R.nv[i];
+    R.sc += n;
+    R.sd += n ? 1u : 0u;
+    R.sl += (i == R.iz ? mult0 : 1u) - (n ? 1u : 0u);
+  }
+  return R;
+}
+
+__global__ __launch_bounds__(SC_THREADS) void lk_scan_sums(const uint32_t* __restrict__ perm,
+                                                           const uint32_t* __restrict__ count,
+                                                           uint64_t usable, uint32_t* __restrict__ part) {
+  const uint32_t pt = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
   const uint32_t mult0 = (uint32_t)(usable - TROWS + 1);  // table row 0 fills the rest
-  uint32_t sc = 0, sd = 0, sl = 0;
-#pragma unroll
-  for (int i = 0; i < 64; i++) {
-    const uint32_t n = nv[i];
-    sc += n;
-    sd += n ? 1u : 0u;
-    sl += (i == iz ? mult0 : 1u) - (n ? 1u : 0u);
-  }
-  __shared__ uint32_t s[3][1024];
-  s[0][t] = sc; s[1][t] = sd; s[2][t] = sl;
+  const RankRun R = rank_run(perm, count + (uint64_t)c * TROWS, (pt * SC_THREADS + t) * SC_PER, mult0);
+  __shared__ uint32_t s[3][SC_THREADS];
+  s[0][t] = R.sc;
+  s[1][t] = R.sd;
+  s[2][t] = R.sl;
   __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele
-    uint32_t a = 0, b = 0, d = 0;
-    if (t >= (uint32_t)off) { a = s[0][t - off]; b = s[1][t - off]; d = s[2][t - off]; }
-    __syncthreads();
-    s[0][t] += a; s[1][t] += b; s[2][t] += d;
+  for (uint32_t w = SC_THREADS / 2; w > 0; w >>= 1) {
+    if (t < w) {
+      s[0][t] += s[0][t + w];
+      s[1][t] += s[1][t + w];
+      s[2][t] += s[2][t + w];
+    }
     __syncthreads();
   }
-  uint32_t ec = s[0][t] - sc, ed = s[1][t] - sd, el = s[2][t] - sl;  // exclusive
-  uint4* P4 = reinterpret_cast<uint4*>(pos + (uint64_t)c * TROWS + t * 64);
-  uint4* D4 = reinterpret_cast<uint4*>(dcnt + (uint64_t)c * TROWS + t * 64);
-  uint4* L4 = reinterpret_cast<uint4*>(lp + (uint64_t)c * TROWS + t * 64);
+  if (t < 3) part[((uint64_t)c * SC_PARTS + pt) * 3 + t] = s[t][0];
+}
+
+__global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __restrict__ perm,
+                                                            const uint32_t* __restrict__ count,
+                                                            uint64_t usable, const uint32_t* __restrict__ part,
+                                                            uint32_t* __restrict__ pos, uint32_t* __restrict__ dcnt,
+                                                            uint32_t* __restrict__ lp, uint32_t* __restrict__ samp) {
+  const uint32_t pt = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
+  const uint32_t mult0 = (uint32_t)(usable - TROWS + 1);
+  const uint32_t r0 = (pt * SC_THREADS + t) * SC_PER;
+  const RankRun R = rank_run(perm, count + (uint64_t)c * TROWS, r0, mult0);
+  uint32_t bc = 0, bd = 0, bl = 0;  // totals of the parts before this one
+  for (uint32_t q = 0; q < pt; q++) {
+    const uint32_t* pq = part + ((uint64_t)c * SC_PARTS + q) * 3;
+    bc += pq[0];
+    bd += pq[1];
+    bl += pq[2];
+  }
+  __shared__ uint32_t s[3][SC_THREADS];
+  s[0][t] = R.sc;
+  s[1][t] = R.sd;
+  s[2][t] = R.sl;
+  __syncthreads();
+  uint32_t ic = R.sc, id = R.sd, il = R.sl;
+  for (uint32_t off = 1; off < SC_THREADS; off <<= 1) {  // inclusive Hillis-Steele
+    uint32_t a = 0, b = 0, d = 0;
+    if (t >= off) {
+      a = s[0][t - off];
+      b = s[1][t - off];
+      d = s[2][t - off];
+    }
+    __syncthreads();
+    ic += a;
+    id += b;
+    il += d;
+    s[0][t] = ic;
+    s[1][t] = id;
+    s[2][t] = il;
+    __syncthreads();
+  }
+  uint32_t ec = bc + ic - R.sc, ed = bd + id - R.sd, el = bl + il - R.sl;  // exclusive
+  uint4* P4 = reinterpret_cast<uint4*>(pos + (uint64_t)c * TROWS + r0);
+  uint4* D4 = reinterpret_cast<uint4*>(dcnt + (uint64_t)c * TROWS + r0);
+  uint4* L4 = reinterpret_cast<uint4*>(lp + (uint64_t)c * TROWS + r0);
+  samp[(uint64_t)c * 2 * SAMPLE + (r0 >> 4)] = ec;  // r0 is a multiple of 16: a search sample
+  samp[(uint64_t)c * 2 * SAMPLE + SAMPLE + (r0 >> 4)] = el;
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
+  for (int i = 0; i < SC_PER / 4; i++) {
     uint32_t pq[4], dq[4], lq[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const uint32_t n = nv[4 * i + j];
+      const uint32_t n = R.nv[4 * i + j];
       pq[j] = ec;
       ed += n ? 1u : 0u;
       dq[j] = ed;
       lq[j] = el;
       ec += n;
-      el += (4 * i + j == iz ? mult0 : 1u) - (n ? 1u : 0u);
+      el += (4 * i + j == R.iz ? mult0 : 1u) - (n ? 1u : 0u);
     }
     P4[i] = make_uint4(pq[0], pq[1], pq[2], pq[3]);
     D4[i] = make_uint4(dq[0], dq[1], dq[2], dq[3]);
     L4[i] = make_uint4(lq[0], lq[1], lq[2], lq[3]);
-    if ((i & 3) == 0) {  // rank t * 64 + 4 i is a multiple of 16: a search sample
-      const uint32_t r = t * 64 + 4 * i;
-      samp[(uint64_t)c * 2 * SAMPLE + (r >> 4)] = pq[0];
-      samp[(uint64_t)c * 2 * SAMPLE + SAMPLE + (r >> 4)] = lq[0];
-    }
   }
 }
 
@@ -297,7 +377,6 @@ struct Carve {
   Fe* Tx;
   Fe* Ts;
   uint64_t* key;   // 4 x TROWS canonical limbs
-  uint64_t* kin;   // TROWS
   uint64_t* kout;  // TROWS
   uint32_t* perm;  // TROWS
   uint32_t* perm2;
@@ -306,6 +385,7 @@ struct Carve {
   uint32_t* dcnt;
   uint32_t* lp;
   uint32_t* samp;  // group x 2 x SAMPLE
+  uint32_t* part;  // group x SC_PARTS x 3 (rank-scan part totals)
   Fe* num;  // group x usable
   Fe* den;
   Fe* zs;  // group x gp::scratch_elems
@@ -333,7 +413,6 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.Tx = (Fe*)take(sizeof(Fe) * TROWS);
   k.Ts = (Fe*)take(sizeof(Fe) * TROWS);
   k.key = (uint64_t*)take(8ull * 4 * TROWS);
-  k.kin = (uint64_t*)take(8ull * TROWS);
   k.kout = (uint64_t*)take(8ull * TROWS);
   k.perm = (uint32_t*)take(4ull * TROWS);
   k.perm2 = (uint32_t*)take(4ull * TROWS);
@@ -342,6 +421,7 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.dcnt = (uint32_t*)take(4ull * TROWS * group);
   k.lp = (uint32_t*)take(4ull * TROWS * group);
   k.samp = (uint32_t*)take(8ull * SAMPLE * group);
+  k.part = (uint32_t*)take(12ull * SC_PARTS * group);
   k.num = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);  // chunk-interleaved (b2f_gprod.h)
   k.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);
   k.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * group);
@@ -359,20 +439,16 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   Carve k = carve(scratch, group, usable_rows);
   const dim3 tb(TROWS / 256);
   hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm);
-  // stable LSD over the four 64-bit limbs of the canonical value
-  uint32_t* pa = k.perm;
-  uint32_t* pb = k.perm2;
-  for (int limb = 0; limb < 4; limb++) {
-    hipLaunchKernelGGL(lk_gather_key_kernel, tb, dim3(256), 0, s, k.key + (uint64_t)limb * TROWS,
-                       pa, k.kin);
+  // one radix sort by the top limb of the canonical value (< 2^63: both moduli are < 2^255),
+  // then ties in the top limb ordered by the lower limbs
+  uint32_t* pa = k.perm2;
+  {
     size_t bytes = k.sort_bytes;
-    hipError_t e = rocprim::radix_sort_pairs(k.sort_tmp, bytes, k.kin, k.kout, pa, pb,
-                                             (size_t)TROWS, 0, limb == 3 ? 63 : 64, s);
+    hipError_t e = rocprim::radix_sort_pairs(k.sort_tmp, bytes, k.key + 3ull * TROWS, k.kout, k.perm, pa,
+                                             (size_t)TROWS, 0, 63, s);
     if (e != hipSuccess) return e;
-    uint32_t* t = pa;
-    pa = pb;
-    pb = t;
   }
+  hipLaunchKernelGGL(lk_tie_fix_kernel, tb, dim3(256), 0, s, k.key, k.kout, pa);
   hipLaunchKernelGGL(lk_rank_kernel, tb, dim3(256), 0, s, k.Tx, pa, k.Ts);
   hipError_t e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s);
   if (e != hipSuccess) return e;
@@ -380,8 +456,9 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
     const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
     hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
                        total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
-    hipLaunchKernelGGL(lk_scan_kernel, dim3(g), dim3(1024), 0, s, pa, k.count, usable_rows, k.pos,
-                       k.dcnt, k.lp, k.samp);
+    hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
+    hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
+                       k.part, k.pos, k.dcnt, k.lp, k.samp);
     // permute: ~4096 rows per workgroup (the LDS samples are staged once per workgroup)
     const uint32_t px = (uint32_t)((usable_rows + 4095) / 4096);
     hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
