@@ -103,7 +103,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void gp_scan(uint64_t nq, Fe* __restr
   }
   const Fe s = seed ? seed[c] : field::one<F>();
   if (t == 0) {
+#ifdef B2F_INV_EUCLID  // diagnostics: the plain binary extended Euclid
     dinv = field::inv<F>(sd[0]);  // sd[0] = D
+#else
+    dinv = field::inv_kaliski<F>(sd[0]);  // sd[0] = D
+#endif
     if (closing) closing[c] = field::mul<F>(field::mul<F>(s, sn[SCAN_THREADS - 1]), dinv);
   }
   __syncthreads();
