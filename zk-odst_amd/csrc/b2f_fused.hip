@@ -315,9 +315,10 @@ enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16,
 // the compiler's vmcnt bookkeeping exact: a branch that might skip a tile's stores would make
 // every later wait for an older load wait for those stores too (vmcnt is in order).
 #ifndef B2F_BUF_POLICY
-#define B2F_BUF_POLICY 2
+#define B2F_BUF_POLICY 0  // default (write-back) policy: at 2 workgroups per CU 2.9 % faster than
+                          // non-temporal (2; it had been neutral at 4 per CU), sc0 (1) in between
 #endif
-constexpr int BUF_NT = B2F_BUF_POLICY;  // gfx94x/gfx950 cache-policy bit 1: non-temporal
+constexpr int BUF_NT = B2F_BUF_POLICY;  // gfx94x/gfx950 cache-policy bits: 1 sc0, 2 non-temporal
 __device__ __forceinline__ void tile_store(uint32_t* base, uint32_t nq, uint32_t lane, uint4 v) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const i32x4 rsrc = {(int32_t)(uint32_t)a, (int32_t)(uint32_t)(a >> 32), (int32_t)(nq * 16u), 0x00020000};
