@@ -72,14 +72,17 @@ __global__ __launch_bounds__(256) void gp_chunk(uint64_t usable, Fe* __restrict_
 // D_end(q)^-1 = D^-1 prod_{q' > q} zd[q']. Per-thread runs of chunks, Hillis-Steele scans
 // of the run products in LDS (a prefix for num, a suffix for den), one inversion.
 // seed: Montgomery elements per product (nullptr: 1); closing (nullable) <- seed N / D.
-template <class F>
-__global__ __launch_bounds__(SCAN_THREADS) void gp_scan(uint64_t nq, Fe* __restrict__ zn,
-                                                        const Fe* __restrict__ zd,
-                                                        const Fe* __restrict__ seed,
-                                                        Fe* __restrict__ closing) {
+// T threads: SCAN_THREADS, or one wave when there are at most 64 chunk totals (the block totals
+// of the three-level path) -- a 1,024-thread scan of 8 values spent ten levels of products on
+// every thread.
+template <class F, int T = SCAN_THREADS>
+__global__ __launch_bounds__(T) void gp_scan(uint64_t nq, Fe* __restrict__ zn,
+                                             const Fe* __restrict__ zd,
+                                             const Fe* __restrict__ seed,
+                                             Fe* __restrict__ closing) {
   const uint32_t c = blockIdx.x, t = threadIdx.x;
-  const uint64_t per = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
-  __shared__ Fe sn[SCAN_THREADS], sd[SCAN_THREADS];
+  const uint64_t per = (nq + T - 1) / T;
+  __shared__ Fe sn[T], sd[T];
   __shared__ Fe dinv;
   Fe* an = zn + (uint64_t)c * nq;
   const Fe* ad = zd + (uint64_t)c * nq;
@@ -92,10 +95,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void gp_scan(uint64_t nq, Fe* __restr
   sn[t] = pn;
   sd[t] = pd;
   __syncthreads();
-  for (int off = 1; off < SCAN_THREADS; off <<= 1) {  // inclusive: prefix of sn, suffix of sd
+  for (int off = 1; off < T; off <<= 1) {  // inclusive: prefix of sn, suffix of sd
     Fe xn = pn, xd = pd;
     if (t >= (uint32_t)off) xn = field::mul<F>(sn[t - off], pn);
-    if (t + off < (uint32_t)SCAN_THREADS) xd = field::mul<F>(pd, sd[t + off]);
+    if (t + off < (uint32_t)T) xd = field::mul<F>(pd, sd[t + off]);
     __syncthreads();
     sn[t] = pn = xn;
     sd[t] = pd = xd;
@@ -108,10 +111,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void gp_scan(uint64_t nq, Fe* __restr
 #else
     dinv = field::inv_kaliski<F>(sd[0]);  // sd[0] = D
 #endif
-    if (closing) closing[c] = field::mul<F>(field::mul<F>(s, sn[SCAN_THREADS - 1]), dinv);
+    if (closing) closing[c] = field::mul<F>(field::mul<F>(s, sn[T - 1]), dinv);
   }
   __syncthreads();
-  Fe rd = t + 1 < (uint32_t)SCAN_THREADS ? field::mul<F>(dinv, sd[t + 1]) : dinv;
+  Fe rd = t + 1 < (uint32_t)T ? field::mul<F>(dinv, sd[t + 1]) : dinv;
   Fe rn = t ? field::mul<F>(s, sn[t - 1]) : s;
   for (uint64_t q = b; q < e; q++) {  // forward: seed times the exclusive num prefix
     const Fe vn = an[q];
@@ -252,12 +255,17 @@ hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_
   Fe* td = tn + (uint64_t)g * nb;
   const uint32_t zq = (uint32_t)((nq + 255) / 256);
   hipLaunchKernelGGL(gp_chunk<F>, dim3(zq, g), dim3(256), 0, s, usable, num, den, zn, zd);
-  if (nq <= 4ull * SCAN_THREADS) {
+  if (nq <= 64) {
+    hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nq, zn, zd, seed, closing);
+  } else if (nq <= 4ull * SCAN_THREADS) {
     hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, seed, closing);
   } else {
     hipLaunchKernelGGL(gp_block_reduce<F>, dim3((uint32_t)nb, g), dim3(SCAN_THREADS), 0, s, nq, zn, zd,
                        tn, td);
-    hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, tn, td, seed, closing);
+    if (nb <= 64)
+      hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nb, tn, td, seed, closing);
+    else
+      hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, tn, td, seed, closing);
     hipLaunchKernelGGL(gp_block_down<F>, dim3((uint32_t)nb, g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, tn);
   }
   if (chain) hipLaunchKernelGGL(gp_chain_seeds<F>, dim3(1), dim3(64), 0, s, chain, post, g);
