@@ -301,7 +301,10 @@ __device__ __forceinline__ void producer_words(uint64_t* prod, const Ops& P, uin
 
 // MODE (diagnostics; the product launches FZ_FULL, with FZ_INJECT only under the test hook)
 #ifndef B2F_FUSED_WAVES
-#define B2F_FUSED_WAVES 4  // waves per SIMD the fused kernel is compiled for (VGPR budget)
+// waves per SIMD the half-round kernel is compiled for (its VGPR budget): 2 -- the launch runs 2
+// workgroups per CU, and the larger budget (153 VGPRs, no scratch) was 1.7 % faster on average
+// over four boxes (-3.8 / -1.3 / +0.9 / -2.5 %, profiles/r02l_ab15-18)
+#define B2F_FUSED_WAVES 2
 #endif
 #ifndef B2F_FUSED_HR_PER_CU
 #define B2F_FUSED_HR_PER_CU 2  // half-round launch: workgroups per CU (at most what fits)
