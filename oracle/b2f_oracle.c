@@ -564,7 +564,7 @@ static int gate_fails(const gctx* g, int sel) {
     case S_A2: {
         i128 s = 0;
         for (unsigned k = 0; k < 4; k++)
-            s += (cv(g, A3, k) + cv(g, A4, k) + cv(g, A5, k) - cv(g, A1, k)) << (16 * k);
+            s += (cv(g, A3, k) + cv(g, A4, k) + cv(g, A5, k) - cv(g, A1, k)) * ((i128)1 << (16 * k));
         i128 c = cv(g, A9, 0);
         return (s - P64 * c) != 0 || c * (c - 1) * (c - 2) != 0;
     }
@@ -572,7 +572,7 @@ static int gate_fails(const gctx* g, int sel) {
     case S_C2: {
         i128 s = 0;
         for (unsigned k = 0; k < 4; k++)
-            s += (cv(g, A3, k) + cv(g, A4, k) - cv(g, A1, k)) << (16 * k);
+            s += (cv(g, A3, k) + cv(g, A4, k) - cv(g, A1, k)) * ((i128)1 << (16 * k));
         i128 c = cv(g, A9, 0);
         return (s - P64 * c) != 0 || c * (c - 1) != 0;
     }

@@ -224,3 +224,27 @@ def test_tampered_trace_caught_only_by_the_fixed_check(orc, kind, row, delta):
     assert rep["fixed_failures"] == len(bad_rows) >= 1
     assert rep["first_failure"] == (int(bad_rows[0]) << 8) | orc.CODE_FIXED
     assert int(off[1]) + row <= int(bad_rows[0]) < int(off[1]) + row + 4  # the altered block
+
+
+def test_oracle_under_host_sanitizers():
+    """The oracle's every entry point under AddressSanitizer + UndefinedBehaviorSanitizer
+    (`make -C oracle asan`, driver oracle/asan_check.c): mixed rounds, a padded tail, single-cell
+    corruptions, a tampered fill, the Fp export. Host code only (GPU sanitizers are not available
+    on the pool). Found and fixed: a left shift of a negative 128-bit sum in the ADD gates."""
+    import os
+    import shutil
+    import subprocess
+
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    b = subprocess.run(["make", "-s", "-C", root, "asan"], capture_output=True, text=True, timeout=300)
+    if b.returncode != 0 and "sanitize" in (b.stderr or ""):
+        pytest.skip("sanitizer runtime unavailable: " + b.stderr[-200:])
+    assert b.returncode == 0, b.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1",
+               OMP_NUM_THREADS="2")
+    r = subprocess.run([os.path.join(root, "_asan", "asan_check")], capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout[-500:], r.stderr[-2000:])
+    assert "asan_check ok" in r.stdout
