@@ -1813,8 +1813,11 @@ __device__ __forceinline__ uint32_t edge_fast_checks(const ELane& E) {
   return acc;
 }
 
+#ifndef B2F_EDGE_WAVES
+#define B2F_EDGE_WAVES 3  // waves per SIMD the edge kernel is compiled for (VGPR budget)
+#endif
 template <int MODE>
-__global__ void __launch_bounds__(FW * WAVES, 3)
+__global__ void __launch_bounds__(FW * WAVES, B2F_EDGE_WAVES)
 fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
                   uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
                   uint32_t* __restrict__ fixed, uint32_t* __restrict__ redo,

@@ -130,6 +130,16 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
   if (c == 1) vd ^= x->t[1];
   if (c == 2 && x->f) vd = ~vd;
 
+  // the instance's 16 message words in LDS (each lane of the quad loads four), so the rounds'
+  // SIGMA-permuted reads are LDS reads instead of dependent global loads
+  __shared__ uint64_t Msg[BLOCK / 4][16];
+  uint64_t* mw = Msg[threadIdx.x >> 2];
+#pragma unroll
+  for (int k = 0; k < 4; k++) mw[4 * c + k] = x->m[4 * c + k];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
   uint64_t* s = rec + st * 16 + c;
   auto dump = [&](void) {
     s[0] = va;
@@ -147,8 +157,8 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
   dump();
   for (uint32_t r = 0; r < rounds; r++) {
     const uint8_t* sg = c_sigma[r % 10];
-    const uint64_t m0 = x->m[sg[2 * c]], m1 = x->m[sg[2 * c + 1]];
-    const uint64_t m2 = x->m[sg[8 + 2 * c]], m3 = x->m[sg[9 + 2 * c]];
+    const uint64_t m0 = mw[sg[2 * c]], m1 = mw[sg[2 * c + 1]];
+    const uint64_t m2 = mw[sg[8 + 2 * c]], m3 = mw[sg[9 + 2 * c]];
     G(m0, m1);  // column step
     dump();
     vb = quad_dpp64<QROT1>(vb);
