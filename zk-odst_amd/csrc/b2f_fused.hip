@@ -322,6 +322,10 @@ enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16,
                           // non-temporal (2; it had been neutral at 4 per CU), sc0 (1) in between
 #endif
 constexpr int BUF_NT = B2F_BUF_POLICY;  // gfx94x/gfx950 cache-policy bits: 1 sc0, 2 non-temporal
+#ifndef B2F_EDGE_BUF_POLICY
+#define B2F_EDGE_BUF_POLICY 2  // the edge launch's region stores: non-temporal (690 vs 763 us)
+#endif
+constexpr int EDGE_NT = B2F_EDGE_BUF_POLICY;
 __device__ __forceinline__ void tile_store(uint32_t* base, uint32_t nq, uint32_t lane, uint4 v) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const i32x4 rsrc = {(int32_t)(uint32_t)a, (int32_t)(uint32_t)(a >> 32), (int32_t)(nq * 16u), 0x00020000};
@@ -1691,7 +1695,7 @@ __device__ __forceinline__ void region_store(uint32_t* base, uint32_t nq, uint32
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const i32x4 rsrc = {(int32_t)(uint32_t)a, (int32_t)(uint32_t)(a >> 32), (int32_t)(nq * 16u), 0x00020000};
   b2f_raw_buffer_store_v4(i32x4{(int32_t)v.x, (int32_t)v.y, (int32_t)v.z, (int32_t)v.w}, rsrc,
-                          (int)(16u * (lane - q0)), 0, BUF_NT);  // lanes outside: past the range
+                          (int)(16u * (lane - q0)), 0, EDGE_NT);  // lanes outside: past the range
 }
 
 struct ECtx {
