@@ -1062,11 +1062,11 @@ __device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) { return (uin
 // tag of a 16-bit value (0: < 2^8, 1: < 2^15, 2: otherwise), branch-free
 __device__ __forceinline__ uint32_t tag_of(uint32_t x) { return ((x + 0xff00u) >> 16) + (x >> 15); }
 __device__ __forceinline__ uint32_t sel32(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
-// spread16 of the low 16 bits of x by two lookups in the byte spread table at LDS byte address
-// `tb` (4 VALU + 2 LDS reads instead of 8-12 VALU for the shift/mask interleave)
+// spread16 of x (< 2^16) -- optionally (B2F_HR_SPT) by two lookups in a byte spread table at LDS
+// byte address `tb` (4 VALU + 2 LDS reads instead of 8-12 VALU for the shift/mask interleave)
 __device__ __forceinline__ uint32_t spread_t(uint32_t tb, uint32_t x) {
-#ifndef B2F_HR_SPT  // the table form measured 1 % slower in the fused kernel (more LDS traffic)
-  return spread16(x & 0xffffu);
+#ifndef B2F_HR_SPT  // the table form measured 1-7 % slower in the fused kernel (more LDS traffic)
+  return spread16(x);  // x < 2^16 here, or a check whose (x & 0xffff0000) term already flags it
 #else
   const uint32_t lo = ld16(tb + ((x & 0xffu) << 1));
   const uint32_t hi = ld16(tb + ((x >> 7) & 0x1feu));
