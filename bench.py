@@ -425,6 +425,8 @@ def main():
                 floors[kname + "_floor_ms"] = round(tot / max(cnt, 1), 4)
                 floors[kname + "_over_floor"] = round(kern[kname]["avg_ms"] / (tot / max(cnt, 1)), 4) \
                     if kname in kern else None
+                if kname == "fill" and "fill_eval" in kern:  # the fused pass writes the same trace
+                    floors["fill_eval_over_fill_floor"] = round(kern["fill_eval"]["avg_ms"] / (tot / max(cnt, 1)), 4)
             deng.sync(stream)
             deng.close()
             batch.fill(eng, stream)  # leave a real trace behind
