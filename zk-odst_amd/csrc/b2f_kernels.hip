@@ -140,6 +140,29 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+#ifndef B2F_REC_COLUMN  // diagnostics: B2F_REC_COLUMN = the column-wise 8-byte stores
+  // each dump transposed inside the quad through LDS: lane c writes row c of the 4 x 4 work matrix
+  // (words 4c .. 4c + 3, 32 contiguous bytes) instead of column c as four 8-byte stores
+  __shared__ __attribute__((aligned(16))) uint64_t Tq[BLOCK / 4][16];
+  uint64_t* tq = Tq[threadIdx.x >> 2];
+  uint64_t* s = rec + st * 16 + 4 * c;
+  auto dump = [&](void) {
+    tq[c] = va;
+    tq[4 + c] = vb;
+    tq[8 + c] = vc;
+    tq[12 + c] = vd;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint4 r0 = *reinterpret_cast<const uint4*>(tq + 4 * c), r1 = *reinterpret_cast<const uint4*>(tq + 4 * c + 2);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    *reinterpret_cast<uint4*>(s) = r0;
+    *reinterpret_cast<uint4*>(s + 2) = r1;
+    s += 16;
+  };
+#else
   uint64_t* s = rec + st * 16 + c;
   auto dump = [&](void) {
     s[0] = va;
@@ -148,6 +171,7 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
     s[12] = vd;
     s += 16;
   };
+#endif
   auto G = [&](uint64_t mx, uint64_t my) {
     va = va + vb + mx; vd = rotr64(vd ^ va, 32);
     vc = vc + vd;      vb = rotr64(vb ^ vc, 24);
