@@ -1346,9 +1346,17 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
 
   if (*status == 0) {  // the record kernel accepted the layout
     const uint64_t used_rows = off[n];
+#ifdef B2F_XCD_REGION  // diagnostics: XCD x owns the x-th eighth of the tiles as one region
+    const uint64_t n_all = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
+    const uint64_t W = (uint64_t)(gridDim.x / 8) * WAVES;
+    const uint64_t R8 = (n_all + 7) / 8, lo8 = (uint64_t)(blockIdx.x % 8) * R8;
+    const uint64_t n_hr = lo8 + R8 < n_all ? lo8 + R8 : n_all;
+    uint64_t t = lo8 + (uint64_t)(blockIdx.x / 8) * WAVES + __builtin_amdgcn_readfirstlane(wv);
+#else
     const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
     const uint64_t W = (uint64_t)gridDim.x * WAVES;
     uint64_t t = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
+#endif
     auto raw_desc = [&](uint64_t tt) -> uint4 {
       const uint64_t ti = tt < n_hr ? tt : 0;
       const uint4 v = desc[ti].v;
