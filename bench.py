@@ -16,7 +16,8 @@ the verdict counters and one RCCL all_gather of the h' outputs. The whole witnes
 reassembled on every rank (dist.gather_trace: one all-gather per column into the final
 column-major buffers) where it fits in HBM, timed apart ("witness_gather"); at N = 8 a
 BASELINE configs[3] leg (2^20 sharded, gather of the full 241 GB table) runs after the headline
-unless --config4 0. Rank 0 prints one JSON line.
+unless --config4 0 (--config4-world picks the N it runs at, for rehearsals). Rank 0 prints one
+JSON line.
 """
 import argparse
 import json
@@ -153,8 +154,16 @@ def main():
                          "whole witness table is all-gathered to every rank (timed apart; 0 "
                          "skips). With --global-batch the step's own trace is gathered if it fits")
     ap.add_argument("--config4", type=int, default=1 << 20,
-                    help="N = 8 without --global-batch: after the headline, run BASELINE "
-                         "configs[3] (this many instances sharded, full witness gather); 0 skips")
+                    help="N = --config4-world without --global-batch: after the headline, run "
+                         "BASELINE configs[3] (this many instances sharded, full witness "
+                         "gather); 0 skips")
+    ap.add_argument("--config4-world", type=int, default=8,
+                    help="world size at which the config-4 leg runs (8 = BASELINE configs[3]; "
+                         "a smaller N with a small --config4 rehearses the same code)")
+    ap.add_argument("--gather-cap-gb", type=float, default=0.0,
+                    help="treat every rank as having at most this much free HBM when deciding "
+                         "whether a witness gather fits (0 = the real free memory; rehearses "
+                         "the skip branch)")
     ap.add_argument("--aux-steps", type=int, default=5,
                     help="steps of the other path timed after the headline loop (0 = skip)")
     ap.add_argument("--floor-reps", type=int, default=3,
@@ -292,6 +301,8 @@ def main():
     def fits_everywhere(nbytes, margin=2 << 30):
         """True on every rank iff every rank has nbytes + margin of free HBM (collective)."""
         free = torch.cuda.mem_get_info(local)[0]
+        if args.gather_cap_gb > 0:
+            free = min(free, int(args.gather_cap_gb * 1e9))
         ok = torch.tensor([1 if free >= nbytes + margin else 0], dtype=torch.int64, device=device)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         return bool(ok.item()), free
@@ -541,8 +552,9 @@ def main():
 
     # BASELINE configs[3] after a weak-scaling headline at N = 8: 2^20 instances sharded over
     # the ranks, fill + eval timed the same way, then the whole witness table gathered
+    # (--config4-world 2 --config4 32768 rehearses the same code on a one-GPU box)
     config4 = None
-    if world == 8 and not global_n and args.config4 > 0:
+    if world > 1 and world == args.config4_world and not global_n and args.config4 > 0:
         try:
             del batch
             torch.cuda.empty_cache()
@@ -557,6 +569,9 @@ def main():
             del b4
         except Exception as e:
             config4 = {"error": repr(e)}
+        # free-memory evidence per rank for the 2^20 leg (the gather's buffers are the largest)
+        if isinstance(config4, dict):
+            config4["hbm_free_after_gb"] = round(torch.cuda.mem_get_info(local)[0] / 1e9, 1)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

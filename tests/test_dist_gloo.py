@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, inputs_bytes, q):
+def _worker(rank, world, port, inputs_bytes, q, coalesce=None):
     import sys
 
     for p in (os.path.join(ROOT, "zk-odst_amd"), os.path.join(ROOT, "oracle")):
@@ -50,7 +50,12 @@ def _worker(rank, world, port, inputs_bytes, q):
         bdist.verdict_words(torch.from_numpy(raw.view(np.int64)), sbase[rank], torch), dist)
     h = bdist.gather_h_out(torch.from_numpy(h_out.view(np.int64)), shards, dist, torch)
     ga, gf = bdist.gather_trace(torch.from_numpy(adv.view(np.int32)),
-                                torch.from_numpy(fixed.view(np.int32)), srows, dist, torch)
+                                torch.from_numpy(fixed.view(np.int32)), srows, dist, torch,
+                                coalesce=coalesce)
+    # a refused coalescing attempt must leave the group usable: this collective runs now
+    probe = torch.tensor([rank + 1], dtype=torch.int64)
+    dist.all_reduce(probe)
+    assert int(probe.item()) == world * (world + 1) // 2
     q.put((rank, combined, words.tolist(), h.numpy().view(np.uint64).tobytes(), shards, sbase,
            ga.numpy().view(np.uint32).tobytes(), gf.numpy().view(np.uint32).tobytes()))
     dist.destroy_process_group()
@@ -69,11 +74,16 @@ def test_plan_shards_balances_rows():
         assert max(rows) - min(rows) <= 2 * 5220  # within two instances of even
 
 
-@pytest.mark.parametrize("n,rounds,seed", [(37, (0, 1, 4, 12), 42), (23, (1, 4, 12), 43)])
-def test_gloo_world2_matches_single_process(orc, n, rounds, seed):
+@pytest.mark.parametrize("n,rounds,seed,coalesce", [(37, (0, 1, 4, 12), 42, None),
+                                                    (23, (1, 4, 12), 43, None),
+                                                    (23, (1, 4, 12), 44, True)])
+def test_gloo_world2_matches_single_process(orc, n, rounds, seed, coalesce):
     """Unequal mixed-rounds shards: the all-gathered witness table is the single-process
     trace (total_rows = world x window), h' is the batch's, and the combined verdict equals the
-    oracle's verdict on the reassembled table, first failure at its global row."""
+    oracle's verdict on the reassembled table, first failure at its global row. coalesce=True
+    forces gather_trace's RCCL-style coalesced attempt, which gloo refuses (no
+    startCoalescing): the guarded fallback must gather the same table and leave the group
+    usable."""
     import multiprocessing as mp
 
     from b2f import dist as bdist
@@ -82,7 +92,8 @@ def test_gloo_world2_matches_single_process(orc, n, rounds, seed):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, x.tobytes(), q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, x.tobytes(), q, coalesce))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

@@ -243,3 +243,94 @@ def test_2p18_mixed_split_equals_fused(engine, orc):
         r = x[int(i)]
         ref = orc.compress(int(r["rounds"]), r["h"], r["m"], r["t"], int(r["f"]))
         assert np.array_equal(h_host[int(i)], ref), int(i)
+
+
+def test_2p18x12_fused_equals_split_past_2p30(engine, orc):
+    """BASELINE config 3 at full size, on the headline path itself: 2^18 uniform 12-round
+    instances = 1.368 G rows, so every column runs past row 2^30 and past 4 GiB of bytes.
+    The fused kernel's verdict reads its wave's LDS staging, not HBM, so it cannot see a
+    store-address error; this test can. (1) The fused trace, fixed column and h' written over
+    poisoned buffers equal the split path's (fill_dev + eval_dev) bit for bit on the device,
+    with the same clean verdict. (2) Instances whose rows lie past 2^30 (a random sample plus
+    the first and last of them) equal the oracle's fill of those instances. (3) Single-cell
+    faults injected past row 2^30 as the fused kernel assigns them change exactly that cell of
+    the written trace, and the fused verdict equals b2f_eval_dev's on the written trace and
+    the oracle's on the faulted instance (re-based to the global row)."""
+    import b2f
+    import torch
+
+    from b2f import synth
+
+    n = 1 << 18
+    x = synth.batch(n, rounds=12)
+    a = b2f.DeviceBatch(x)
+    a.fill(engine)
+    a.evaluate(engine)
+    engine.sync(_stream())
+    ra = a.report_dict()
+    assert ra["first_failure"] == NONE and ra["rows_checked"] == a.used_rows
+    assert a.used_rows > 1 << 30 and a.used_rows * 4 > 1 << 32
+    adv, fx, h = a.advice.clone(), a.fixed.clone(), a.h_out.clone()
+    a.advice.fill_(-1)
+    a.fixed.fill_(-1)
+    a.h_out.fill_(-1)
+    a.fill_evaluate(engine)
+    engine.sync(_stream())
+    assert a.report_dict() == ra
+    for c in range(10):
+        assert torch.equal(a.advice[c], adv[c]), "fused a_%d != split a_%d" % (c, c)
+    assert torch.equal(a.fixed, fx) and torch.equal(a.h_out, h)
+
+    off = a.offsets_host
+    first_past = int(np.searchsorted(off, 1 << 30, side="right")) - 1  # holds row 2^30
+    assert 200000 < first_past < n - 40000
+    rng = np.random.default_rng(60)
+    sample = sorted({first_past, first_past + 1, n - 1}
+                    | {int(i) for i in rng.integers(first_past, n, 45)})
+    h_host = a.host_h_out()
+    for i in sample:
+        oadv, ofixed, oh, _ = orc.fill(_as_oracle(x[i:i + 1], orc))
+        r0, r1 = int(off[i]), int(off[i + 1])
+        assert np.array_equal(a.advice[:, r0:r1].cpu().numpy().view(np.uint32), oadv), i
+        assert np.array_equal(a.fixed[r0:r1].cpu().numpy().view(np.uint32), ofixed), i
+        assert np.array_equal(h_host[i], oh[0]), i
+
+    # (instance, column (10 = fixed), row inside the instance, bit): a half-round a1 limb, an
+    # XOR63 cell, a selector bit, an XOR3 operand (a copy) of the last instance, the lookup
+    # cell of the first row past 2^30
+    cross = (1 << 30) - int(off[first_past])
+    faults = [(n - 3, 1, 164 + 416 * 7 + 52 * 2 + 3, 5), (230001, 8, 164 + 416 * 4 + 46, 0),
+              (250000, 10, 164 + 416 * 10 + 52 * 1 + 4, 2), (n - 1, 5, 164 + 416 * 12 + 8, 9),
+              (first_past, 1, cross, 11)]
+    for i, c, r, b in faults:
+        r0, r1 = int(off[i]), int(off[i + 1])
+        row = r0 + r
+        assert row >= 1 << 30 and row < r1
+        try:
+            engine.debug_inject(row, c, 1 << b)
+            a.fill_evaluate(engine)
+            engine.sync(_stream())
+        finally:
+            engine.debug_inject(None)
+        got = a.report_dict()
+        if c < 10:
+            for cc in range(10):
+                d = (a.advice[cc] != adv[cc]).nonzero().reshape(-1).tolist()
+                assert d == ([row] if cc == c else []), (i, c, r, cc, d[:4])
+            assert torch.equal(a.fixed, fx)
+        else:
+            for cc in range(10):
+                assert torch.equal(a.advice[cc], adv[cc])
+            assert (a.fixed != fx).nonzero().reshape(-1).tolist() == [row]
+        assert torch.equal(a.h_out, h)
+        a.evaluate(engine)  # the standalone eval on the trace the fused kernel wrote
+        engine.sync(_stream())
+        assert a.report_dict() == got, (i, c, r, b)
+        iadv = a.advice[:, r0:r1].cpu().numpy().view(np.uint32)
+        ifx = a.fixed[r0:r1].cpu().numpy().view(np.uint32)
+        o = orc.evaluate(iadv, ifx, np.array([0, r1 - r0], dtype=np.uint64))
+        assert o["first_failure"] != NONE, (i, c, r, b)
+        want = dict(o, rows_checked=a.used_rows, first_failure=o["first_failure"] + (r0 << 8))
+        assert got == want, (i, c, r, b, got, want)
+    del adv, fx, h
+    torch.cuda.empty_cache()

@@ -113,7 +113,36 @@ def gather_trace_bytes(rows_per_rank):
     return 11 * 4 * (world * w + min(STAGE_ROWS, w))
 
 
-def gather_trace(adv_local, fixed_local, rows_per_rank, dist, torch, group=None, out=None):
+def _gather_coalesced(out, cols, dist, group, dev):
+    """The eleven column all-gathers as one coalesced group (torch's private
+    _coalescing_manager; RCCL issues them between one group start/end). Returns False, having
+    issued nothing, when this torch or backend cannot coalesce (no such API, another signature,
+    or a backend without startCoalescing, as gloo): the caller then runs the plain loop. The
+    manager registers the group in its pending-op table before it starts coalescing, so a start
+    that raises would leave every later collective of the group queued there; that entry is
+    removed on the way out."""
+    coalesce = getattr(dist, "_coalescing_manager", None)
+    if coalesce is None:
+        return False
+    issued = []
+    try:
+        with coalesce(group=group, device=dev):
+            for c in range(11):
+                dist.all_gather_into_tensor(out[c], cols[c], group=group)
+                issued.append(c)
+        return True
+    except (RuntimeError, TypeError, ValueError, NotImplementedError):
+        if issued:  # a failure after ops were queued is not a capability problem
+            raise
+        c10d = getattr(dist, "distributed_c10d", None)
+        state = getattr(getattr(c10d, "_world", None), "pg_coalesce_state", None)
+        if state is not None:
+            state.pop(group if group is not None else c10d._get_default_group(), None)
+        return False
+
+
+def gather_trace(adv_local, fixed_local, rows_per_rank, dist, torch, group=None, out=None,
+                 coalesce=None):
     """The whole batch's witness table on every rank.
 
     adv_local [10, W] and fixed_local [W] (int32 bit patterns): this rank's trace, allocated
@@ -124,7 +153,9 @@ def gather_trace(adv_local, fixed_local, rows_per_rank, dist, torch, group=None,
     fill for the whole batch with total_rows = world * W.
 
     One all_gather_into_tensor per column, straight into that column of the result (no
-    pad-and-cat copies; on RCCL the eleven calls are issued in one coalesced group), then an
+    pad-and-cat copies; on RCCL the eleven calls are issued in one coalesced group, falling back
+    to the plain loop where this torch cannot coalesce; `coalesce` forces the attempt (True) or
+    the loop (False), default: RCCL only), then an
     in-place compaction of the padded windows through a bounded staging buffer: rank k's rows
     move from k * W down to the prefix sum of the shards before it, in increasing row order, so
     a staged chunk never overwrites rows that still have to move."""
@@ -137,12 +168,9 @@ def gather_trace(adv_local, fixed_local, rows_per_rank, dist, torch, group=None,
     if out is None:
         out = torch.empty((11, world * w), dtype=adv_local.dtype, device=dev)
     cols = [adv_local[c] for c in range(10)] + [fixed_local]
-    coalesce = getattr(dist, "_coalescing_manager", None)
-    if coalesce is not None and dist.get_backend(group) == "nccl":
-        with coalesce(group=group, device=dev):
-            for c in range(11):
-                dist.all_gather_into_tensor(out[c], cols[c], group=group)
-    else:
+    if coalesce is None:
+        coalesce = dist.get_backend(group) == "nccl"
+    if not (coalesce and _gather_coalesced(out, cols, dist, group, dev)):
         for c in range(11):
             dist.all_gather_into_tensor(out[c], cols[c], group=group)
     # compaction of the padded windows (no-op when every shard fills its window)
