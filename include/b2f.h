@@ -52,6 +52,8 @@ extern "C" {
 #define B2F_ERR_HIP 4       /* HIP runtime error */
 #define B2F_ERR_LAYOUT 5    /* offsets are not the prefix sums of R(rounds_i) */
 #define B2F_ERR_INPUT 6     /* malformed EIP-152 input (length != 213 or f not 0/1) */
+#define B2F_ERR_FIELD 7     /* (at b2f_sync) a grand product's denominator product is zero: a
+                               challenge collides with a cell value, its z column is meaningless */
 
 /* One EIP-152 compression: the reference's Blake2fWitness{rounds, h, m, t, f}
  * (blake2f.rs:208-239), 216 bytes, naturally aligned. f must be 0 or 1. */
@@ -177,8 +179,9 @@ B2F_API int b2f_fill_fixed_dev(b2f_ctx* ctx, const uint64_t* d_offsets, size_t n
  * returns count = 24 + 576 * rounds + 96 (0 if rounds > B2F_MAX_ROUNDS). Host function. */
 B2F_API uint64_t b2f_copy_constraints(uint32_t rounds, uint32_t* out4, uint64_t cap);
 
-/* Wait for `stream` and return the first device-side error of the fill/eval calls issued
- * since the previous b2f_sync (B2F_ERR_LAYOUT / B2F_ERR_ROUNDS), then clear it. */
+/* Wait for `stream` and return the first device-side error of the calls issued since the
+ * previous b2f_sync (B2F_ERR_LAYOUT / B2F_ERR_ROUNDS from fill/eval, B2F_ERR_FIELD from the
+ * lookup / permutation grand products), then clear it. */
 B2F_API int b2f_sync(b2f_ctx* ctx, void* stream);
 
 /* Host-pointer conveniences (allocate, copy, run, copy back; blocking). b2f_fill sizes the
@@ -288,7 +291,11 @@ B2F_API uint64_t b2f_permutation_mapping(uint32_t rounds, uint32_t* out, uint64_
  * canonical elements of the field chosen by `form` (any B2F_FP_*; outputs in that form).
  * out_rows >= usable_rows + 1 (and >= 2^k with d_sigma); 16-byte aligned outputs. A valid
  * trace closes: z_last[usable_rows] = 1. Asynchronous on `stream` after a short host setup
- * (mapping patterns cached per rounds in the context). */
+ * (mapping patterns cached per rounds in the context; the instance table goes up by an async
+ * copy from pinned staging). The host waits only for the previous call's table upload, and for
+ * the whole stream only when a device buffer has to grow (a new `rounds`, more instances, a
+ * larger k or a smaller chunk_len than before). Scratch: ceil(8 / chunk_len) column sets of
+ * 3 x 32 B per usable row plus O(2^k / 1024) tables. */
 B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t total_rows,
                                         const uint64_t* h_offsets, size_t n, uint32_t k,
                                         uint64_t usable_rows, const uint64_t omega[4],

@@ -135,3 +135,15 @@ def test_copy_constraints_match_oracle_structure(orc, rounds):
     assert len(got) == 24 + 576 * rounds + 96 == len(want)
     assert np.array_equal(got, want)
     assert len(set(map(tuple, got[:, :2].tolist()))) == len(got)  # one copy per operand cell
+
+
+def test_status_codes_match_the_header():
+    """The ctypes binding's status codes and names are the header's #defines."""
+    from b2f import _lib
+
+    src = open(ROOT + "/include/b2f.h").read()
+    codes = {m.group(1): int(m.group(2))
+             for m in re.finditer(r"#define (B2F_(?:OK|ERR_\w+))\s+(\d+)", src)}
+    assert codes["B2F_ERR_FIELD"] == 7
+    assert {v: k for k, v in _lib.STATUS_NAMES.items()} == \
+        {("OK" if k == "B2F_OK" else k): v for k, v in codes.items()}

@@ -75,3 +75,27 @@ def test_chain_inputs_errors(engine):
         engine.chain_inputs_dev(0, m.data_ptr(), t.data_ptr(), f.data_ptr(), 12, 4, out.data_ptr())
     engine.chain_inputs_dev(h.data_ptr(), m.data_ptr(), t.data_ptr(), f.data_ptr(), 12, 0,
                             out.data_ptr())  # n = 0: nothing to do
+
+
+@pytest.mark.parametrize("use_side_stream", [False, True])
+def test_split_right_after_fused_without_host_sync(engine, use_side_stream):
+    """run_plan once needed a host synchronize between torch's copies/allocations
+    and the library's launches. Back-to-back batches on alternating paths, on the current
+    stream or on a side stream, with nothing between them but stream order, must all give
+    hashlib's digests."""
+    import torch
+
+    from b2f import hasher
+
+    rng = np.random.default_rng(11)
+    side = torch.cuda.Stream() if use_side_stream else None
+    s = side.cuda_stream if side is not None else None
+    batches = [_msgs(rng, n, L) for n, L in ((700, 2000), (400, 900), (900, 2600), (300, 400))]
+    plans = [hasher.Plan(m) for m in batches]
+    results = []
+    for i, plan in enumerate(plans):  # fused, split, fused, split; no synchronize between
+        results.append(hasher.run_plan(engine, plan, "fused" if i % 2 == 0 else "split", stream=s))
+    for msgs, res in zip(batches, results):
+        assert res.verified
+        for m, d in zip(msgs, res.digests):
+            assert d == hashlib.blake2b(m).digest(), len(m)

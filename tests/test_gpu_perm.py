@@ -128,3 +128,61 @@ def test_permutation_argument_errors(engine, batch):
         assert e.value.code == code, kw
     call()
     engine.sync(s)
+
+
+def test_permutation_scratch_scales_with_column_sets(engine, batch):
+    """The scratch holds one num / den / product slice per column SET (ceil(8 / chunk_len)),
+    not per column: measured as the device memory a fresh context takes on its first call,
+    chunk_len 1 (8 sets) against chunk_len 8 (1 set) at a 2^20-row domain."""
+    import b2f
+    import torch
+
+    k, usable = 20, (1 << 20) - 7
+    dev = batch.advice.device
+    w, d = pm.domain(pm.P_PALLAS, k)
+    s = torch.cuda.current_stream().cuda_stream
+    taken = {}
+    for chunk in (8, 1, 3):
+        sets = (8 + chunk - 1) // chunk
+        z = torch.empty((sets, 1 << k, 4), dtype=torch.int64, device=dev)
+        eng = b2f.Engine(0)
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info(dev)[0]
+        eng.permutation_columns_dev(batch.advice.data_ptr(), batch.total_rows, batch.offsets_host,
+                                    k, usable, w, d, 3, 5, chunk, 1, 0, z.data_ptr(), 1 << k, s)
+        eng.sync(s)
+        taken[sets] = free0 - torch.cuda.mem_get_info(dev)[0]
+        eng.close()
+        del z
+        torch.cuda.empty_cache()
+    per_set = (taken[8] - taken[1]) / 7
+    # num + den (2 x 32 B per row) + the grand product's chunk totals (~4 B per row)
+    assert 60 * usable < per_set < 80 * usable, taken
+    assert abs((taken[3] - taken[1]) - 2 * per_set) < 0.1 * per_set, taken
+
+
+def test_zero_denominator_is_reported(engine, batch):
+    """A challenge that makes a den factor zero (beta = gamma = 0 against a zero cell) cannot
+    give a meaningful z (halo2's batch_invert would leave a zero and the proof fail): the call
+    reports B2F_ERR_FIELD at b2f_sync, and the sticky word is clear after that."""
+    import b2f
+    import torch
+
+    s = torch.cuda.current_stream().cuda_stream
+    k = 12
+    sig, z = batch.permutation_columns(engine, k, (1 << k) - 7, 0, 0, chunk_len=3, form=1,
+                                       sigma=False)
+    with pytest.raises(b2f.B2FError) as e:
+        engine.sync(s)
+    assert e.value.code == b2f._lib.ERR_FIELD
+    engine.sync(s)  # cleared
+    # the lookup argument: (A' + beta) is zero for the zero row's compressed value when beta = 0
+    usable = (1 << 16) + 100
+    out, bad = batch.lookup_columns(engine, [0], usable, 7, 0, 11, form=1)
+    with pytest.raises(b2f.B2FError) as e:
+        engine.sync(s)
+    assert e.value.code == b2f._lib.ERR_FIELD
+    # non-degenerate challenges: clean
+    batch.permutation_columns(engine, k, (1 << k) - 7, 3, 5, chunk_len=3, form=1, sigma=False)
+    batch.lookup_columns(engine, [0], usable, 7, 3, 11, form=1)
+    engine.sync(s)

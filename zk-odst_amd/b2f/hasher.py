@@ -146,28 +146,29 @@ def run_plan(engine, plan, path="fused", device="cuda:0", stream=None):
     s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
     compute = torch.cuda.ExternalStream(s, device=dev)
     p_blocks, p_t, p_f = plan.pinned()
-    d_blocks = torch.empty(p_blocks.shape, dtype=p_blocks.dtype, device=dev)
-    d_t = torch.empty(p_t.shape, dtype=p_t.dtype, device=dev)
-    d_f = torch.empty(p_f.shape, dtype=p_f.dtype, device=dev)
     R = rows(BLAKE2B_ROUNDS)
-    # h' of every compression, step-major like the plan: step j's outputs are rows
-    # start[j] .. start[j] + active[j] - 1, and step j + 1 reads its h from that prefix
+    # Everything is allocated, copied and launched on the one stream `s`: torch's caching
+    # allocator hands a freed block to a new tensor of the same stream without a host wait, so
+    # the allocations must be made under `compute` too, or a block still read by an earlier
+    # launch on `s` could be handed to an allocation of another stream and overwritten early.
+    # No host synchronize is needed (tests/test_gpu_hasher.py runs split right after fused).
     with torch.cuda.stream(compute):
+        d_blocks = torch.empty(p_blocks.shape, dtype=p_blocks.dtype, device=dev)
+        d_t = torch.empty(p_t.shape, dtype=p_t.dtype, device=dev)
+        d_f = torch.empty(p_f.shape, dtype=p_f.dtype, device=dev)
+        # h' of every compression, step-major like the plan: step j's outputs are rows
+        # start[j] .. start[j] + active[j] - 1, and step j + 1 reads its h from that prefix
         h0 = torch.from_numpy(np.broadcast_to(plan.h0, (n, 8)).copy().view(np.int64)).to(dev)
         offsets = torch.arange(n + 1, dtype=torch.int64, device=dev) * R
-    hs = torch.empty((int(plan.start[-1]), 8), dtype=torch.int64, device=dev)
-    inputs = torch.empty(n * 216, dtype=torch.uint8, device=dev)
-    advice = torch.empty((_lib.NUM_ADVICE, R * n), dtype=torch.int32, device=dev)
-    fixed = torch.empty(R * n, dtype=torch.int32, device=dev)
-    report = torch.empty((plan.steps, _lib.REPORT_BYTES // 8), dtype=torch.int64, device=dev)
-    with torch.cuda.stream(compute):  # one asynchronous DMA from page-locked memory
+        hs = torch.empty((int(plan.start[-1]), 8), dtype=torch.int64, device=dev)
+        inputs = torch.empty(n * 216, dtype=torch.uint8, device=dev)
+        advice = torch.empty((_lib.NUM_ADVICE, R * n), dtype=torch.int32, device=dev)
+        fixed = torch.empty(R * n, dtype=torch.int32, device=dev)
+        report = torch.empty((plan.steps, _lib.REPORT_BYTES // 8), dtype=torch.int64, device=dev)
+        # one asynchronous DMA from page-locked memory, ordered before the launches below
         d_blocks.copy_(p_blocks, non_blocking=True)
         d_t.copy_(p_t, non_blocking=True)
         d_f.copy_(p_f, non_blocking=True)
-    # torch's copies and allocations are ordered before the library's launches by a host
-    # synchronize, not by stream order alone (measured: without it, the first split-path batch
-    # after a fused one read stale blocks)
-    torch.cuda.synchronize(dev)
     for j in range(plan.steps):
         a = int(plan.active[j])
         s0 = int(plan.start[j])
@@ -188,9 +189,10 @@ def run_plan(engine, plan, path="fused", device="cuda:0", stream=None):
     engine.sync(s)
     # message at sorted position p ends at step nblocks - 1, i.e. at row start[nb - 1] + p
     last = (plan.active[None, :] > np.arange(n)[:, None]).sum(1) - 1
-    idx = torch.from_numpy((plan.start[last] + np.arange(n)).astype(np.int64)).to(dev)
-    fin_host = hs.index_select(0, idx).cpu().numpy().view(np.uint64)
-    raw = report.cpu().numpy().view(np.uint64)
+    with torch.cuda.stream(compute):
+        idx = torch.from_numpy((plan.start[last] + np.arange(n)).astype(np.int64)).to(dev)
+        fin_host = hs.index_select(0, idx).cpu().numpy().view(np.uint64)
+        raw = report.cpu().numpy().view(np.uint64)
     reps = [_lib.EvalReport.from_buffer_copy(raw[j].tobytes()).as_dict()
             for j in range(plan.steps)]
     return ChainResult(plan, reps, fin_host)

@@ -71,7 +71,8 @@ __global__ __launch_bounds__(256) void gp_chunk(uint64_t usable, Fe* __restrict_
 // zn[q] <- K_q = seed N_before(q) D_end(q)^-1 with N_before(q) = prod_{q' < q} zn[q'],
 // D_end(q)^-1 = D^-1 prod_{q' > q} zd[q']. Per-thread runs of chunks, Hillis-Steele scans
 // of the run products in LDS (a prefix for num, a suffix for den), one inversion.
-// seed: Montgomery elements per product (nullptr: 1); closing (nullable) <- seed N / D.
+// seed: Montgomery elements per product (nullptr: 1); closing (nullable) <- seed N / D;
+// sticky (nullable): the context's sticky error word, B2F_ERR_FIELD set when D = 0.
 // T threads: SCAN_THREADS, or one wave when there are at most 64 chunk totals (the block totals
 // of the three-level path) -- a 1,024-thread scan of 8 values spent ten levels of products on
 // every thread.
@@ -79,7 +80,7 @@ template <class F, int T = SCAN_THREADS>
 __global__ __launch_bounds__(T) void gp_scan(uint64_t nq, Fe* __restrict__ zn,
                                              const Fe* __restrict__ zd,
                                              const Fe* __restrict__ seed,
-                                             Fe* __restrict__ closing) {
+                                             Fe* __restrict__ closing, int* __restrict__ sticky) {
   const uint32_t c = blockIdx.x, t = threadIdx.x;
   const uint64_t per = (nq + T - 1) / T;
   __shared__ Fe sn[T], sd[T];
@@ -111,6 +112,10 @@ __global__ __launch_bounds__(T) void gp_scan(uint64_t nq, Fe* __restrict__ zn,
 #else
     dinv = field::inv_kaliski<F>(sd[0]);  // sd[0] = D
 #endif
+    // D = 0: some den factor is zero (a challenge collides with a cell value). halo2's
+    // batch_invert would leave that entry zero and the proof would fail; here every z would
+    // come from a meaningless inverse, so the call reports B2F_ERR_FIELD at b2f_sync instead.
+    if (sticky && field::is_zero(sd[0])) atomicOr(sticky, 1 << B2F_ERR_FIELD);
     if (closing) closing[c] = field::mul<F>(field::mul<F>(s, sn[T - 1]), dinv);
   }
   __syncthreads();
@@ -262,7 +267,7 @@ __host__ __device__ inline uint64_t scratch_elems(uint64_t usable) {
 template <class F>
 hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_t z_stride,
                Fe* num, const Fe* den, Fe* zs, const Fe* seed, Fe* closing, hipStream_t s,
-               Fe* chain = nullptr) {
+               Fe* chain = nullptr, int* sticky = nullptr) {
   Fe* post = nullptr;
   if (chain) {
     seed = nullptr;
@@ -277,16 +282,16 @@ hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_
   const uint32_t zq = (uint32_t)((nq + 255) / 256);
   hipLaunchKernelGGL(gp_chunk<F>, dim3(zq, g), dim3(256), 0, s, usable, num, den, zn, zd);
   if (nq <= 64) {
-    hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nq, zn, zd, seed, closing);
+    hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nq, zn, zd, seed, closing, sticky);
   } else if (nq <= 4ull * SCAN_THREADS) {
-    hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, seed, closing);
+    hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, seed, closing, sticky);
   } else {
     hipLaunchKernelGGL(gp_block_reduce<F>, dim3((uint32_t)nb, g), dim3(SCAN_THREADS), 0, s, nq, zn, zd,
                        tn, td);
     if (nb <= 64)
-      hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nb, tn, td, seed, closing);
+      hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nb, tn, td, seed, closing, sticky);
     else
-      hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, tn, td, seed, closing);
+      hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, tn, td, seed, closing, sticky);
     hipLaunchKernelGGL(gp_block_down<F>, dim3((uint32_t)nb, g), dim3(DOWN_T), 0, s, nq, zn, zd, tn);
   }
   if (chain) hipLaunchKernelGGL(gp_chain_seeds<F>, dim3(1), dim3(64), 0, s, chain, post, g);

@@ -38,16 +38,16 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* d_row_begin, uint32_t n_circuits, uint64_t usable_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
-                         void* scratch, uint32_t group, hipStream_t s);
+                         void* scratch, uint32_t group, int* sticky, hipStream_t s);
 hipError_t launch_spread_table(uint64_t usable_rows, uint32_t form, uint64_t* d_out,
                                uint64_t out_rows, hipStream_t s);
-size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst);
+size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst, uint32_t chunk_len);
 hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0,
                               const uint64_t* d_inst, size_t n_inst, const uint32_t* d_pool,
                               uint32_t k, uint64_t usable_rows, const uint64_t* omega,
                               const uint64_t* delta, const uint64_t* beta, const uint64_t* gamma,
                               uint32_t chunk_len, uint32_t form, uint64_t* d_sigma, uint64_t* d_z,
-                              uint64_t out_rows, void* scratch, hipStream_t s);
+                              uint64_t out_rows, void* scratch, int* sticky, hipStream_t s);
 hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
                             uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
                             int cu_count, hipStream_t s);  // b2f_export.hip
@@ -784,7 +784,10 @@ struct b2f_ctx {
   std::map<uint32_t, std::vector<uint32_t>> pm_pat;
   std::map<uint32_t, uint64_t> pm_pool_off;  // rounds -> offset in d_pm_pool (u32 units)
   uint32_t* d_pm_pool;
-  std::vector<uint64_t> pm_inst_host;
+  uint64_t* h_pm_inst;     // pinned staging of the per-call instance table
+  size_t h_pm_inst_cap;
+  hipEvent_t pm_inst_ev;   // recorded after the table's async upload (the staging is reusable
+  bool pm_inst_ev_live;    // once it completes)
   uint64_t* d_pm_inst;
   size_t pm_inst_cap;
   void* d_pm;
@@ -1053,6 +1056,9 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
   (void)hipFree(ctx->d_pm_pool);
   (void)hipFree(ctx->d_pm_inst);
   (void)hipFree(ctx->d_pm);
+  if (ctx->pm_inst_ev_live) (void)hipEventSynchronize(ctx->pm_inst_ev);
+  if (ctx->pm_inst_ev) (void)hipEventDestroy(ctx->pm_inst_ev);
+  (void)hipHostFree(ctx->h_pm_inst);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   delete ctx;
 }
@@ -1387,7 +1393,8 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
   }
   int tk = timed_begin(ctx, B2F_KERNEL_LOOKUP, s);
   HIPCHK(ctx, launch_lookup(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, theta, beta,
-                            gamma, form, d_out, out_rows, d_first_bad, ctx->d_lk, group, s));
+                            gamma, form, d_out, out_rows, d_first_bad, ctx->d_lk, group,
+                            ctx->d_status + 2, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
@@ -1483,20 +1490,34 @@ B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, 
     HIPCHK(ctx, hipMalloc(&ctx->d_pm_pool, 4 * pool.size()));
     HIPCHK(ctx, hipMemcpy(ctx->d_pm_pool, pool.data(), 4 * pool.size(), hipMemcpyHostToDevice));
   }
-  // instance table: n + 1 circuit start rows, then n pool offsets
-  std::vector<uint64_t>& it = ctx->pm_inst_host;
-  it.assign(2 * n + 1, 0);
+  // instance table: n + 1 circuit start rows, then n pool offsets, staged in pinned host
+  // memory and uploaded asynchronously; the host waits only for the previous call's upload
+  // (so the staging can be rewritten), or for the whole stream when a device buffer grows
+  const size_t m = 2 * n + 1;
+  if (ctx->pm_inst_ev_live) {
+    HIPCHK(ctx, hipEventSynchronize(ctx->pm_inst_ev));
+    ctx->pm_inst_ev_live = false;
+  }
+  if (m > ctx->h_pm_inst_cap) {
+    if (ctx->h_pm_inst) HIPCHK(ctx, hipHostFree(ctx->h_pm_inst));
+    ctx->h_pm_inst = nullptr;
+    ctx->h_pm_inst_cap = 0;
+    HIPCHK(ctx, hipHostMalloc((void**)&ctx->h_pm_inst, 8 * m, hipHostMallocDefault));
+    ctx->h_pm_inst_cap = m;
+  }
+  if (!ctx->pm_inst_ev) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->pm_inst_ev, hipEventDisableTiming));
+  uint64_t* it = ctx->h_pm_inst;
   for (size_t i = 0; i <= n; i++) it[i] = h_offsets[i] - row0;
   for (size_t i = 0; i < n; i++) it[n + 1 + i] = ctx->pm_pool_off[need[i]];
-  const size_t need_scr = perm_scratch_bytes(k, usable_rows, n);
-  if (it.size() > ctx->pm_inst_cap || need_scr > ctx->pm_cap) {
+  const size_t need_scr = perm_scratch_bytes(k, usable_rows, n, chunk_len);
+  if (m > ctx->pm_inst_cap || need_scr > ctx->pm_cap) {
     HIPCHK(ctx, hipStreamSynchronize(s));
-    if (it.size() > ctx->pm_inst_cap) {
+    if (m > ctx->pm_inst_cap) {
       if (ctx->d_pm_inst) HIPCHK(ctx, hipFree(ctx->d_pm_inst));
       ctx->d_pm_inst = nullptr;
       ctx->pm_inst_cap = 0;
-      HIPCHK(ctx, hipMalloc(&ctx->d_pm_inst, 8 * it.size()));
-      ctx->pm_inst_cap = it.size();
+      HIPCHK(ctx, hipMalloc(&ctx->d_pm_inst, 8 * m));
+      ctx->pm_inst_cap = m;
     }
     if (need_scr > ctx->pm_cap) {
       if (ctx->d_pm) HIPCHK(ctx, hipFree(ctx->d_pm));
@@ -1506,13 +1527,14 @@ B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, 
       ctx->pm_cap = need_scr;
     }
   }
-  // the table is small; a blocking upload keeps the host vector reusable by the next call
-  HIPCHK(ctx, hipStreamSynchronize(s));
-  HIPCHK(ctx, hipMemcpy(ctx->d_pm_inst, it.data(), 8 * it.size(), hipMemcpyHostToDevice));
+  // stream-ordered after the previous call's kernels, which read the same device table
+  HIPCHK(ctx, hipMemcpyAsync(ctx->d_pm_inst, it, 8 * m, hipMemcpyHostToDevice, s));
+  HIPCHK(ctx, hipEventRecord(ctx->pm_inst_ev, s));
+  ctx->pm_inst_ev_live = true;
   int tk = timed_begin(ctx, B2F_KERNEL_PERM, s);
   HIPCHK(ctx, launch_permutation(d_advice, total_rows, row0, ctx->d_pm_inst, n, ctx->d_pm_pool, k,
                                  usable_rows, omega, delta, beta, gamma, chunk_len, form, d_sigma,
-                                 d_z, out_rows, ctx->d_pm, s));
+                                 d_z, out_rows, ctx->d_pm, ctx->d_status + 2, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
@@ -1558,6 +1580,8 @@ B2F_API int b2f_sync(b2f_ctx* ctx, void* stream) {
   if (bits & (1 << B2F_ERR_ROUNDS)) return set_err(ctx, B2F_ERR_ROUNDS, "rounds > %u", B2F_MAX_ROUNDS);
   if (bits & (1 << B2F_ERR_LAYOUT))
     return set_err(ctx, B2F_ERR_LAYOUT, "row offsets are not the LAYOUT v1 prefix sums");
+  if (bits & (1 << B2F_ERR_FIELD))
+    return set_err(ctx, B2F_ERR_FIELD, "a grand product's denominator is zero (challenge collision)");
   return B2F_OK;
 }
 

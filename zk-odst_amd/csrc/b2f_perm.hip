@@ -24,13 +24,13 @@
 
 namespace b2f {
 
-size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst);
+size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst, uint32_t chunk_len);
 hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0,
                               const uint64_t* d_inst, size_t n_inst, const uint32_t* d_pool,
                               uint32_t k, uint64_t usable_rows, const uint64_t* omega,
                               const uint64_t* delta, const uint64_t* beta, const uint64_t* gamma,
                               uint32_t chunk_len, uint32_t form, uint64_t* d_sigma, uint64_t* d_z,
-                              uint64_t out_rows, void* scratch, hipStream_t s);
+                              uint64_t out_rows, void* scratch, int* sticky, hipStream_t s);
 
 namespace {
 
@@ -174,7 +174,9 @@ struct Carve {
   size_t total;
 };
 
-Carve carve(void* base, uint32_t k, uint64_t usable) {
+// num, den and the grand-product scratch hold one slice per column set: ceil(8 / chunk_len)
+// of them (3 for halo2's usual chunk_len 3), not one per column
+Carve carve(void* base, uint32_t k, uint64_t usable, uint32_t sets) {
   Carve m;
   char* p = (char*)base;
   size_t off = 0;
@@ -187,10 +189,10 @@ Carve carve(void* base, uint32_t k, uint64_t usable) {
   m.OL = (Fe*)take(sizeof(Fe) * NCOL * LO);
   m.BL = (Fe*)take(sizeof(Fe) * NCOL * LO);
   m.OH = (Fe*)take(sizeof(Fe) * n_hi);
-  m.num = (Fe*)take(sizeof(Fe) * gp::elems(usable) * NCOL);  // one slice per column set (<= 8)
-  m.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * NCOL);
-  m.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * NCOL);
-  m.seed = (Fe*)take(sizeof(Fe) * 2 * NCOL);
+  m.num = (Fe*)take(sizeof(Fe) * gp::elems(usable) * sets);
+  m.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * sets);
+  m.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * sets);
+  m.seed = (Fe*)take(sizeof(Fe) * 2 * sets);
   m.total = off;
   return m;
 }
@@ -199,8 +201,9 @@ template <class F>
 hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0, const Inst& I,
                     const uint32_t* d_pool, uint32_t k, uint64_t usable, const Params& prm,
                     const uint64_t* gamma, uint32_t chunk_len, bool mont, uint64_t* d_sigma,
-                    uint64_t* d_z, uint64_t out_rows, void* scratch, hipStream_t s) {
-  Carve m = carve(scratch, k, usable);
+                    uint64_t* d_z, uint64_t out_rows, void* scratch, int* sticky, hipStream_t s) {
+  const uint32_t sets = (NCOL + chunk_len - 1) / chunk_len;
+  Carve m = carve(scratch, k, usable, sets);
   const uint64_t n_rows = 1ull << k, n_hi = n_rows / LO;
   const uint64_t tab = n_hi > (uint64_t)NCOL * LO ? n_hi : (uint64_t)NCOL * LO;
   hipLaunchKernelGGL(pm_table_kernel<F>, dim3((uint32_t)((tab + 255) / 256)), dim3(256), 0, s, prm,
@@ -212,20 +215,19 @@ hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0
   for (int i = 0; i < 4; i++) pg.beta[i] = gamma[i];
   // every column set's factors in one launch, then their grand products side by side,
   // chained (set c starts where set c - 1 closed)
-  const uint32_t sets = (NCOL + chunk_len - 1) / chunk_len;
   hipLaunchKernelGGL(pm_factor_kernel<F>, dim3((uint32_t)((usable + 255) / 256), sets), dim3(256), 0, s,
                      I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, pg, m.num,
                      m.den);
   hipError_t e = gp::run<F>(sets, usable, mont, d_z, out_rows * 4, m.num, m.den, m.zs, nullptr,
-                            nullptr, s, m.seed);
+                            nullptr, s, m.seed, sticky);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 
 }  // namespace
 
-size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t) {
-  return carve(nullptr, k, usable_rows).total;
+size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t, uint32_t chunk_len) {
+  return carve(nullptr, k, usable_rows, (NCOL + chunk_len - 1) / chunk_len).total;
 }
 
 // d_inst: n + 1 circuit start rows, then n pool offsets
@@ -234,7 +236,7 @@ hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uin
                               uint32_t k, uint64_t usable_rows, const uint64_t* omega,
                               const uint64_t* delta, const uint64_t* beta, const uint64_t* gamma,
                               uint32_t chunk_len, uint32_t form, uint64_t* d_sigma, uint64_t* d_z,
-                              uint64_t out_rows, void* scratch, hipStream_t s) {
+                              uint64_t out_rows, void* scratch, int* sticky, hipStream_t s) {
   Params prm;
   for (int i = 0; i < 4; i++) {
     prm.omega[i] = omega[i];
@@ -248,9 +250,9 @@ hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uin
   const bool mont = (form & 1u) != 0;
   if (form >> 1)
     return run_perm<field::Bn254>(d_advice, total_rows, row0, I, d_pool, k, usable_rows, prm, gamma,
-                                  chunk_len, mont, d_sigma, d_z, out_rows, scratch, s);
+                                  chunk_len, mont, d_sigma, d_z, out_rows, scratch, sticky, s);
   return run_perm<field::Pallas>(d_advice, total_rows, row0, I, d_pool, k, usable_rows, prm, gamma,
-                                 chunk_len, mont, d_sigma, d_z, out_rows, scratch, s);
+                                 chunk_len, mont, d_sigma, d_z, out_rows, scratch, sticky, s);
 }
 
 }  // namespace b2f
