@@ -85,6 +85,8 @@ def cpu_baseline(rounds, mix, target_s, threads):
     import oracle
     from b2f import synth
 
+    flags = oracle.use_fastest_build()  # x86-64-v4 (AVX-512) where the host has it
+
     chunk = max(2048, 64 * threads)  # ~0.5 GB of trace per 2,048 instances: memory bounded
 
     def run(seed, n, nt):
@@ -111,6 +113,7 @@ def cpu_baseline(rounds, mix, target_s, threads):
     hc = host_cpus()
     eff = rate / (threads * single)
     out = {"value": round(rate, 1), "unit": "compressions/s", "cores": threads, "kind": "port",
+           "build": "gcc " + flags,
            "single_thread": round(single, 1), "scaling_efficiency": round(eff, 3),
            "host_cpus": hc["logical"], "host": hc,
            "sample": "%d x %s-round compressions in chunks of %d, oracle fill + eval "

@@ -43,6 +43,30 @@ class Report(ctypes.Structure):
 
 
 _lib = None
+V4_PATH = os.path.join(HERE, "liboracle_b2f_v4.so")
+V4_FLAGS = "-O3 -march=x86-64-v4 -mtune=znver3 -fopenmp"
+V2_FLAGS = "-O3 -march=x86-64-v2 -mtune=generic -fopenmp"
+
+
+def host_has_avx512():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("flags"):
+                    f = set(line.split(":", 1)[1].split())
+                    return {"avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl"} <= f
+    except OSError:
+        pass
+    return False
+
+
+def use_fastest_build():
+    """Bind the x86-64-v4 build when the host has AVX-512 (before the first call); returns the
+    compiler flags of the build in use. For bench.py's CPU baseline only."""
+    global LIB_PATH
+    if _lib is None and host_has_avx512() and os.path.exists(V4_PATH):
+        LIB_PATH = V4_PATH
+    return V4_FLAGS if LIB_PATH == V4_PATH else V2_FLAGS
 
 
 def build():

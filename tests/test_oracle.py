@@ -4,7 +4,7 @@ CPU only. The oracle is test infrastructure (oracle/b2f_oracle.h)."""
 import numpy as np
 import pytest
 
-from conftest import random_inputs, words
+from conftest import ROOT, random_inputs, words
 
 
 def _orc_inputs(x, orc):
@@ -248,3 +248,30 @@ def test_oracle_under_host_sanitizers():
                        timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-500:], r.stderr[-2000:])
     assert "asan_check ok" in r.stdout
+
+
+def test_v4_build_matches_the_checker_build(orc):
+    """bench.py's CPU baseline may run the x86-64-v4 (AVX-512) build of the same source; it must
+    compute what the x86-64-v2 checker build computes (run in a fresh interpreter so it binds
+    the other library)."""
+    import hashlib
+    import subprocess
+    import sys
+
+    if not orc.host_has_avx512():
+        pytest.skip("host without AVX-512")
+    x = random_inputs(40, (0, 1, 4, 12), 77)
+    ox = np.frombuffer(x.tobytes(), dtype=orc.INPUT_DTYPE).copy()
+    adv, fixed, h, off = orc.fill(ox)
+    want = hashlib.sha256(adv.tobytes() + fixed.tobytes() + h.tobytes()).hexdigest()
+    code = ("import sys, hashlib, numpy as np; sys.path.insert(0, %r); import oracle\n"
+            "print(oracle.use_fastest_build())\n"
+            "x = np.frombuffer(bytes.fromhex(sys.stdin.read()), dtype=oracle.INPUT_DTYPE).copy()\n"
+            "a, f, h, o = oracle.fill(x)\n"
+            "print(oracle.LIB_PATH); print(hashlib.sha256(a.tobytes() + f.tobytes() + h.tobytes()).hexdigest())"
+            ) % (ROOT + "/oracle")
+    out = subprocess.run([sys.executable, "-c", code], input=ox.tobytes().hex(), capture_output=True,
+                         text=True, timeout=120)
+    lines = out.stdout.split()
+    assert "x86-64-v4" in out.stdout and lines[-2].endswith("liboracle_b2f_v4.so"), out.stdout + out.stderr
+    assert lines[-1] == want

@@ -131,7 +131,7 @@ def blake2b_batch(engine, messages, digest_size=64, key=b"", path="fused", devic
     return run_plan(engine, Plan(messages, digest_size, key), path, device, stream)
 
 
-def run_plan(engine, plan, path="fused", device="cuda:0", stream=None):
+def run_plan(engine, plan, path="fused", device="cuda:0", stream=None, _diag=None):
     """The device half of blake2b_batch for a prebuilt Plan. The blocks go up in one
     asynchronous copy from page-locked memory (Plan.pinned), every block step runs on the
     stream, and only the final chaining values come back to the host."""
@@ -169,6 +169,8 @@ def run_plan(engine, plan, path="fused", device="cuda:0", stream=None):
         d_blocks.copy_(p_blocks, non_blocking=True)
         d_t.copy_(p_t, non_blocking=True)
         d_f.copy_(p_f, non_blocking=True)
+    if _diag is not None and _diag.get("sync_upload"):  # diagnostics (tools/hasher_race.py)
+        torch.cuda.synchronize(dev)
     for j in range(plan.steps):
         a = int(plan.active[j])
         s0 = int(plan.start[j])
@@ -195,7 +197,10 @@ def run_plan(engine, plan, path="fused", device="cuda:0", stream=None):
         raw = report.cpu().numpy().view(np.uint64)
     reps = [_lib.EvalReport.from_buffer_copy(raw[j].tobytes()).as_dict()
             for j in range(plan.steps)]
-    return ChainResult(plan, reps, fin_host)
+    res = ChainResult(plan, reps, fin_host)
+    if _diag is not None:  # diagnostics: every step's h' (step-major, sorted order)
+        res.all_h = hs.cpu().numpy().view(np.uint64)
+    return res
 
 
 class Blake2f:
