@@ -19,6 +19,21 @@ def _np_ptr(a):
     return ctypes.c_void_p(a.ctypes.data)
 
 
+def upload(a, device, dtype=None):
+    """Host array -> device tensor as an asynchronous copy from page-locked memory on the current
+    stream, ordered before every later launch on that stream. A copy from pageable memory
+    (tensor.to(device)) is not: measured on MI355X, the tail of such a copy could still be in
+    flight when the next kernel on the same stream read it (tools/hasher_race.py: the last
+    instance of a batch read a stale h0 row; a host synchronize hid it). The page-locked block
+    stays alive until the copy is done (torch's host allocator records the stream)."""
+    import torch
+
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.view(dtype)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 class Engine:
     """Wraps b2f_create/b2f_destroy and the fill/eval entry points."""
 
@@ -206,8 +221,8 @@ class DeviceBatch:
                                 % (self.total_rows, self.used_rows))
         dev = torch.device(device)
         raw = np.frombuffer(inputs.tobytes(), dtype=np.uint8)
-        self.inputs = torch.from_numpy(raw.copy()).to(dev)
-        self.offsets = torch.from_numpy(off.view(np.int64).copy()).to(dev)
+        self.inputs = upload(raw, dev)
+        self.offsets = upload(off.view(np.int64), dev)
         self.advice = torch.empty((_lib.NUM_ADVICE, self.total_rows), dtype=torch.int32, device=dev)
         self.fixed = torch.empty(self.total_rows, dtype=torch.int32, device=dev)
         self.h_out = torch.empty((self.n, 8), dtype=torch.int64, device=dev)
@@ -255,7 +270,7 @@ class DeviceBatch:
         [n_circuits]) -- see b2f_lookup_columns_dev."""
         torch = self.torch
         dev = self.advice.device
-        rb = torch.tensor([int(r) for r in row_begin], dtype=torch.int64, device=dev)
+        rb = upload(np.array([int(r) for r in row_begin], dtype=np.int64), dev)
         nc = len(row_begin)
         out = torch.empty((nc, 5, usable_rows + 1, 4), dtype=torch.int64, device=dev)
         bad = torch.empty(nc, dtype=torch.int64, device=dev)

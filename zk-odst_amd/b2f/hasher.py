@@ -72,16 +72,23 @@ class Plan:
             self.f[idx[-1]] = 1
 
     def pinned(self):
-        """The plan's blocks, counters and flags as page-locked host tensors (built once and
-        cached), so their upload is one asynchronous DMA."""
+        """The plan's blocks, counters, flags, initial states and the row of every message's
+        final h' (step-major), as page-locked host tensors (built once and cached), so every
+        upload is an asynchronous DMA ordered on the stream (engine.upload explains why a
+        pageable copy is not)."""
         if not hasattr(self, "_pinned"):
             import torch
 
             def pin(a):
                 a = np.ascontiguousarray(a)
-                return torch.from_numpy(a.view(np.int64 if a.dtype == np.uint64 else np.int32)).pin_memory()
+                return torch.from_numpy(a.view(np.int64 if a.dtype in (np.uint64, np.int64)
+                                               else np.int32)).pin_memory()
 
-            self._pinned = (pin(self.blocks), pin(self.t), pin(self.f))
+            h0 = np.broadcast_to(self.h0, (self.n, 8))
+            # message at sorted position p ends at step nblocks - 1, i.e. at row start[nb - 1] + p
+            last = (self.active[None, :] > np.arange(self.n)[:, None]).sum(1) - 1
+            fin = (self.start[last] + np.arange(self.n)).astype(np.int64)
+            self._pinned = (pin(self.blocks), pin(self.t), pin(self.f), pin(h0), pin(fin))
         return self._pinned
 
     def step(self, j):
@@ -145,20 +152,21 @@ def run_plan(engine, plan, path="fused", device="cuda:0", stream=None, _diag=Non
     dev = torch.device(device)
     s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
     compute = torch.cuda.ExternalStream(s, device=dev)
-    p_blocks, p_t, p_f = plan.pinned()
+    p_blocks, p_t, p_f, p_h0, p_fin = plan.pinned()
     R = rows(BLAKE2B_ROUNDS)
-    # Everything is allocated, copied and launched on the one stream `s`: torch's caching
-    # allocator hands a freed block to a new tensor of the same stream without a host wait, so
-    # the allocations must be made under `compute` too, or a block still read by an earlier
-    # launch on `s` could be handed to an allocation of another stream and overwritten early.
-    # No host synchronize is needed (tests/test_gpu_hasher.py runs split right after fused).
+    # Everything is allocated, copied and launched on the one stream `s`, and every host ->
+    # device copy is from page-locked memory (a pageable copy's tail was measured still in
+    # flight when the first launch read it: the last instance of step 0 got a stale h0 row;
+    # engine.upload). No host synchronize is needed (tests/test_gpu_hasher.py runs batches back
+    # to back on alternating paths).
     with torch.cuda.stream(compute):
         d_blocks = torch.empty(p_blocks.shape, dtype=p_blocks.dtype, device=dev)
         d_t = torch.empty(p_t.shape, dtype=p_t.dtype, device=dev)
         d_f = torch.empty(p_f.shape, dtype=p_f.dtype, device=dev)
         # h' of every compression, step-major like the plan: step j's outputs are rows
         # start[j] .. start[j] + active[j] - 1, and step j + 1 reads its h from that prefix
-        h0 = torch.from_numpy(np.broadcast_to(plan.h0, (n, 8)).copy().view(np.int64)).to(dev)
+        h0 = p_h0.to(dev, non_blocking=True)
+        fin_idx = p_fin.to(dev, non_blocking=True)
         offsets = torch.arange(n + 1, dtype=torch.int64, device=dev) * R
         hs = torch.empty((int(plan.start[-1]), 8), dtype=torch.int64, device=dev)
         inputs = torch.empty(n * 216, dtype=torch.uint8, device=dev)
@@ -189,11 +197,8 @@ def run_plan(engine, plan, path="fused", device="cuda:0", stream=None, _diag=Non
             engine.eval_dev(advice.data_ptr(), fixed.data_ptr(), offsets.data_ptr(), a, total,
                             report[j].data_ptr(), s)
     engine.sync(s)
-    # message at sorted position p ends at step nblocks - 1, i.e. at row start[nb - 1] + p
-    last = (plan.active[None, :] > np.arange(n)[:, None]).sum(1) - 1
     with torch.cuda.stream(compute):
-        idx = torch.from_numpy((plan.start[last] + np.arange(n)).astype(np.int64)).to(dev)
-        fin_host = hs.index_select(0, idx).cpu().numpy().view(np.uint64)
+        fin_host = hs.index_select(0, fin_idx).cpu().numpy().view(np.uint64)
         raw = report.cpu().numpy().view(np.uint64)
     reps = [_lib.EvalReport.from_buffer_copy(raw[j].tobytes()).as_dict()
             for j in range(plan.steps)]

@@ -401,90 +401,6 @@ __device__ Fe inv_kaliski(const Fe& a) {
   return mul<F>(mul<F>(X, Y), fe_const<F>(F::R2));
 }
 
-namespace detail {
-// scalar-friendly forms of the word operations (no v_alignbit: a 64-bit shift of the word pair,
-// which the scalar unit has), for values every lane of the wave holds alike
-__device__ __forceinline__ void shr_n_s(uint32_t (&u)[8], uint32_t sh) {
-#pragma unroll
-  for (int i = 0; i < 7; i++) u[i] = (uint32_t)((((uint64_t)u[i + 1] << 32) | u[i]) >> sh);
-  u[7] >>= sh;
-}
-__device__ __forceinline__ void shl_n_s(uint32_t (&u)[8], uint32_t sh) {
-#pragma unroll
-  for (int i = 7; i > 0; i--) u[i] = (uint32_t)((((uint64_t)u[i] << 32) | u[i - 1]) << sh >> 32);
-  u[0] <<= sh;
-}
-}  // namespace detail
-
-// inv_kaliski for a wave-uniform element, written for the scalar unit: the caller makes `a`
-// uniform (readfirstlane of every word) and the whole wave runs it. Every step's values are then
-// uniform, so the compiler keeps u, v, r, s in SGPRs and the ~270 steps run as scalar
-// instructions (one issue per cycle) instead of one lane's vector instructions (a wave64 vector
-// instruction occupies the SIMD for 4 cycles, and a lone wave waits out each dependency).
-template <class F>
-__device__ Fe inv_uniform(const Fe& a) {
-  using namespace detail;
-  uint32_t u[8], v[8], r[8], s[8], pm[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    pm[i] = F::P[i];
-    u[i] = F::P[i];
-    v[i] = __builtin_amdgcn_readfirstlane(a.w[i]);
-    r[i] = 0;
-    s[i] = 0;
-  }
-  s[0] = 1;
-  uint32_t k = 0;
-#pragma unroll 1
-  for (uint32_t it = 0; it < 512 && nonzero(v); it++) {
-    if (!(u[0] & 1u)) {
-      const uint32_t tz = u[0] ? (uint32_t)__builtin_ctz(u[0]) : 31u;
-      shr_n_s(u, tz);
-      shl_n_s(s, tz);
-      k += tz;
-    } else if (!(v[0] & 1u)) {
-      const uint32_t tz = v[0] ? (uint32_t)__builtin_ctz(v[0]) : 31u;
-      shr_n_s(v, tz);
-      shl_n_s(r, tz);
-      k += tz;
-    } else if (!geq(v, u)) {
-      sub_to(u, v);
-      shr_n_s(u, 1);
-      add_to(r, s);
-      shl_n_s(s, 1);
-      k += 1;
-    } else {
-      sub_to(v, u);
-      shr_n_s(v, 1);
-      add_to(s, r);
-      shl_n_s(r, 1);
-      k += 1;
-    }
-  }
-  if (geq(r, pm)) sub_to(r, pm);
-  uint32_t x[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) x[i] = pm[i];
-  sub_to(x, r);
-  const uint32_t j = 512u - k;
-  const uint32_t j0 = j < 253u ? j : 253u;
-  uint32_t y[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) y[i] = (uint32_t)(i == (int)(j0 >> 5)) << (j0 & 31u);
-#pragma unroll 1
-  for (uint32_t d = j0; d < j; d++) {
-    shl_n_s(y, 1);
-    if (geq(y, pm)) sub_to(y, pm);
-  }
-  Fe X, Y;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    X.w[i] = x[i];
-    Y.w[i] = y[i];
-  }
-  return mul<F>(mul<F>(X, Y), fe_const<F>(F::R2));
-}
-
 __device__ __forceinline__ bool is_zero(const Fe& a) {
   uint32_t o = 0;
 #pragma unroll

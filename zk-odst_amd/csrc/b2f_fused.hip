@@ -941,6 +941,46 @@ constexpr uint32_t psel(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
 }
 constexpr uint32_t limb_sel(uint32_t k) { return psel(2 * k, 2 * k + 1, 12, 12); }  // on (hi, lo)
 
+// The ADD block each lane checks in the fast checks (every lane checks one of the tile's 16 ADD
+// blocks, i = 4 G + kind). ds_read_b128 serves a wave in four 16-lane groups, a lane's 16 bytes on
+// banks (a / 4) mod 64 .. +3; the blocks' first rows mod 64 are 0 12 28 40 | 52 0 16 28 | 40 52 4 16
+// | 28 40 56 4, so one lane per block within a group is up to 4-way conflicted. Instead each group
+// reads four blocks whose bank ranges are disjoint, each by four lanes (the same address:
+// broadcast): {0 16 28 52} {0 16 40 52} {4 12 28 40} {4 28 40 56} by first row mod 64.
+struct AddBlk {
+  uint32_t b[64];
+};
+constexpr AddBlk make_add_blk() {
+  AddBlk T{};
+  const uint32_t sets[4][4] = {{0, 6, 2, 4}, {5, 11, 3, 9}, {10, 1, 7, 8}, {15, 12, 13, 14}};
+  // ds_read_b128 lane groups, in lane order
+  const uint32_t grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                               {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                               {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                               {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+  for (uint32_t g = 0; g < 4; g++)
+    for (uint32_t k = 0; k < 16; k++) T.b[grp[g][k]] = sets[g][k & 3u];
+  return T;
+}
+constexpr bool add_blk_ok() {  // every block covered; bank ranges disjoint inside each group
+  const AddBlk T = make_add_blk();
+  uint32_t seen = 0;
+  for (uint32_t l = 0; l < 64; l++) seen |= 1u << T.b[l];
+  if (seen != 0xffffu) return false;
+  const uint32_t off[4] = {0, 12, 28, 40};
+  const uint32_t sets[4][4] = {{0, 6, 2, 4}, {5, 11, 3, 9}, {10, 1, 7, 8}, {15, 12, 13, 14}};
+  for (uint32_t g = 0; g < 4; g++)
+    for (uint32_t a = 0; a < 4; a++)
+      for (uint32_t b = a + 1; b < 4; b++) {
+        const uint32_t ra = (52 * (sets[g][a] >> 2) + off[sets[g][a] & 3u]) % 64;
+        const uint32_t rb = (52 * (sets[g][b] >> 2) + off[sets[g][b] & 3u]) % 64;
+        if (ra < rb + 4 && rb < ra + 4) return false;
+      }
+  return true;
+}
+static_assert(add_blk_ok(), "ADD block lane map: all 16 blocks, conflict-free groups");
+__constant__ AddBlk c_add_blk = make_add_blk();
+
 // Per quad position p: the byte selectors of every cell of the quad (LAYOUT.md §4, the same
 // recipes as make_rows / quad_round).
 struct QuadProg {
@@ -1213,8 +1253,11 @@ __device__ __forceinline__ Lane make_lane(uint32_t lane, uint32_t Sb) {
     L.gsF = kind == 1 ? 8u : 1u;
     L.gsH = kind == 1 ? 16u : 2u;
   }
-  {  // ADD block lane & 15: a1 +0, c1 +12, a2 +28, c2 +40 of G (lane >> 2) & 3
-    const uint32_t w4 = lane & 3u, r = 52 * ((lane >> 2) & 3u) + (w4 == 0 ? 0u : w4 == 1 ? 12u : w4 == 2 ? 28u : 40u);
+  {  // ADD block i = c_add_blk[lane] (a1 +0, c1 +12, a2 +28, c2 +40 of G i >> 2): every
+     // ds_read_b128 lane group reads 4 blocks whose 16-byte bank ranges are disjoint, each by 4
+     // lanes (one address: a broadcast) -- conflict-free
+    const uint32_t i = c_add_blk.b[lane], w4 = i & 3u;
+    const uint32_t r = 52 * (i >> 2) + (w4 == 0 ? 0u : w4 == 1 ? 12u : w4 == 2 ? 28u : 40u);
     L.ar = Sb + 4 * r;
     L.m3 = (w4 & 1u) ? 0u : ~0u;  // ADD3: a_5 is an operand
   }
@@ -1495,26 +1538,46 @@ auto put = [&](int col, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
       // in issue order, so placed after this tile's 11 stores it is vmcnt(11) -- the load and
       // the PREVIOUS tile's stores, issued a tile ago -- never a wait for these stores
       tick(3);
-      store_staged<MODE>(S, lane, HR_Q, c.row0, adv, fixed, total_rows);
+      // the stores read each staged column of the lane's quad into registers; the lookup and
+      // fixed checks below use those registers (the cells as stored), not a second LDS read.
+      // Lanes 52-63 read quads 0-11 again (their stores fall past the tile's range and are
+      // dropped): those quads' checks, which the lane programs of K are built for.
+      uint4 cq0, cq1, cq2, cfx;
+      const uint32_t ls = lane < HR_Q ? lane : lane - HR_Q;
+      auto store_cols = [&](int lo, int hi) {
+#pragma unroll
+        for (int col = 0; col < NSTAGE; col++) {
+          if (col < lo || col >= hi) continue;
+          const uint4 v = *reinterpret_cast<const uint4*>(S + col * STR + 4 * ls);
+          if (col == A0) cq0 = v;
+          if (col == A1) cq1 = v;
+          if (col == A2) cq2 = v;
+          if (col == FXC) cfx = v;
+          if (MODE & FZ_STORE)
+            tile_store((col < 10 ? adv + (uint64_t)col * total_rows : fixed) + c.row0, HR_Q, lane, v);
+        }
+      };
+#ifndef B2F_HR_SPLITST
+#define B2F_HR_SPLITST NSTAGE
+#endif
+      // diagnostics: B2F_HR_SPLITST < 11 stores the first columns before the checks and the rest
+      // between the gate checks and the copies (a store stream spread over the checks)
+      constexpr int SPLIT = B2F_HR_SPLITST;
+      store_cols(0, SPLIT);
       tick(4);
 #ifndef B2F_HR_SETTLE_EARLY
-      asm volatile("" ::"v"(Pn));
+      if (SPLIT == NSTAGE) asm volatile("" ::"v"(Pn));
 #endif
       tick(7);
       // ---- 6. fast checks: acc |= (every identity's lhs ^ rhs) -- hr_fast_checks, kept inline
       // here: called as a function it moved the register allocation (hot-loop spill reloads)
       uint32_t acc = 0;
-      if (MODE & (FZ_LOOKUP | FZ_GATES)) {
-        const uint4 q0 = ld128(K.aQ + 4 * A0 * STR), q1 = ld128(K.aQ + 4 * A1 * STR), q2 = ld128(K.aQ + 4 * A2 * STR);
-        const uint4 fx = ld128(K.aQ + 4 * FXC * STR);
-        if (MODE & FZ_LOOKUP) {
+      if (MODE & FZ_LOOKUP) {
 #pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const uint32_t de = comp(q1, j);
-            acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(q0, j)) | (spread_t(TB, de) ^ comp(q2, j));
-          }
+        for (int j = 0; j < 4; j++) {
+          const uint32_t de = comp(cq1, j);
+          acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(cq0, j)) | (spread_t(TB, de) ^ comp(cq2, j));
         }
-        if (MODE & FZ_GATES) acc |= (fx.x ^ K.fx0) | fx.y | fx.z | fx.w;
       }
       if (MODE & FZ_GATES) {
         {  // XOR / XOR24 / XOR63 limb item
@@ -1531,7 +1594,7 @@ auto put = [&](int col, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
           const uint32_t G = sel32(K.gm24, E2, E);
           acc |= (((E + (F << K.gsF)) ^ w7) | ((G + (H << K.gsH)) ^ w8)) & K.grs;
         }
-        {  // ADD block (lanes 16-63 repeat lanes 0-15)
+        {  // ADD block (c_add_blk: each lane one of the 16, 4 lanes per block)
           const uint4 s = ld128(K.ar + 4 * A1 * STR), x = ld128(K.ar + 4 * A3 * STR);
           const uint4 y = ld128(K.ar + 4 * A4 * STR), z = ld128(K.ar + 4 * A5 * STR);
           const uint32_t a9 = ld32(K.ar + 4 * A9 * STR);
@@ -1545,6 +1608,11 @@ auto put = [&](int col, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
           acc |= (uint32_t)cy ^ a9;
         }
       }
+      if (SPLIT < NSTAGE) {
+        store_cols(SPLIT, NSTAGE);
+        asm volatile("" ::"v"(Pn));
+      }
+      if (MODE & FZ_GATES) acc |= (cfx.x ^ K.fx0) | cfx.y | cfx.z | cfx.w;
       if (MODE & FZ_COPIES) {
         const bool odd = c.hr & 1u;
 #pragma unroll

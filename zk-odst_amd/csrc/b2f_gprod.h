@@ -106,11 +106,12 @@ __global__ __launch_bounds__(T) void gp_scan(uint64_t nq, Fe* __restrict__ zn,
     __syncthreads();
   }
   const Fe s = seed ? seed[c] : field::one<F>();
-  if (__builtin_amdgcn_readfirstlane(t) < 64) {  // wave 0, all lanes: the inversion on the scalar unit
-    const Fe di = field::inv_uniform<F>(sd[0]);  // sd[0] = D
-    if (t == 0) dinv = di;
-  }
   if (t == 0) {
+#ifdef B2F_INV_EUCLID  // diagnostics: the plain binary extended Euclid
+    dinv = field::inv<F>(sd[0]);  // sd[0] = D
+#else
+    dinv = field::inv_kaliski<F>(sd[0]);  // sd[0] = D
+#endif
     // D = 0: some den factor is zero (a challenge collides with a cell value). halo2's
     // batch_invert would leave that entry zero and the proof would fail; here every z would
     // come from a meaningless inverse, so the call reports B2F_ERR_FIELD at b2f_sync instead.
@@ -263,17 +264,10 @@ __host__ __device__ inline uint64_t scratch_elems(uint64_t usable) {
 // (2 g elements of scratch) the products are chained -- product c starts from product c - 1's
 // closing value, product 0 from 1 -- and still scanned side by side: their single inversions
 // run in parallel, the seeds are applied in gp_write.
-// Where gp::run keeps the chunk totals in its scratch (a caller that computes them itself, as
-// the lookup's permute pass does, writes them there and passes totals_done).
-__host__ __device__ inline Fe* zn_of(Fe* zs) { return zs; }
-__host__ __device__ inline Fe* zd_of(Fe* zs, uint32_t g, uint64_t usable) {
-  return zs + (uint64_t)g * n_chunks(usable);
-}
-
 template <class F>
 hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_t z_stride,
                Fe* num, const Fe* den, Fe* zs, const Fe* seed, Fe* closing, hipStream_t s,
-               Fe* chain = nullptr, int* sticky = nullptr, bool totals_done = false) {
+               Fe* chain = nullptr, int* sticky = nullptr) {
   Fe* post = nullptr;
   if (chain) {
     seed = nullptr;
@@ -286,8 +280,7 @@ hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_
   Fe* tn = zd + (uint64_t)g * nq;
   Fe* td = tn + (uint64_t)g * nb;
   const uint32_t zq = (uint32_t)((nq + 255) / 256);
-  if (!totals_done)  // num -> the chunks' num prefixes in place, chunk totals -> zn, zd
-    hipLaunchKernelGGL(gp_chunk<F>, dim3(zq, g), dim3(256), 0, s, usable, num, den, zn, zd);
+  hipLaunchKernelGGL(gp_chunk<F>, dim3(zq, g), dim3(256), 0, s, usable, num, den, zn, zd);
   if (nq <= 64) {
     hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nq, zn, zd, seed, closing, sticky);
   } else if (nq <= 4ull * SCAN_THREADS) {

@@ -17,14 +17,13 @@
 //   scan:    in rank order, run starts pos[r] (exclusive prefix of counts), D[r] (runs up to
 //            and including r) and LP[r] (exclusive prefix of leftover table multiplicities), 16
 //            workgroups per circuit (part totals, then each part's scan);
-//   permute: row p of A' is Ts[r] for the run r holding p; a run start gets S'[p] = Ts[r];
-//            the j-th repeated row gets leftover item L - 1 - j (halo2 hands leftovers out in
-//            ascending order, each to the last open repeated row). One thread walks a 16-row
-//            chunk: one search of pos (and of LP) per chunk, then runs walked in order;
-//   z:       the same pass computes each row's factors num = (A + beta)(S + gamma) and
-//            den = (A' + beta)(S' + gamma) and the chunk's running products (the grand
-//            product's first pass); the rest of the grand product (b2f_gprod.h: one
-//            inversion per circuit) writes the z column. 6 products per row in all.
+//   permute: row p of A' is Ts[r] for the run r holding p (binary search of pos); a run
+//            start gets S'[p] = Ts[r]; the j-th repeated row gets leftover item L - 1 - j
+//            (halo2 hands leftovers out in ascending order, each to the last open repeated
+//            row), found by binary search of LP;
+//   z:       the permute pass also writes each row's factors num = (A + beta)(S + gamma) and
+//            den = (A' + beta)(S' + gamma); the grand product over them (b2f_gprod.h: one
+//            inversion per circuit, 4 products per row) writes the z column.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -317,17 +316,6 @@ __device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, cons
   return 16 * lo + n;
 }
 
-// The permute pass fused with the grand product's first pass: one thread per ZC-row chunk q
-// (rows 16 q .. 16 q + 15), walking its rows in order. A' is the run holding row p: one search
-// of pos at the chunk's first row, then the run index only moves forward (runs of empty ranks
-// -- table values absent from the circuit -- are stepped over, at most WALK of them before a
-// fresh search). S' of a repeated row is leftover item n_left - 1 - j (j = repeated rows before
-// it), so as p grows the leftover rank only moves backward: one search at the chunk's first
-// repeated row, then the same bounded walk. Per row it writes A, S, A', S', the grand product's
-// den factor and the chunk's running num prefix Nloc (chunk-interleaved, b2f_gprod.h); per chunk
-// the num and den totals -- what gp_chunk would compute from stored num/den, which are never
-// written. 4 products per row (num, den, the two running products).
-constexpr uint32_t WALK = 12;
 template <class F>
 __global__ __launch_bounds__(256) void lk_permute_kernel(
     const uint32_t* __restrict__ adv, uint64_t total_rows, const uint64_t* __restrict__ row_begin,
@@ -335,9 +323,18 @@ __global__ __launch_bounds__(256) void lk_permute_kernel(
     const uint32_t* __restrict__ pos, const uint32_t* __restrict__ dcnt,
     const uint32_t* __restrict__ lp, const uint32_t* __restrict__ samp, bool mont,
     uint64_t* __restrict__ out, uint64_t out_rows, Chal ch, Fe* __restrict__ num,
-    Fe* __restrict__ den, Fe* __restrict__ zn, Fe* __restrict__ zd) {
+    Fe* __restrict__ den) {
   const uint32_t c = blockIdx.y;
+  const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
+  const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
+  Fe* nm = num + (uint64_t)c * gp::elems(usable);
+  Fe* dn = den + (uint64_t)c * gp::elems(usable);
   const uint64_t nq = gp::n_chunks(usable);
+  const Circ k = circ(row_begin, total_rows, usable, c0 + c);
+  const uint32_t* P = pos + (uint64_t)c * TROWS;
+  const uint32_t* D = dcnt + (uint64_t)c * TROWS;
+  const uint32_t* L = lp + (uint64_t)c * TROWS;
+  const uint32_t n_left = (uint32_t)usable - D[TROWS - 1];
   __shared__ uint32_t sP[SAMPLE], sL[SAMPLE];
   {
     const uint4* sa = reinterpret_cast<const uint4*>(samp + (uint64_t)c * 2 * SAMPLE);
@@ -349,70 +346,29 @@ __global__ __launch_bounds__(256) void lk_permute_kernel(
     }
   }
   __syncthreads();
-  const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (q >= nq) return;
-  const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
-  const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
-  Fe* nm = num + (uint64_t)c * gp::elems(usable);
-  Fe* dn = den + (uint64_t)c * gp::elems(usable);
-  const Circ k = circ(row_begin, total_rows, usable, c0 + c);
-  const uint32_t* P = pos + (uint64_t)c * TROWS;
-  const uint32_t* D = dcnt + (uint64_t)c * TROWS;
-  const uint32_t* L = lp + (uint64_t)c * TROWS;
-  const uint32_t n_left = (uint32_t)usable - D[TROWS - 1];
   uint64_t* o = out + (uint64_t)(c0 + c) * 5 * out_rows * 4;
-  const uint32_t b = (uint32_t)(q * gp::ZC);
-  const uint32_t e = b + gp::ZC < usable ? b + gp::ZC : (uint32_t)usable;
-  uint32_t r = last_le(P, sP, b);
-  uint32_t rl = 0xffffffffu;  // leftover rank: searched at the chunk's first repeated row
-  Fe pn = field::one<F>(), pd = field::one<F>();
-#pragma unroll 1
-  for (uint32_t p = b; p < e; p++) {
-    // the run holding p: step over the empty ranks after r
-    uint32_t steps = 0;
-    while (r + 1 < (uint32_t)TROWS && P[r + 1] <= p) {
-      if (++steps > WALK) {
-        r = last_le(P, sP, p);
-        break;
-      }
-      r++;
-    }
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < usable; p += stride) {
     const uint32_t x = p < k.n_in ? (adv[total_rows + k.first + p] & 0xffffu) : 0u;
     const Fe a = Tx[x];
-    const Fe sv = Tx[p < (uint32_t)TROWS ? p : 0u];
+    const Fe sv = Tx[p < (uint64_t)TROWS ? (uint32_t)p : 0u];
+    const uint32_t r = last_le(P, sP, (uint32_t)p);
     const Fe ap = Ts[r];
-    Fe sp = ap;
-    if (P[r] != p) {  // a repeated row: leftover item n_left - 1 - j, j = p - D[r]
-      const uint32_t idx = n_left - 1 - (p - D[r]);
-      if (rl == 0xffffffffu) {
-        rl = last_le(L, sL, idx);
-      } else {
-        uint32_t st = 0;
-        while (L[rl] > idx) {
-          if (++st > WALK) {
-            rl = last_le(L, sL, idx);
-            break;
-          }
-          rl--;
-        }
-      }
-      sp = Ts[rl];
+    Fe sp;
+    if (P[r] == (uint32_t)p) {
+      sp = ap;
+    } else {
+      const uint32_t j = (uint32_t)p - D[r];
+      sp = Ts[last_le(L, sL, n_left - 1 - j)];
     }
-    store(o + 4ull * p, out_form<F>(a, mont));
+    store(o + 4 * p, out_form<F>(a, mont));
     store(o + (out_rows + p) * 4, out_form<F>(sv, mont));
     store(o + (2 * out_rows + p) * 4, out_form<F>(ap, mont));
     store(o + (3 * out_rows + p) * 4, out_form<F>(sp, mont));
     // the grand product's factors (A + beta)(S + gamma) / ((A' + beta)(S' + gamma))
-    const Fe fn = field::mul<F>(field::add<F>(a, beta), field::add<F>(sv, gamma));
-    const Fe fd = field::mul<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma));
-    pn = p == b ? fn : field::mul<F>(pn, fn);
-    pd = p == b ? fd : field::mul<F>(pd, fd);
-    const uint64_t sl = gp::slot_of(p, nq);
-    nm[sl] = pn;  // Nloc: the chunk's num prefix through p
-    dn[sl] = fd;
+    nm[gp::slot_of(p, nq)] = field::mul<F>(field::add<F>(a, beta), field::add<F>(sv, gamma));
+    dn[gp::slot_of(p, nq)] = field::mul<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma));
   }
-  zn[(uint64_t)c * nq + q] = pn;
-  zd[(uint64_t)c * nq + q] = pd;
 }
 
 using gp::ZC;
@@ -503,16 +459,13 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
     hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
     hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
                        k.part, k.pos, k.dcnt, k.lp, k.samp);
-    // permute + the grand product's chunk pass: one thread per 16-row chunk, 256 per workgroup
-    // (the LDS samples staged once per workgroup)
-    const uint64_t nq = gp::n_chunks(usable_rows);
-    const uint32_t px = (uint32_t)((nq + 255) / 256);
+    // permute: ~4096 rows per workgroup (the LDS samples are staged once per workgroup)
+    const uint32_t px = (uint32_t)((usable_rows + 4095) / 4096);
     hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
                        d_row_begin, c0, usable_rows, k.Tx, k.Ts, k.pos, k.dcnt, k.lp, k.samp, mont,
-                       d_out, out_rows, ch, k.num, k.den, gp::zn_of(k.zs), gp::zd_of(k.zs, g, usable_rows));
+                       d_out, out_rows, ch, k.num, k.den);
     e = gp::run<F>(g, usable_rows, mont, d_out + ((uint64_t)c0 * 5 + 4) * out_rows * 4,
-                   5 * out_rows * 4, k.num, k.den, k.zs, nullptr, nullptr, s, nullptr, sticky,
-                   /*totals_done=*/true);
+                   5 * out_rows * 4, k.num, k.den, k.zs, nullptr, nullptr, s, nullptr, sticky);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
