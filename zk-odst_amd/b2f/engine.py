@@ -4,6 +4,7 @@ PyTorch is plumbing here (device memory, the stream handle); the work is the HIP
 behind include/b2f.h.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -19,19 +20,39 @@ def _np_ptr(a):
     return ctypes.c_void_p(a.ctypes.data)
 
 
-def upload(a, device, dtype=None):
-    """Host array -> device tensor as an asynchronous copy from page-locked memory on the current
-    stream, ordered before every later launch on that stream. A copy from pageable memory
-    (tensor.to(device)) is not: measured on MI355X, the tail of such a copy could still be in
-    flight when the next kernel on the same stream read it (tools/hasher_race.py: the last
-    instance of a batch read a stale h0 row; a host synchronize hid it). The page-locked block
-    stays alive until the copy is done (torch's host allocator records the stream)."""
-    import torch
+_hip = None
 
-    t = torch.from_numpy(np.ascontiguousarray(a))
-    if dtype is not None:
-        t = t.view(dtype)
-    return t.pin_memory().to(device, non_blocking=True)
+
+def hip_runtime():
+    """The HIP runtime this process (torch and libb2f.so) uses, for the one call torch does not
+    order for us (copy_h2d_async)."""
+    global _hip
+    if _hip is None:
+        import torch
+
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+        _hip = ctypes.CDLL(path if os.path.exists(path) else "libamdhip64.so")
+        _hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.c_int, ctypes.c_void_p]
+        _hip.hipMemcpyAsync.restype = ctypes.c_int
+    return _hip
+
+
+def copy_h2d_async(dst, src, stream):
+    """dst (device tensor) <- src (page-locked host tensor, same bytes) as hipMemcpyAsync on
+    `stream`, the stream the library's launches go to: ordered before them. torch's own
+    non_blocking copy (dst.copy_(src, non_blocking=True) under that stream) was measured NOT to
+    be: tools/hasher_race.py (profiles/r03f_hasher_race.txt) -- 3 of 4 runs of 2^14 messages read
+    a stale t counter in every step-0 input (49,152 wrong digests), 0 with this call, 0 with a
+    host synchronize, 0 with blocking copies. The caller keeps src alive until the copy is done
+    (the HIP call is invisible to torch's host allocator)."""
+    nbytes = src.numel() * src.element_size()
+    if nbytes != dst.numel() * dst.element_size():
+        raise _lib.B2FError(_lib.ERR_ARG, "copy_h2d_async: %d bytes into %d"
+                            % (nbytes, dst.numel() * dst.element_size()))
+    rc = hip_runtime().hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), nbytes, 1, stream)
+    if rc:
+        raise _lib.B2FError(_lib.ERR_HIP, "hipMemcpyAsync returned %d" % rc)
 
 
 class Engine:
@@ -221,8 +242,10 @@ class DeviceBatch:
                                 % (self.total_rows, self.used_rows))
         dev = torch.device(device)
         raw = np.frombuffer(inputs.tobytes(), dtype=np.uint8)
-        self.inputs = upload(raw, dev)
-        self.offsets = upload(off.view(np.int64), dev)
+        # synchronous (pageable) uploads: construction is not the hot path, and a later launch
+        # on any stream sees them (see copy_h2d_async for the asynchronous form)
+        self.inputs = torch.from_numpy(raw.copy()).to(dev)
+        self.offsets = torch.from_numpy(off.view(np.int64).copy()).to(dev)
         self.advice = torch.empty((_lib.NUM_ADVICE, self.total_rows), dtype=torch.int32, device=dev)
         self.fixed = torch.empty(self.total_rows, dtype=torch.int32, device=dev)
         self.h_out = torch.empty((self.n, 8), dtype=torch.int64, device=dev)
@@ -270,7 +293,7 @@ class DeviceBatch:
         [n_circuits]) -- see b2f_lookup_columns_dev."""
         torch = self.torch
         dev = self.advice.device
-        rb = upload(np.array([int(r) for r in row_begin], dtype=np.int64), dev)
+        rb = torch.tensor([int(r) for r in row_begin], dtype=torch.int64, device=dev)
         nc = len(row_begin)
         out = torch.empty((nc, 5, usable_rows + 1, 4), dtype=torch.int64, device=dev)
         bad = torch.empty(nc, dtype=torch.int64, device=dev)

@@ -18,6 +18,7 @@ and every step's trace, offsets and outputs are prefixes of one allocation.
 import numpy as np
 
 from . import _lib
+from .engine import copy_h2d_async
 from .layout import rows
 
 BLOCK_BYTES = 128
@@ -154,35 +155,46 @@ def run_plan(engine, plan, path="fused", device="cuda:0", stream=None, _diag=Non
     compute = torch.cuda.ExternalStream(s, device=dev)
     p_blocks, p_t, p_f, p_h0, p_fin = plan.pinned()
     R = rows(BLAKE2B_ROUNDS)
-    # Everything is allocated, copied and launched on the one stream `s`, and every host ->
-    # device copy is from page-locked memory (a pageable copy's tail was measured still in
-    # flight when the first launch read it: the last instance of step 0 got a stale h0 row;
-    # engine.upload). No host synchronize is needed (tests/test_gpu_hasher.py runs batches back
-    # to back on alternating paths).
+    # Everything is allocated, copied and launched on the one stream `s`; every host -> device
+    # copy is hipMemcpyAsync from page-locked memory on `s` (engine.copy_h2d_async). No host
+    # synchronize is needed (tests/test_gpu_hasher.py runs batches back to back on alternating
+    # paths, without one).
     with torch.cuda.stream(compute):
         d_blocks = torch.empty(p_blocks.shape, dtype=p_blocks.dtype, device=dev)
         d_t = torch.empty(p_t.shape, dtype=p_t.dtype, device=dev)
         d_f = torch.empty(p_f.shape, dtype=p_f.dtype, device=dev)
         # h' of every compression, step-major like the plan: step j's outputs are rows
         # start[j] .. start[j] + active[j] - 1, and step j + 1 reads its h from that prefix
-        h0 = p_h0.to(dev, non_blocking=True)
-        fin_idx = p_fin.to(dev, non_blocking=True)
+        h0 = torch.empty(p_h0.shape, dtype=p_h0.dtype, device=dev)
+        fin_idx = torch.empty(p_fin.shape, dtype=p_fin.dtype, device=dev)
         offsets = torch.arange(n + 1, dtype=torch.int64, device=dev) * R
         hs = torch.empty((int(plan.start[-1]), 8), dtype=torch.int64, device=dev)
-        inputs = torch.empty(n * 216, dtype=torch.uint8, device=dev)
+        keep = _diag is not None and _diag.get("keep_inputs")
+        inputs_all = torch.empty(int(plan.start[-1]) * 216 if keep else n * 216, dtype=torch.uint8,
+                                 device=dev)
         advice = torch.empty((_lib.NUM_ADVICE, R * n), dtype=torch.int32, device=dev)
         fixed = torch.empty(R * n, dtype=torch.int32, device=dev)
         report = torch.empty((plan.steps, _lib.REPORT_BYTES // 8), dtype=torch.int64, device=dev)
-        # one asynchronous DMA from page-locked memory, ordered before the launches below
-        d_blocks.copy_(p_blocks, non_blocking=True)
-        d_t.copy_(p_t, non_blocking=True)
-        d_f.copy_(p_f, non_blocking=True)
+        # asynchronous DMAs from page-locked memory on `s` itself (engine.copy_h2d_async: torch's
+        # non_blocking copy is not ordered before the library's launches)
+        how = _diag.get("upload", "hip") if _diag is not None else "hip"
+        if how == "hip":
+            for d, p in ((d_blocks, p_blocks), (d_t, p_t), (d_f, p_f), (h0, p_h0), (fin_idx, p_fin)):
+                copy_h2d_async(d, p, s)
+        else:  # diagnostics (tools/hasher_race.py): torch's copy, non-blocking or blocking
+            nb = how != "blocking"
+            for d, p in ((d_blocks, p_blocks), (d_t, p_t), (d_f, p_f), (h0, p_h0), (fin_idx, p_fin)):
+                d.copy_(p, non_blocking=nb)
     if _diag is not None and _diag.get("sync_upload"):  # diagnostics (tools/hasher_race.py)
-        torch.cuda.synchronize(dev)
+        if _diag["sync_upload"] == "stream":
+            compute.synchronize()
+        else:
+            torch.cuda.synchronize(dev)
     for j in range(plan.steps):
         a = int(plan.active[j])
         s0 = int(plan.start[j])
         h_prev = h0 if j == 0 else hs[int(plan.start[j - 1])]
+        inputs = inputs_all[s0 * 216:] if keep else inputs_all
         engine.chain_inputs_dev(h_prev.data_ptr(), d_blocks[s0].data_ptr(), d_t[s0].data_ptr(),
                                 d_f[s0:].data_ptr(), BLAKE2B_ROUNDS, a, inputs.data_ptr(), s)
         total = R * a
@@ -205,6 +217,9 @@ def run_plan(engine, plan, path="fused", device="cuda:0", stream=None, _diag=Non
     res = ChainResult(plan, reps, fin_host)
     if _diag is not None:  # diagnostics: every step's h' (step-major, sorted order)
         res.all_h = hs.cpu().numpy().view(np.uint64)
+        res.stream = int(s)
+        if keep:  # every step's b2f_input records as chain_inputs built them
+            res.all_inputs = inputs_all.cpu().numpy()
     return res
 
 
