@@ -109,12 +109,15 @@ __global__ void __launch_bounds__(256) wave_rr_pad(uint32_t* adv, uint64_t total
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 __device__ void probe_buffer_store(i32x4 data, i32x4 rsrc, int voffset, int soffset,
                                    int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
-template <int STEP, bool STAGE, bool BUF>
+template <int STEP, bool STAGE, bool BUF, int POL = 2, bool XCD = false>
 __global__ void __launch_bounds__(256) wave_rr_work(uint32_t* adv, uint64_t total_rows, int work) {
   __shared__ __attribute__((aligned(16))) uint32_t L[4 * 11 * 256];
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t* S = L + (threadIdx.x >> 6) * 11 * 256;
-  const uint64_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  // XCD: the fused kernel's deal (workgroups go to the 8 XCDs round-robin; XCD x takes the x-th
+  // eighth of every round as one contiguous run, so neighbouring tiles share an L2)
+  const uint64_t bx = XCD ? (uint64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
+  const uint64_t wid = bx * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
   const uint64_t total_quads = total_rows >> 2;
   const uint64_t n_t = (total_quads + STEP - 1) / STEP;
   for (uint64_t t = wid; t < n_t; t += nw) {
@@ -139,7 +142,7 @@ __global__ void __launch_bounds__(256) wave_rr_work(uint32_t* adv, uint64_t tota
       if (BUF) {
         const uint64_t a = reinterpret_cast<uint64_t>(base);
         const i32x4 rsrc = {(int32_t)(uint32_t)a, (int32_t)(uint32_t)(a >> 32), (int32_t)(nq * 16u), 0x00020000};
-        probe_buffer_store(i32x4{(int32_t)v[c].x, (int32_t)v[c].y, (int32_t)v[c].z, (int32_t)v[c].w}, rsrc, (int)(16 * lane), 0, 2);
+        probe_buffer_store(i32x4{(int32_t)v[c].x, (int32_t)v[c].y, (int32_t)v[c].z, (int32_t)v[c].w}, rsrc, (int)(16 * lane), 0, POL);
       } else if (lane < nq) {
         __builtin_nontemporal_store(v[c], reinterpret_cast<u32x4*>(base + 4 * lane));
       }
@@ -359,6 +362,36 @@ int main(int argc, char** argv) {
       SPEC(7, 1, 2)
       SPEC(4, 3, 1)
 #undef SPEC
+    }
+    return 0;
+  }
+  if (argc > 2 && argv[2][0] == 'a') {  // tile alignment: 52-quad (832 B, lines split between
+                                        // neighbouring tiles) vs 64-quad (1 KiB, whole lines)
+    // tiles, against the fill kernel's 1024-row workgroup tiles, on this box
+    for (int w : {8}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "tile_rr_%dwg", w);
+      run(nm, [&] { hipLaunchKernelGGL(tile_store, dim3(cus * w), dim3(256), 0, 0, adv, total, nt); });
+    }
+    for (int w : {2, 4, 8}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "wave_rr_q52_%dwg", w);
+      run(nm, [&] { hipLaunchKernelGGL(wave_rr_store<52>, dim3(cus * w), dim3(256), 0, 0, adv, total); });
+      snprintf(nm, sizeof nm, "wave_rr_q64_%dwg", w);
+      run(nm, [&] { hipLaunchKernelGGL(wave_rr_store<64>, dim3(cus * w), dim3(256), 0, 0, adv, total); });
+    }
+    for (int work : {0, 120}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "buf_pol0_q52_xcd_work%d_2wg", work);
+      run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<52, false, true, 0, true>), dim3(cus * 2), dim3(256), 0, 0, adv, total, work); });
+      snprintf(nm, sizeof nm, "buf_pol0_q64_xcd_work%d_2wg", work);
+      run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<64, false, true, 0, true>), dim3(cus * 2), dim3(256), 0, 0, adv, total, work); });
+      snprintf(nm, sizeof nm, "buf_pol0_q52_work%d_2wg", work);
+      run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<52, false, true, 0>), dim3(cus * 2), dim3(256), 0, 0, adv, total, work); });
+      snprintf(nm, sizeof nm, "buf_pol0_q64_work%d_2wg", work);
+      run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<64, false, true, 0>), dim3(cus * 2), dim3(256), 0, 0, adv, total, work); });
+      snprintf(nm, sizeof nm, "buf_pol2_q52_work%d_2wg", work);
+      run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<52, false, true, 2>), dim3(cus * 2), dim3(256), 0, 0, adv, total, work); });
     }
     return 0;
   }

@@ -9,14 +9,17 @@
 // chunk):
 //   gp_chunk:  the chunk's num prefix Nloc_p (written over num in place), the chunk totals of
 //              num and den (2 products per row);
-//   gp_scan:   K_q = seed N_before(q) D_end(q)^-1 per chunk, the inversion, and the closing
-//              value seed N / D (= z[usable]) for a next product. Up to SCAN_THREADS x 4
-//              chunks one workgroup per product scans them directly; beyond, three levels over
-//              blocks of SCAN_THREADS chunks (gp_block_reduce: block totals; gp_scan over the
-//              block totals; gp_block_down: in-block exclusive prefix / suffix combined with the
-//              block's K), so the serial run per lane stays short at any size;
-//   gp_write:  backward over the chunk: z[p + 1] = K_q Nloc_p prod_{p < i < e} den_i
-//              (2 products per row), converted to the output form.
+//   gp_scan:   K'_q = seed N_before(q) prod_{q' > q} D_q' per chunk (K_q = K'_q D^-1), the den
+//              total D and seed N (the closing value seed N / D = z[usable] before its D^-1).
+//              Up to SCAN_THREADS x 4 chunks one workgroup per product scans them directly;
+//              beyond, three levels over blocks of SCAN_THREADS chunks (gp_block_reduce: block
+//              totals; gp_scan over the block totals; gp_block_down: in-block exclusive prefix /
+//              suffix combined with the block's K'), so the serial run per lane stays short;
+//   gp_inv:    D^-1 (one lane's Kaliski inversion, ~100 us of latency) and the closing values.
+//              It depends only on gp_scan, so it runs on a second stream beside gp_block_down;
+//   gp_write:  backward over the chunk: z[p + 1] = K'_q D^-1 Nloc_p prod_{p < i < e} den_i
+//              (2 products per row), converted to the output form and staged through LDS so a
+//              wave's stores cover whole 128-byte row groups.
 // Products are independent along blockIdx.y: product y reads num/den + y * elems(usable) and
 // writes z column z_base + y * z_stride (u64 units, 4 per element).
 #pragma once
@@ -33,13 +36,21 @@ constexpr int SCAN_THREADS = 1024;    // one workgroup per product
 
 __host__ __device__ inline uint64_t n_chunks(uint64_t usable) { return (usable + ZC - 1) / ZC; }
 
-// num / den are stored chunk-interleaved: row p of a product at (p mod ZC) * nq + p / ZC, so
-// that the lanes of a wave (consecutive chunks) walking their chunks read consecutive
-// elements at every step -- a row-major layout put the lanes 512 bytes apart and turned each
-// 32-byte read into a 128-byte line fetch. Writers (the factor passes) place rows this way;
-// an array holds ZC * nq elements per product.
-__host__ __device__ inline uint64_t slot_of(uint64_t p, uint64_t nq) { return (p % ZC) * nq + p / ZC; }
-__host__ __device__ inline uint64_t elems(uint64_t usable) { return n_chunks(usable) * ZC; }
+// num / den are stored interleaved by tiles of ZC chunks (ZC x ZC rows): row p = ZC q + j of chunk
+// q = ZC Q + k sits at ZC^2 Q + ZC j + k. Readers (a lane per chunk, walking j) see 16 consecutive
+// chunks' row j as 16 consecutive elements (512 contiguous bytes per 16 lanes); writers (a lane per
+// row: the factor passes) see 64 consecutive rows as 16 runs of 4 elements (128-byte lines). Row-
+// major put the readers' lanes 512 bytes apart; interleaving over ALL chunks ((p mod ZC) nq + p /
+// ZC) put the writers' lanes nq x 32 bytes apart (every 32-byte store a partial line: the lookup's
+// permute pass wrote its num / den at a fraction of the bandwidth). An array holds elems(usable)
+// elements per product (whole tiles).
+__host__ __device__ inline uint64_t slot_of(uint64_t p, uint64_t nq) {
+  (void)nq;
+  return (p / (ZC * ZC)) * (ZC * ZC) + (p % ZC) * ZC + (p / ZC) % ZC;
+}
+__host__ __device__ inline uint64_t elems(uint64_t usable) {
+  return (usable + ZC * ZC - 1) / (ZC * ZC) * (ZC * ZC);
+}
 
 template <class F>
 __device__ __forceinline__ Fe out_form(const Fe& a, bool mont) {
@@ -57,7 +68,7 @@ __global__ __launch_bounds__(256) void gp_chunk(uint64_t usable, Fe* __restrict_
   Fe* nm = num + (uint64_t)c * elems(usable);
   const Fe* dn = den + (uint64_t)c * elems(usable);
   const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
-  Fe pn = nm[q], pd = dn[q];  // row b (slot 0 of chunk q)
+  Fe pn = nm[slot_of(b, nq)], pd = dn[slot_of(b, nq)];  // row b
   for (uint64_t p = b + 1; p < e; p++) {
     const uint64_t k = slot_of(p, nq);
     pn = field::mul<F>(pn, nm[k]);
@@ -68,11 +79,10 @@ __global__ __launch_bounds__(256) void gp_chunk(uint64_t usable, Fe* __restrict_
   zd[(uint64_t)c * nq + q] = pd;
 }
 
-// zn[q] <- K_q = seed N_before(q) D_end(q)^-1 with N_before(q) = prod_{q' < q} zn[q'],
-// D_end(q)^-1 = D^-1 prod_{q' > q} zd[q']. Per-thread runs of chunks, Hillis-Steele scans
-// of the run products in LDS (a prefix for num, a suffix for den), one inversion.
-// seed: Montgomery elements per product (nullptr: 1); closing (nullable) <- seed N / D;
-// sticky (nullable): the context's sticky error word, B2F_ERR_FIELD set when D = 0.
+// zn[q] <- K'_q = seed N_before(q) prod_{q' > q} zd[q'] with N_before(q) = prod_{q' < q} zn[q']
+// (K_q = K'_q D^-1: gp_write applies D^-1). Per-thread runs of chunks, Hillis-Steele scans of the
+// run products in LDS (a prefix for num, a suffix for den). seed: Montgomery elements per product
+// (nullptr: 1); sn[c] <- seed N.
 // T threads: SCAN_THREADS, or one wave when there are at most 64 chunk totals (the block totals
 // of the three-level path) -- a 1,024-thread scan of 8 values spent ten levels of products on
 // every thread.
@@ -80,11 +90,10 @@ template <class F, int T = SCAN_THREADS>
 __global__ __launch_bounds__(T) void gp_scan(uint64_t nq, Fe* __restrict__ zn,
                                              const Fe* __restrict__ zd,
                                              const Fe* __restrict__ seed,
-                                             Fe* __restrict__ closing, int* __restrict__ sticky) {
+                                             Fe* __restrict__ sn_out) {
   const uint32_t c = blockIdx.x, t = threadIdx.x;
   const uint64_t per = (nq + T - 1) / T;
   __shared__ Fe sn[T], sd[T];
-  __shared__ Fe dinv;
   Fe* an = zn + (uint64_t)c * nq;
   const Fe* ad = zd + (uint64_t)c * nq;
   const uint64_t b = t * per < nq ? t * per : nq, e = b + per < nq ? b + per : nq;
@@ -106,30 +115,62 @@ __global__ __launch_bounds__(T) void gp_scan(uint64_t nq, Fe* __restrict__ zn,
     __syncthreads();
   }
   const Fe s = seed ? seed[c] : field::one<F>();
-  if (t == 0) {
-#ifdef B2F_INV_EUCLID  // diagnostics: the plain binary extended Euclid
-    dinv = field::inv<F>(sd[0]);  // sd[0] = D
-#else
-    dinv = field::inv_kaliski<F>(sd[0]);  // sd[0] = D
-#endif
-    // D = 0: some den factor is zero (a challenge collides with a cell value). halo2's
-    // batch_invert would leave that entry zero and the proof would fail; here every z would
-    // come from a meaningless inverse, so the call reports B2F_ERR_FIELD at b2f_sync instead.
-    if (sticky && field::is_zero(sd[0])) atomicOr(sticky, 1 << B2F_ERR_FIELD);
-    if (closing) closing[c] = field::mul<F>(field::mul<F>(s, sn[T - 1]), dinv);
-  }
-  __syncthreads();
-  Fe rd = t + 1 < (uint32_t)T ? field::mul<F>(dinv, sd[t + 1]) : dinv;
+  if (t == 0) sn_out[c] = field::mul<F>(s, sn[T - 1]);  // seed N (the closing value before D^-1)
+  Fe rd = t + 1 < (uint32_t)T ? sd[t + 1] : field::one<F>();
   Fe rn = t ? field::mul<F>(s, sn[t - 1]) : s;
   for (uint64_t q = b; q < e; q++) {  // forward: seed times the exclusive num prefix
     const Fe vn = an[q];
     an[q] = rn;
     rn = field::mul<F>(rn, vn);
   }
-  for (uint64_t q = e; q-- > b;) {  // backward: K_q
+  for (uint64_t q = e; q-- > b;) {  // backward: K'_q
     an[q] = field::mul<F>(an[q], rd);
     rd = field::mul<F>(rd, ad[q]);
   }
+}
+
+// D = the product of a product's chunk den totals, straight after gp_chunk (so the inversion can
+// start before the scans): one workgroup per product, a strided product per thread, then a tree.
+template <class F>
+__global__ __launch_bounds__(1024) void gp_total(uint64_t nq, const Fe* __restrict__ zd,
+                                                 Fe* __restrict__ dt) {
+  const uint32_t c = blockIdx.x, t = threadIdx.x;
+  __shared__ Fe sp[1024];
+  Fe p = field::one<F>();
+  for (uint64_t q = t; q < nq; q += 1024) p = field::mul<F>(p, zd[(uint64_t)c * nq + q]);
+  for (uint32_t w = 512; w > 0; w >>= 1) {
+    if (t >= w && t < 2 * w) sp[t] = p;
+    __syncthreads();
+    if (t < w) p = field::mul<F>(p, sp[t + w]);
+    __syncthreads();
+  }
+  if (t == 0) dt[c] = p;
+}
+
+// D^-1 in place of D (one lane per product: Kaliski, ~100 us of latency; it needs only gp_total,
+// so it runs on the side stream beside the scans). D = 0: some den factor is zero (a challenge
+// collides with a cell value). halo2's batch_invert would leave that entry zero and the proof
+// would fail; here every z would come from a meaningless inverse, so the call reports
+// B2F_ERR_FIELD at b2f_sync instead.
+template <class F>
+__global__ __launch_bounds__(64) void gp_inv(Fe* __restrict__ dt, int* __restrict__ sticky) {
+  const uint32_t c = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  const Fe D = dt[c];
+  if (sticky && field::is_zero(D)) atomicOr(sticky, 1 << B2F_ERR_FIELD);
+#ifdef B2F_INV_EUCLID  // diagnostics: the plain binary extended Euclid
+  dt[c] = field::inv<F>(D);
+#else
+  dt[c] = field::inv_kaliski<F>(D);
+#endif
+}
+
+// closing[c] = seed N / D (the value z[usable] ends at), for a chained next product
+template <class F>
+__global__ void gp_close(const Fe* __restrict__ sn, const Fe* __restrict__ dinv, Fe* __restrict__ closing,
+                         uint32_t g) {
+  const uint32_t c = threadIdx.x;
+  if (c < g) closing[c] = field::mul<F>(sn[c], dinv[c]);
 }
 
 // block b of product c: the products of its SCAN_THREADS chunks' zn and zd -> tn/td[c][b]
@@ -213,31 +254,64 @@ __global__ __launch_bounds__(DOWN_T) void gp_block_down(uint64_t nq, Fe* __restr
   }
 }
 
+// z rows go out through LDS in groups of GW_ROWS rows: each lane walks its chunk backward as
+// before, stages the z values of GW_ROWS rows, and the wave then stores the group's rows of its
+// 64 chunks so that every 8 lanes write one 128-byte run of rows (a lane storing its own rows
+// straight away wrote 64 lines 512 bytes apart per store instruction).
+constexpr int GW_ROWS = 4;
+static_assert(ZC % GW_ROWS == 0, "whole row groups per chunk");
 template <class F>
 __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint64_t* __restrict__ z_base,
                                                 uint64_t z_stride, const Fe* __restrict__ num,
                                                 const Fe* __restrict__ den,
                                                 const Fe* __restrict__ zn,
                                                 const Fe* __restrict__ seed,
-                                                const Fe* __restrict__ post) {
-  const uint32_t c = blockIdx.y;
+                                                const Fe* __restrict__ post,
+                                                const Fe* __restrict__ dinv) {
+  __shared__ uint4 stage[4][64][GW_ROWS][2];
+  const uint32_t c = blockIdx.y, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint64_t nq = n_chunks(usable);
-  const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (q >= nq) return;
+  const uint64_t q0w = (uint64_t)blockIdx.x * 256 + 64 * wv;  // the wave's first chunk
+  const uint64_t q = q0w + lane;
+  const bool act = q < nq;
   const Fe* nm = num + (uint64_t)c * elems(usable);  // Nloc, from gp_chunk
   const Fe* dn = den + (uint64_t)c * elems(usable);
   uint64_t* zcol = z_base + (uint64_t)c * z_stride;
-  const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
+  const uint64_t b = q * ZC, e = !act ? b : (b + ZC < usable ? b + ZC : usable);
   // post: a factor applied here rather than in the scan (chained products: the seed of
   // product c is only known once the scans of products 0 .. c - 1 are done)
   const Fe s0 = post ? post[c] : (seed ? seed[c] : field::one<F>());
   if (q == 0) field::store(zcol, out_form<F>(s0, mont));
-  Fe k = zn[(uint64_t)c * nq + q];
-  if (post) k = field::mul<F>(k, post[c]);
-  for (uint64_t p = e; p-- > b;) {
-    const uint64_t sl = slot_of(p, nq);
-    field::store(zcol + 4 * (p + 1), out_form<F>(field::mul<F>(nm[sl], k), mont));
-    if (p > b) k = field::mul<F>(k, dn[sl]);
+  Fe k = field::one<F>();
+  if (act) {
+    k = field::mul<F>(zn[(uint64_t)c * nq + q], dinv[c]);  // K'_q D^-1
+    if (post) k = field::mul<F>(k, post[c]);
+  }
+#pragma unroll 1
+  for (int j = ZC - 1; j >= 0; j--) {
+    const uint64_t p = b + (uint64_t)j;
+    if (p < e) {
+      const uint64_t sl = slot_of(p, nq);
+      const Fe z = out_form<F>(field::mul<F>(nm[sl], k), mont);
+      stage[wv][lane][j % GW_ROWS][0] = make_uint4(z.w[0], z.w[1], z.w[2], z.w[3]);
+      stage[wv][lane][j % GW_ROWS][1] = make_uint4(z.w[4], z.w[5], z.w[6], z.w[7]);
+      if (j > 0) k = field::mul<F>(k, dn[sl]);
+    }
+    if (j % GW_ROWS == 0) {  // rows b + j + 1 .. b + j + GW_ROWS of the wave's 64 chunks
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int i = 0; i < 64 * GW_ROWS * 2 / 64; i++) {
+        const uint32_t u = 64u * i + lane, ch = u / (2 * GW_ROWS), rr = (u >> 1) % GW_ROWS, h = u & 1u;
+        const uint64_t cq = q0w + ch, pr = cq * ZC + (uint64_t)j + rr;  // the row p whose z[p + 1] this is
+        if (cq < nq && pr < usable && pr < cq * ZC + ZC) {
+          const uint4 v = stage[wv][ch][rr][h];
+          *reinterpret_cast<uint4*>(zcol + 4 * (pr + 1) + 2 * h) = v;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+    }
   }
 }
 
@@ -257,17 +331,23 @@ __global__ void gp_chain_seeds(const Fe* __restrict__ T, Fe* __restrict__ S, uin
 // Scratch (Fe elements) gp::run needs per product: chunk products, and block totals + K.
 __host__ __device__ inline uint64_t scratch_elems(uint64_t usable) {
   const uint64_t nq = n_chunks(usable), nb = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
-  return 2 * nq + 2 * nb;
+  return 2 * nq + 2 * nb + 2;  // chunk totals, block totals, (seed N, D / D^-1)
 }
 
 // The passes for `g` products on `s`. zs: scratch of g * scratch_elems(usable). With `chain`
 // (2 g elements of scratch) the products are chained -- product c starts from product c - 1's
 // closing value, product 0 from 1 -- and still scanned side by side: their single inversions
-// run in parallel, the seeds are applied in gp_write.
+// run in parallel, the seeds are applied in gp_write. With a second stream `s2` and two events
+// the inversions run there, beside gp_block_down (they need only gp_scan's totals); s2 = null
+// runs them on `s`.
+struct Side {
+  hipStream_t s2;
+  hipEvent_t fork, join;
+};
 template <class F>
 hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_t z_stride,
                Fe* num, const Fe* den, Fe* zs, const Fe* seed, Fe* closing, hipStream_t s,
-               Fe* chain = nullptr, int* sticky = nullptr) {
+               Fe* chain = nullptr, int* sticky = nullptr, Side side = Side{nullptr, nullptr, nullptr}) {
   Fe* post = nullptr;
   if (chain) {
     seed = nullptr;
@@ -279,24 +359,37 @@ hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_
   Fe* zd = zs + (uint64_t)g * nq;
   Fe* tn = zd + (uint64_t)g * nq;
   Fe* td = tn + (uint64_t)g * nb;
+  Fe* sn = td + (uint64_t)g * nb;  // g: seed N per product (gp_scan)
+  Fe* dt = sn + g;                  // g: D, then D^-1 (gp_total, gp_inv)
   const uint32_t zq = (uint32_t)((nq + 255) / 256);
+  hipError_t e;
   hipLaunchKernelGGL(gp_chunk<F>, dim3(zq, g), dim3(256), 0, s, usable, num, den, zn, zd);
+  hipLaunchKernelGGL(gp_total<F>, dim3(g), dim3(1024), 0, s, nq, zd, dt);
+  const bool fork = side.s2 && nq > 4ull * SCAN_THREADS;  // the scans are long enough to hide it
+  if (fork) {
+    if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(gp_inv<F>, dim3(g), dim3(64), 0, fork ? side.s2 : s, dt, sticky);
+  if (fork && (e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;
   if (nq <= 64) {
-    hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nq, zn, zd, seed, closing, sticky);
+    hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nq, zn, zd, seed, sn);
   } else if (nq <= 4ull * SCAN_THREADS) {
-    hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, seed, closing, sticky);
+    hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, seed, sn);
   } else {
     hipLaunchKernelGGL(gp_block_reduce<F>, dim3((uint32_t)nb, g), dim3(SCAN_THREADS), 0, s, nq, zn, zd,
                        tn, td);
     if (nb <= 64)
-      hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nb, tn, td, seed, closing, sticky);
+      hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nb, tn, td, seed, sn);
     else
-      hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, tn, td, seed, closing, sticky);
+      hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, tn, td, seed, sn);
     hipLaunchKernelGGL(gp_block_down<F>, dim3((uint32_t)nb, g), dim3(DOWN_T), 0, s, nq, zn, zd, tn);
   }
+  if (fork && (e = hipStreamWaitEvent(s, side.join, 0)) != hipSuccess) return e;
+  if (closing) hipLaunchKernelGGL(gp_close<F>, dim3(1), dim3(256), 0, s, sn, dt, closing, g);
   if (chain) hipLaunchKernelGGL(gp_chain_seeds<F>, dim3(1), dim3(64), 0, s, chain, post, g);
   hipLaunchKernelGGL(gp_write<F>, dim3(zq, g), dim3(256), 0, s, usable, mont, z_base, z_stride, num,
-                     den, zn, seed, post);
+                     den, zn, seed, post, dt);
   return hipGetLastError();
 }
 

@@ -38,7 +38,8 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* d_row_begin, uint32_t n_circuits, uint64_t usable_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
-                         void* scratch, uint32_t group, int* sticky, hipStream_t s);
+                         void* scratch, uint32_t group, int* sticky, hipStream_t s2,
+                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s);
 hipError_t launch_spread_table(uint64_t usable_rows, uint32_t form, uint64_t* d_out,
                                uint64_t out_rows, hipStream_t s);
 size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst, uint32_t chunk_len);
@@ -47,7 +48,8 @@ hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uin
                               uint32_t k, uint64_t usable_rows, const uint64_t* omega,
                               const uint64_t* delta, const uint64_t* beta, const uint64_t* gamma,
                               uint32_t chunk_len, uint32_t form, uint64_t* d_sigma, uint64_t* d_z,
-                              uint64_t out_rows, void* scratch, int* sticky, hipStream_t s);
+                              uint64_t out_rows, void* scratch, int* sticky, hipStream_t s2,
+                              hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s);
 hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
                             uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
                             int cu_count, hipStream_t s);  // b2f_export.hip
@@ -792,6 +794,10 @@ struct b2f_ctx {
   size_t pm_inst_cap;
   void* d_pm;
   size_t pm_cap;
+  // a second stream and two events: the grand products' inversions run beside their block
+  // down-sweep (b2f_gprod.h), forked from and joined back to the caller's stream
+  hipStream_t s2;
+  hipEvent_t ev_fork, ev_join;
 };
 
 namespace {
@@ -852,6 +858,14 @@ int fused_mode() {
 constexpr int diag_mode(const char*, int full) { return full; }
 constexpr int fused_mode() { return 27; }
 #endif
+
+// the side stream and events of the grand products (created on first use)
+int ensure_side(b2f_ctx* ctx) {
+  if (!ctx->s2) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
+  if (!ctx->ev_fork) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+  if (!ctx->ev_join) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+  return B2F_OK;
+}
 
 uint64_t layout_rows(uint32_t rounds) {
   if (rounds > B2F_MAX_ROUNDS) return 0;
@@ -1058,6 +1072,9 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
   (void)hipFree(ctx->d_pm);
   if (ctx->pm_inst_ev_live) (void)hipEventSynchronize(ctx->pm_inst_ev);
   if (ctx->pm_inst_ev) (void)hipEventDestroy(ctx->pm_inst_ev);
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+  if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
   (void)hipHostFree(ctx->h_pm_inst);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   delete ctx;
@@ -1376,8 +1393,8 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
   if (n_circuits == 0) return B2F_OK;
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(ctx, hipSetDevice(ctx->device));
-  // circuits per pass: per-circuit scratch is 1 MiB + 64 B per row + 64 B per 64-row chunk;
-  // keep it under 1 GiB
+  // circuits per pass: per-circuit scratch is 1 MiB (count, pos, D, LP, samples) + 64 B per
+  // row (num, den) + the grand product's chunk scratch; keep it under 1 GiB
   const uint64_t per = (4ull << 18) + usable_rows * 64 + ((usable_rows + 63) / 64) * 64;
   uint32_t group = (uint32_t)((1ull << 30) / per);
   if (group < 1) group = 1;
@@ -1391,10 +1408,11 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
     HIPCHK(ctx, hipMalloc(&ctx->d_lk, need));
     ctx->lk_cap = need;
   }
+  if (int rc = ensure_side(ctx)) return rc;
   int tk = timed_begin(ctx, B2F_KERNEL_LOOKUP, s);
   HIPCHK(ctx, launch_lookup(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, theta, beta,
                             gamma, form, d_out, out_rows, d_first_bad, ctx->d_lk, group,
-                            ctx->d_status + 2, s));
+                            ctx->d_status + 2, ctx->s2, ctx->ev_fork, ctx->ev_join, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
@@ -1531,10 +1549,12 @@ B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, 
   HIPCHK(ctx, hipMemcpyAsync(ctx->d_pm_inst, it, 8 * m, hipMemcpyHostToDevice, s));
   HIPCHK(ctx, hipEventRecord(ctx->pm_inst_ev, s));
   ctx->pm_inst_ev_live = true;
+  if (int rc = ensure_side(ctx)) return rc;
   int tk = timed_begin(ctx, B2F_KERNEL_PERM, s);
   HIPCHK(ctx, launch_permutation(d_advice, total_rows, row0, ctx->d_pm_inst, n, ctx->d_pm_pool, k,
                                  usable_rows, omega, delta, beta, gamma, chunk_len, form, d_sigma,
-                                 d_z, out_rows, ctx->d_pm, ctx->d_status + 2, s));
+                                 d_z, out_rows, ctx->d_pm, ctx->d_status + 2, ctx->s2, ctx->ev_fork,
+                                 ctx->ev_join, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }

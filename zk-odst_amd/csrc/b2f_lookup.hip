@@ -40,7 +40,8 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* d_row_begin, uint32_t n_circuits, uint64_t usable_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
-                         void* scratch, uint32_t group, int* sticky, hipStream_t s);
+                         void* scratch, uint32_t group, int* sticky, hipStream_t s2,
+                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s);
 
 namespace {
 
@@ -435,7 +436,7 @@ template <class F>
 hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint64_t* d_row_begin,
                       uint32_t n_circuits, uint64_t usable_rows, const Chal& ch, bool mont,
                       uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad, void* scratch,
-                      uint32_t group, int* sticky, hipStream_t s) {
+                      uint32_t group, int* sticky, gp::Side side, hipStream_t s) {
   Carve k = carve(scratch, group, usable_rows);
   const dim3 tb(TROWS / 256);
   hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm);
@@ -465,7 +466,7 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
                        d_row_begin, c0, usable_rows, k.Tx, k.Ts, k.pos, k.dcnt, k.lp, k.samp, mont,
                        d_out, out_rows, ch, k.num, k.den);
     e = gp::run<F>(g, usable_rows, mont, d_out + ((uint64_t)c0 * 5 + 4) * out_rows * 4,
-                   5 * out_rows * 4, k.num, k.den, k.zs, nullptr, nullptr, s, nullptr, sticky);
+                   5 * out_rows * 4, k.num, k.den, k.zs, nullptr, nullptr, s, nullptr, sticky, side);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -481,7 +482,9 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* d_row_begin, uint32_t n_circuits, uint64_t usable_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
-                         void* scratch, uint32_t group, int* sticky, hipStream_t s) {
+                         void* scratch, uint32_t group, int* sticky, hipStream_t s2,
+                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s) {
+  const gp::Side side{s2, ev_fork, ev_join};
   Chal ch;
   for (int i = 0; i < 4; i++) {
     ch.theta[i] = theta[i];
@@ -491,9 +494,9 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
   const bool mont = (form & 1u) != 0;
   if (form >> 1)
     return run_lookup<field::Bn254>(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, ch,
-                                    mont, d_out, out_rows, d_first_bad, scratch, group, sticky, s);
+                                    mont, d_out, out_rows, d_first_bad, scratch, group, sticky, side, s);
   return run_lookup<field::Pallas>(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, ch,
-                                   mont, d_out, out_rows, d_first_bad, scratch, group, sticky, s);
+                                   mont, d_out, out_rows, d_first_bad, scratch, group, sticky, side, s);
 }
 
 }  // namespace b2f

@@ -30,7 +30,8 @@ hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uin
                               uint32_t k, uint64_t usable_rows, const uint64_t* omega,
                               const uint64_t* delta, const uint64_t* beta, const uint64_t* gamma,
                               uint32_t chunk_len, uint32_t form, uint64_t* d_sigma, uint64_t* d_z,
-                              uint64_t out_rows, void* scratch, int* sticky, hipStream_t s);
+                              uint64_t out_rows, void* scratch, int* sticky, hipStream_t s2,
+                              hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s);
 
 namespace {
 
@@ -201,7 +202,8 @@ template <class F>
 hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0, const Inst& I,
                     const uint32_t* d_pool, uint32_t k, uint64_t usable, const Params& prm,
                     const uint64_t* gamma, uint32_t chunk_len, bool mont, uint64_t* d_sigma,
-                    uint64_t* d_z, uint64_t out_rows, void* scratch, int* sticky, hipStream_t s) {
+                    uint64_t* d_z, uint64_t out_rows, void* scratch, int* sticky, gp::Side side,
+                    hipStream_t s) {
   const uint32_t sets = (NCOL + chunk_len - 1) / chunk_len;
   Carve m = carve(scratch, k, usable, sets);
   const uint64_t n_rows = 1ull << k, n_hi = n_rows / LO;
@@ -219,7 +221,7 @@ hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0
                      I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, pg, m.num,
                      m.den);
   hipError_t e = gp::run<F>(sets, usable, mont, d_z, out_rows * 4, m.num, m.den, m.zs, nullptr,
-                            nullptr, s, m.seed, sticky);
+                            nullptr, s, m.seed, sticky, side);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }
@@ -236,7 +238,9 @@ hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uin
                               uint32_t k, uint64_t usable_rows, const uint64_t* omega,
                               const uint64_t* delta, const uint64_t* beta, const uint64_t* gamma,
                               uint32_t chunk_len, uint32_t form, uint64_t* d_sigma, uint64_t* d_z,
-                              uint64_t out_rows, void* scratch, int* sticky, hipStream_t s) {
+                              uint64_t out_rows, void* scratch, int* sticky, hipStream_t s2,
+                              hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s) {
+  const gp::Side side{s2, ev_fork, ev_join};
   Params prm;
   for (int i = 0; i < 4; i++) {
     prm.omega[i] = omega[i];
@@ -250,9 +254,9 @@ hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uin
   const bool mont = (form & 1u) != 0;
   if (form >> 1)
     return run_perm<field::Bn254>(d_advice, total_rows, row0, I, d_pool, k, usable_rows, prm, gamma,
-                                  chunk_len, mont, d_sigma, d_z, out_rows, scratch, sticky, s);
+                                  chunk_len, mont, d_sigma, d_z, out_rows, scratch, sticky, side, s);
   return run_perm<field::Pallas>(d_advice, total_rows, row0, I, d_pool, k, usable_rows, prm, gamma,
-                                 chunk_len, mont, d_sigma, d_z, out_rows, scratch, sticky, s);
+                                 chunk_len, mont, d_sigma, d_z, out_rows, scratch, sticky, side, s);
 }
 
 }  // namespace b2f
