@@ -31,6 +31,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "zk-odst_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# The prover columns are bound by 256-bit Montgomery products: tools/mulbench.hip measures 114 G
+# products/s chip-wide for the CIOS product b2f_field.h uses. Products per row:
+# lookup = 2 (permute: num, den factors) + 4 (grand product); permutation = 8 (sigma) + 32 (four
+# per column: two coset values, num and den accumulation) + 3 sets x 4 (grand products).
+MULBENCH_GPS = 114.0
+LOOKUP_PRODUCTS_PER_ROW = 6
+PERM_PRODUCTS_PER_ROW = 52
+# 1 in BN254 Fr Montgomery form (R mod r) as four little-endian int64 limbs
+FR_ONE_MONT = [int.from_bytes((0x0e0a77c19a07df2f666ea36f7879462e36fc76959f60cd29ac96341c4ffffffb
+                               >> (64 * i) & (2**64 - 1)).to_bytes(8, "little"), "little", signed=True)
+               for i in range(4)]
 ADVICE_COLS = 10
 ROW_BYTES = 4 * (ADVICE_COLS + 1)  # 10 advice u32 + 1 fixed u32
 INPUT_BYTES = 216
@@ -148,6 +159,9 @@ def main():
                          "tile as it assigns it; split: the fill kernel then the eval kernel")
     ap.add_argument("--lookup-circuits", type=int, default=64,
                     help="lookup-argument columns for this many 2^17-row circuits of the trace "
+                         "(reported beside the headline; 0 skips)")
+    ap.add_argument("--perm-k", type=int, default=22,
+                    help="permutation-argument columns for one 2^k-row circuit of the trace "
                          "(reported beside the headline; 0 skips)")
     ap.add_argument("--hasher-messages", type=int, default=1 << 16,
                     help="multi-block BLAKE2b over the chip: this many 1 KiB messages "
@@ -519,13 +533,52 @@ def main():
             tot, cnt = eng.kernel_times()["lookup"]
             avg = tot / max(cnt, 1)
             lrows = nc * usable
+            gps = lrows * LOOKUP_PRODUCTS_PER_ROW / (avg * 1e-3) / 1e9
             lookup = {"circuits": nc, "usable_rows": usable, "avg_ms": round(avg, 4),
                       "rows_per_s": round(lrows / (avg * 1e-3)),
                       "algorithmic_GBs": round(lrows * 176 / (avg * 1e-3) / 1e9, 1),
+                      "products_per_row": LOOKUP_PRODUCTS_PER_ROW,
+                      "roofline": {"bound": "field products", "achieved": round(gps, 1),
+                                   "peak": MULBENCH_GPS, "unit": "G products/s",
+                                   "frac": round(gps / MULBENCH_GPS, 4)},
+                      "field": "pasta Fp montgomery",
                       "all_rows_in_table": bool((lbad == -1).all().item())}
             del lout
         except Exception as e:  # reported, never masks the headline
             lookup = {"error": repr(e)}
+    # Permutation-argument prover columns of a 2^k-row circuit cut from
+    # the resident trace: sigma (8 columns) + the grand products of ceil(8 / 3) column sets
+    perm = None
+    if world == 1 and args.perm_k > 0:
+        try:
+            k = args.perm_k
+            usable = (1 << k) - 7
+            n_inst = min(batch.n, usable // 5220)
+            beta, gamma = 0x1234567 << 180, 0x89ABCDEF << 170
+            for _ in range(2):  # the first call builds the mapping pattern and its scratch
+                eng.set_timing(True)
+                sig, z = batch.permutation_columns(eng, k, usable, beta, gamma, chunk_len=3,
+                                                   form=b2f.FP_BN254_MONTGOMERY,
+                                                   instances=(0, n_inst), stream=stream)
+                tot, cnt = eng.kernel_times()["perm"]
+            eng.sync(stream)
+            avg = tot / max(cnt, 1)
+            closes = bool(z[-1, usable].eq(torch.tensor(FR_ONE_MONT, dtype=torch.int64,
+                                                        device=z.device)).all().item())
+            rows = 1 << k
+            gps = rows * PERM_PRODUCTS_PER_ROW / (avg * 1e-3) / 1e9
+            perm = {"k": k, "instances": n_inst, "chunk_len": 3, "sets": 3,
+                    "field": "bn254 Fr montgomery", "avg_ms": round(avg, 4),
+                    "rows_per_s": round(rows / (avg * 1e-3)),
+                    "products_per_row": PERM_PRODUCTS_PER_ROW,
+                    "roofline": {"bound": "field products", "achieved": round(gps, 1),
+                                 "peak": MULBENCH_GPS, "unit": "G products/s",
+                                 "frac": round(gps / MULBENCH_GPS, 4)},
+                    "written_GBs": round(rows * 32 * 11 / (avg * 1e-3) / 1e9, 1),
+                    "z_closes_to_one": closes}
+            del sig, z
+        except Exception as e:  # reported, never masks the headline
+            perm = {"error": repr(e)}
     hasher_aux = None
     if world == 1 and args.hasher_messages > 0:
         try:
@@ -604,7 +657,7 @@ def main():
                "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "floors": floors,
                "other_path": aux,
                "collectives": collectives, "witness_gather": witness, "config4": config4,
-               "fp_export": fp_export, "fp_export_bn254": fp_export_bn254, "lookup_columns": lookup, "hasher": hasher_aux,
+               "fp_export": fp_export, "fp_export_bn254": fp_export_bn254, "lookup_columns": lookup, "permutation_columns": perm, "hasher": hasher_aux,
                "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
                "gpu_vs_cpu_threads": cpu["cores"] if cpu else None}
         print(json.dumps(out), flush=True)

@@ -82,6 +82,30 @@ def test_fused_padded_tail(engine, orc, pad):
     assert rep == orc.evaluate(adv, fixed, batch.offsets_host) and rep["first_failure"] == NONE
 
 
+@pytest.mark.parametrize("pad", [0, 4, 8, 12, 16, 20, 24, 28])
+def test_fused_every_line_offset(engine, orc, pad):
+    """The half-round tiles store whole 128-byte lines: each tile also writes the previous
+    tile's last quads that share its first line (recomputed from the producer chain) and leaves
+    its own last quads to the next tile. Column c's line offset at a tile is (c total_rows +
+    row) mod 32 rows, so total_rows = used + pad over pad = 0 .. 28 puts every column at every
+    offset; the trace must equal the oracle's at each."""
+    import b2f
+
+    x = random_inputs(11, (1, 2, 5), 40 + pad)
+    total = int(b2f.offsets(x)[-1]) + pad
+    batch = _fused(engine, x, total_rows=total)
+    adv, fixed = batch.host_trace()
+    oadv, ofixed, oh, ooff = orc.fill(_as_oracle(x, orc))
+    used = batch.used_rows
+    for c in range(10):
+        bad = np.nonzero(adv[c, :used] != oadv[c])[0]
+        assert bad.size == 0, "pad %d: a_%d differs at rows %s" % (pad, c, bad[:10])
+    assert np.array_equal(fixed[:used], ofixed)
+    assert not adv[:, used:].any() and not fixed[used:].any()
+    rep = batch.report_dict()
+    assert rep == orc.evaluate(adv, fixed, batch.offsets_host) and rep["first_failure"] == NONE
+
+
 def _boundary_rows(total, starts, rng, k):
     """Rows on both sides of the given tile starts, the first/last rows, and random rows."""
     rows = set()

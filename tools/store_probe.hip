@@ -154,6 +154,38 @@ __global__ void __launch_bounds__(256) wave_rr_work(uint32_t* adv, uint64_t tota
   }
 }
 
+// the fused kernel's 52-quad tiles with the lines they share with a neighbouring tile (a partial
+// 128-byte line at each end) stored non-temporal and the whole lines with the default policy:
+// two buffer stores per column, every lane in both, each lane's 16 bytes kept in range by exactly
+// one of them (the other's offset points past the range and is dropped)
+template <int STEP, bool XCD>
+__global__ void __launch_bounds__(256) wave_rr_mixed(uint32_t* adv, uint64_t total_rows, int work) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t bx = XCD ? (uint64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
+  const uint64_t wid = bx * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  const uint64_t total_quads = total_rows >> 2;
+  const uint64_t n_t = (total_quads + STEP - 1) / STEP;
+  for (uint64_t t = wid; t < n_t; t += nw) {
+    const uint64_t q = t * STEP + lane;
+    uint32_t h = (uint32_t)q;
+    for (int k = 0; k < work; k++) h = (h ^ (h >> 7)) * 0x9E3779B1u + (uint32_t)k;
+    const uint32_t nq = (uint32_t)(total_quads - t * STEP < STEP ? total_quads - t * STEP : STEP);
+#pragma unroll
+    for (int c = 0; c < 11; c++) {
+      uint32_t* base = adv + (uint64_t)c * total_rows + 4 * t * STEP;
+      const uint64_t a = reinterpret_cast<uint64_t>(base);
+      const uint32_t lo = (uint32_t)((128 - (a & 127)) & 127);          // bytes before the first whole line
+      const uint32_t hi = nq * 16u - (uint32_t)((a + nq * 16u) & 127);  // bytes up to the last whole line
+      const uint32_t off = 16 * lane;
+      const bool whole = off >= lo && off + 16 <= hi;
+      const i32x4 rsrc = {(int32_t)(uint32_t)a, (int32_t)(uint32_t)(a >> 32), (int32_t)(nq * 16u), 0x00020000};
+      const i32x4 v = {(int32_t)(h + c), (int32_t)(h ^ c), (int32_t)(h * c), (int32_t)(h - c)};
+      probe_buffer_store(v, rsrc, whole ? (int)off : 0x7ffffff0, 0, 0);
+      probe_buffer_store(v, rsrc, whole ? 0x7ffffff0 : (int)off, 0, 2);
+    }
+  }
+}
+
 // interleaved: the tile's work split into 11 parts, each followed by its column's store;
 // STAGGER: wave w of a workgroup first runs (w % 4) / 4 of a tile's work, so the waves of a SIMD
 // are out of phase
@@ -386,6 +418,8 @@ int main(int argc, char** argv) {
       run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<52, false, true, 0, true>), dim3(cus * 2), dim3(256), 0, 0, adv, total, work); });
       snprintf(nm, sizeof nm, "buf_pol0_q64_xcd_work%d_2wg", work);
       run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<64, false, true, 0, true>), dim3(cus * 2), dim3(256), 0, 0, adv, total, work); });
+      snprintf(nm, sizeof nm, "buf_mixed_q52_xcd_work%d_2wg", work);
+      run(nm, [&] { hipLaunchKernelGGL((wave_rr_mixed<52, true>), dim3(cus * 2), dim3(256), 0, 0, adv, total, work); });
       snprintf(nm, sizeof nm, "buf_pol0_q52_work%d_2wg", work);
       run(nm, [&] { hipLaunchKernelGGL((wave_rr_work<52, false, true, 0>), dim3(cus * 2), dim3(256), 0, 0, adv, total, work); });
       snprintf(nm, sizeof nm, "buf_pol0_q64_work%d_2wg", work);

@@ -333,6 +333,22 @@ __device__ __forceinline__ void tile_store(uint32_t* base, uint32_t nq, uint32_t
                       (int)(16 * lane), 0, BUF_NT);
 }
 
+// One column of a quad at LDS word pointer `p`: the test-only injection, then staged.
+template <int MODE>
+__device__ __forceinline__ void emit_at(uint32_t* p, int col, uint64_t qrow, uint32_t v0, uint32_t v1,
+                                        uint32_t v2, uint32_t v3, const Inject& inj) {
+  if (MODE & FZ_INJECT) {
+    if ((inj.row >> 2) == (qrow >> 2) && inj.col == (uint32_t)col) {
+      const uint32_t j = (uint32_t)inj.row & 3u;
+      v0 ^= j == 0 ? inj.mask : 0u;
+      v1 ^= j == 1 ? inj.mask : 0u;
+      v2 ^= j == 2 ? inj.mask : 0u;
+      v3 ^= j == 3 ? inj.mask : 0u;
+    }
+  }
+  *reinterpret_cast<uint4*>(p) = make_uint4(v0, v1, v2, v3);
+}
+
 // One column of this lane's quad: the test-only injection, then staged (wave LDS) or stored
 // (16-byte non-temporal store; column 10 = the fixed column).
 template <int MODE>
@@ -1067,6 +1083,25 @@ static_assert(H_WAVE % 4 == 0 && HW_WORDS % 4 == 0 && T_WD % 4 == 0 && T_GS % 4 
               "16-byte aligned carve");
 static_assert(H_WORDS * 4 * 4 <= 160 * 1024, "four workgroups per CU");
 static_assert(4 * H_WORDS < 65536, "LDS byte addresses fit 16 bits");
+// The fused launch's wave LDS adds TL [11][TL_ROWS] after the eval layout: the previous tile's last
+// seven quads (G 3, quads 6-12), recomputed by lanes TAIL0 .. TAIL0 + 6 from the chain the
+// producer lane HR_Q + 3 publishes at T_GP, so that the wave's stores start on a 128-byte line
+// (fused_hr_kernel, step 5).
+constexpr int TL_ROWS = 28, TAIL0 = 56;
+constexpr int H_TL = HW_WORDS;
+constexpr int HW_WORDS_F = H_TL + NSTAGE * TL_ROWS;
+constexpr int H_WORDS_F = H_WAVE + WAVES * HW_WORDS_F;
+constexpr int T_GP = T_PG + 32;
+static_assert(T_GP + 32 <= NSTAGE * STR, "the producer chain record inside columns a_9 and fixed");
+static_assert(HW_WORDS_F % 4 == 0 && T_GP % 4 == 0, "16-byte aligned carve");
+static_assert(H_WORDS_F * 4 * 3 <= 160 * 1024, "three workgroups per CU");
+static_assert(4 * H_WORDS_F < 65536, "LDS byte addresses fit 16 bits");
+// the quad whose program a lane holds: its own (lanes 0-51), the previous tile's quads 45-51 (the
+// tail lanes), quads 0-3 / 11 again (the producer lanes, lane 63: duplicate checks)
+__host__ __device__ constexpr uint32_t lane_quad(uint32_t lane) {
+  return lane < HR_Q ? lane : (lane >= TAIL0 && lane < TAIL0 + 7) ? lane - (TAIL0 - (HR_Q - 7)) : lane - HR_Q;
+}
+static_assert(lane_quad(TAIL0) == HR_Q - 7 && lane_quad(TAIL0 + 6) == HR_Q - 1, "tail lanes: quads 45-51");
 
 // LDS accesses by byte address (a VGPR holding the address, the offset immediates folded in)
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
@@ -1165,7 +1200,7 @@ struct Lane {
   uint32_t madd, mzm, mhz, mhw, mswap, rsh, fx0;
   uint32_t aWD, aAB, aMX, aGS, aXY, aM, aPG, aLTs, aLTd, ltsh;
   // checks
-  uint32_t aQ;                        // the lane's quad, column a_0 (lanes >= 52: quad 0..11 again)
+  uint32_t aQ;                        // the lane's quad (lane_quad), column a_0
   uint32_t gb, ge, gf, gsel, gm24, gm63, gnl, grs, gsF, gsH;  // XOR-family limb item
   uint32_t ar, m3;                    // ADD block
   uint32_t ce[2][4], cm;              // copies (dst | src << 16), message copy
@@ -1173,7 +1208,7 @@ struct Lane {
 
 __device__ __forceinline__ Lane make_lane(uint32_t lane, uint32_t Sb) {
   Lane L;
-  const uint32_t lq = lane < HR_Q ? lane : lane - HR_Q;
+  const uint32_t lq = lane_quad(lane);
   const uint32_t gg = lq / G_QUADS, p = lq - G_QUADS * gg;
   const QuadProg& Q = c_qprogs.q[p];
 #pragma unroll
@@ -1210,6 +1245,11 @@ __device__ __forceinline__ Lane make_lane(uint32_t lane, uint32_t Sb) {
   L.aGS = Sb + 4 * T_GS + 128 * gg;
   L.aXY = L.aGS + 8 * st;
   L.aM = Sb + 4 * T_GS + 128 * gg + 8 * mi;
+  if (lane == HR_Q + 3) L.aGS = Sb + 4 * T_GP;  // publishes the previous half-round's G 3 chain
+  if (lane >= TAIL0 && lane < TAIL0 + 7) {      // ... which the tail lanes read
+    L.aXY = Sb + 4 * T_GP + 8 * st;
+    L.aM = Sb + 4 * T_GP + 8 * mi;
+  }
   L.aPG = Sb + 4 * T_PG + 32 * (lane - HR_Q);  // producer lanes only
   {  // limb table entry lane = 4 w + k, read from the producer outputs in G order (parity 0 / 1)
     const uint32_t w = lane >> 2, k = lane & 3u, role = w >> 2, pos = w & 3u;
@@ -1357,7 +1397,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
                 b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
                 uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk) {
   using namespace hr2;
-  __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS];
+  __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS_F];
   uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
   auto tick = [&](int k) {
     if (MODE & FZ_CLOCK) {
@@ -1379,12 +1419,14 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
   EvalAcc A{L + H_ACC};
   const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + H_IV);
   const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + H_SG);
-  uint32_t* S = L + H_WAVE + wv * HW_WORDS;  // this wave's staging
+  uint32_t* S = L + H_WAVE + wv * HW_WORDS_F;  // this wave's staging
+  uint32_t* TLp = S + H_TL;                      // ... and the previous tile's tail quads
   const uint32_t Sb = lds_byte(S);
   const uint32_t TB = lds_byte(L + H_SPT);
   const Lane K = make_lane(lane, Sb);
   const bool qlane = lane < HR_Q, p0 = qlane && (lane % G_QUADS) == 0;
   const bool plane = lane >= HR_Q && lane < HR_Q + 4;
+  const bool tlane = lane >= TAIL0 && lane < TAIL0 + 7;
   const uint32_t pg = lane - HR_Q;
 
   if (*status == 0) {  // the record kernel accepted the layout
@@ -1441,8 +1483,8 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       const uint64_t a2 = a1 + b1 + my;
       const uint64_t d2 = rotr64(d1 ^ a2, 16);
       const uint64_t c2 = c1 + d2;
-      if (p0) {
-        const uint32_t g = K.aGS;  // this G's chain record
+      if (p0 || lane == HR_Q + 3) {
+        const uint32_t g = K.aGS;  // this G's chain record (lane HR_Q + 3: G 3 of hr - 1, T_GP)
         st128(g, make_uint4(lo32(a), hi32(a), lo32(d), hi32(d)));
         st128(g + 16, make_uint4(lo32(cc), hi32(cc), lo32(b), hi32(b)));
         st128(g + 32, make_uint4(lo32(a1), hi32(a1), lo32(d1), hi32(d1)));
@@ -1504,10 +1546,12 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       const uint32_t P3 = sel32(K.madd, hi32(X), spread_t(TB, xB)), Q3 = sel32(K.madd, lo32(X), spread_t(TB, xA));
       const uint32_t P4 = sel32(K.madd, hi32(Y), spread_t(TB, yB)), Q4 = sel32(K.madd, lo32(Y), spread_t(TB, yA));
       const uint32_t swA = spread_t(TB, wA), swB = spread_t(TB, wB);
-      if (qlane) {
-        const uint64_t qrow = c.row0 + 4ull * lane;
-auto put = [&](int col, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
-          emit<MODE>(S, col, lane, qrow, v0, v1, v2, v3, adv, fixed, total_rows, inj, true);
+      if (qlane || tlane) {  // tail lanes: the previous tile's quads 45-51, into TL
+        const uint64_t qrow = qlane ? c.row0 + 4ull * lane : c.row0 - TL_ROWS + 4ull * (lane - TAIL0);
+        uint32_t* const q = qlane ? S + 4 * lane : TLp + 4 * (lane - TAIL0);
+        const int qs = qlane ? STR : TL_ROWS;
+        auto put = [&](int col, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
+          emit_at<MODE>(q + col * qs, col, qrow, v0, v1, v2, v3, inj);
         };
         put(A0, tag_of(v[0]), tag_of(v[1]), tag_of(v[2]), tag_of(v[3]));
         put(A1, v[0], v[1], v[2], v[3]);
@@ -1538,23 +1582,31 @@ auto put = [&](int col, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
       // in issue order, so placed after this tile's 11 stores it is vmcnt(11) -- the load and
       // the PREVIOUS tile's stores, issued a tile ago -- never a wait for these stores
       tick(3);
-      // the stores read each staged column of the lane's quad into registers; the lookup and
-      // fixed checks below use those registers (the cells as stored), not a second LDS read.
-      // Lanes 52-63 read quads 0-11 again (their stores fall past the tile's range and are
-      // dropped): those quads' checks, which the lane programs of K are built for.
-      uint4 cq0, cq1, cq2, cfx;
-      const uint32_t ls = lane < HR_Q ? lane : lane - HR_Q;
+      // Line ownership: a 208-row tile is 832 bytes per column, so tile boundaries fall inside
+      // 128-byte lines, and a line written half by one wave and half by another was measured
+      // 15-25 % slower to store (tools/store_probe.hip, profiles/r03i_store_probe_align.jsonl).
+      // Each tile but an instance's first therefore also stores the previous tile's last kc
+      // quads (the head of the line its first row sits in, kc = 0..7 per column, from TL), and
+      // each tile but an instance's last leaves its last tc quads (the head of the line the next
+      // tile starts in) to the next tile: every line inside the instance's half-rounds is
+      // written by one store instruction of one wave.
+      const bool own_head = c.hr != 0, own_tail = c.hr + 1 == 2 * c.rounds;
+      const uint32_t r4 = 4u * (uint32_t)c.row0, tr4 = 4u * (uint32_t)total_rows;
+      const uint32_t adv_lo = (uint32_t)reinterpret_cast<uintptr_t>(adv) + r4;
+      const uint32_t fix_lo = (uint32_t)reinterpret_cast<uintptr_t>(fixed) + r4;
       auto store_cols = [&](int lo, int hi) {
 #pragma unroll
         for (int col = 0; col < NSTAGE; col++) {
           if (col < lo || col >= hi) continue;
-          const uint4 v = *reinterpret_cast<const uint4*>(S + col * STR + 4 * ls);
-          if (col == A0) cq0 = v;
-          if (col == A1) cq1 = v;
-          if (col == A2) cq2 = v;
-          if (col == FXC) cfx = v;
-          if (MODE & FZ_STORE)
-            tile_store((col < 10 ? adv + (uint64_t)col * total_rows : fixed) + c.row0, HR_Q, lane, v);
+          uint32_t* base = (col < 10 ? adv + (uint64_t)col * total_rows : fixed) + c.row0;
+          // the line offset needs only the address's low bits
+          const uint32_t ba = col < 10 ? adv_lo + (uint32_t)col * tr4 : fix_lo;
+          const uint32_t kc = own_head ? (ba >> 4) & 7u : 0u;
+          const uint32_t tc = own_tail ? 0u : ((ba + 16u * HR_Q) >> 4) & 7u;
+          const int32_t sq = (int32_t)lane - (int32_t)kc;  // the staged quad this lane stores
+          const uint32_t* src = sq < 0 ? TLp + col * TL_ROWS + 4 * (7 + sq) : S + col * STR + 4 * sq;
+          const uint4 v = *reinterpret_cast<const uint4*>(src);
+          if (MODE & FZ_STORE) tile_store(base - 4 * kc, HR_Q + kc - tc, lane, v);
         }
       };
 #ifndef B2F_HR_SPLITST
@@ -1569,6 +1621,12 @@ auto put = [&](int col, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
       if (SPLIT == NSTAGE) asm volatile("" ::"v"(Pn));
 #endif
       tick(7);
+      // the lookup and fixed checks read the lane's quad (lane_quad: its K program)
+      const uint32_t ls = lane_quad(lane);
+      const uint4 cq0 = *reinterpret_cast<const uint4*>(S + A0 * STR + 4 * ls);
+      const uint4 cq1 = *reinterpret_cast<const uint4*>(S + A1 * STR + 4 * ls);
+      const uint4 cq2 = *reinterpret_cast<const uint4*>(S + A2 * STR + 4 * ls);
+      const uint4 cfx = *reinterpret_cast<const uint4*>(S + FXC * STR + 4 * ls);
       // ---- 6. fast checks: acc |= (every identity's lhs ^ rhs) -- hr_fast_checks, kept inline
       // here: called as a function it moved the register allocation (hot-loop spill reloads)
       uint32_t acc = 0;

@@ -9,14 +9,15 @@
 // chunk):
 //   gp_chunk:  the chunk's num prefix Nloc_p (written over num in place), the chunk totals of
 //              num and den (2 products per row);
-//   gp_scan:   K'_q = seed N_before(q) prod_{q' > q} D_q' per chunk (K_q = K'_q D^-1), the den
-//              total D and seed N (the closing value seed N / D = z[usable] before its D^-1).
+//   gp_total:  the den total D (from the chunk totals, or from gp_block_reduce's block totals);
+//   gp_scan:   K'_q = seed N_before(q) prod_{q' > q} D_q' per chunk (K_q = K'_q D^-1) and seed N
+//              (the closing value seed N / D = z[usable] before its D^-1).
 //              Up to SCAN_THREADS x 4 chunks one workgroup per product scans them directly;
 //              beyond, three levels over blocks of SCAN_THREADS chunks (gp_block_reduce: block
 //              totals; gp_scan over the block totals; gp_block_down: in-block exclusive prefix /
 //              suffix combined with the block's K'), so the serial run per lane stays short;
 //   gp_inv:    D^-1 (one lane's Kaliski inversion, ~100 us of latency) and the closing values.
-//              It depends only on gp_scan, so it runs on a second stream beside gp_block_down;
+//              It depends only on gp_total, so it runs on a second stream beside the scans;
 //   gp_write:  backward over the chunk: z[p + 1] = K'_q D^-1 Nloc_p prod_{p < i < e} den_i
 //              (2 products per row), converted to the output form and staged through LDS so a
 //              wave's stores cover whole 128-byte row groups.
@@ -129,16 +130,19 @@ __global__ __launch_bounds__(T) void gp_scan(uint64_t nq, Fe* __restrict__ zn,
   }
 }
 
-// D = the product of a product's chunk den totals, straight after gp_chunk (so the inversion can
-// start before the scans): one workgroup per product, a strided product per thread, then a tree.
+// D = the product of a product's den totals: the chunk totals (up to 4 x SCAN_THREADS chunks) or,
+// on the three-level path, gp_block_reduce's block totals -- a few hundred values, so D is ready
+// right after the reduction and the inversion starts before the scans. (Over all chunk totals a
+// workgroup's serial strides took 750 us at 2^22 rows.) One workgroup per product.
+constexpr int TOT_T = 256;
 template <class F>
-__global__ __launch_bounds__(1024) void gp_total(uint64_t nq, const Fe* __restrict__ zd,
-                                                 Fe* __restrict__ dt) {
+__global__ __launch_bounds__(TOT_T) void gp_total(uint64_t n, const Fe* __restrict__ zd,
+                                                  Fe* __restrict__ dt) {
   const uint32_t c = blockIdx.x, t = threadIdx.x;
-  __shared__ Fe sp[1024];
+  __shared__ Fe sp[TOT_T];
   Fe p = field::one<F>();
-  for (uint64_t q = t; q < nq; q += 1024) p = field::mul<F>(p, zd[(uint64_t)c * nq + q]);
-  for (uint32_t w = 512; w > 0; w >>= 1) {
+  for (uint64_t q = t; q < n; q += TOT_T) p = field::mul<F>(p, zd[(uint64_t)c * n + q]);
+  for (uint32_t w = TOT_T / 2; w > 0; w >>= 1) {
     if (t >= w && t < 2 * w) sp[t] = p;
     __syncthreads();
     if (t < w) p = field::mul<F>(p, sp[t + w]);
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(1024) void gp_total(uint64_t nq, const Fe* __restri
 }
 
 // D^-1 in place of D (one lane per product: Kaliski, ~100 us of latency; it needs only gp_total,
-// so it runs on the side stream beside the scans). D = 0: some den factor is zero (a challenge
+// so it runs on the side stream beside the scans and gp_block_down). D = 0: some den factor is zero (a challenge
 // collides with a cell value). halo2's batch_invert would leave that entry zero and the proof
 // would fail; here every z would come from a meaningless inverse, so the call reports
 // B2F_ERR_FIELD at b2f_sync instead.
@@ -364,8 +368,15 @@ hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_
   const uint32_t zq = (uint32_t)((nq + 255) / 256);
   hipError_t e;
   hipLaunchKernelGGL(gp_chunk<F>, dim3(zq, g), dim3(256), 0, s, usable, num, den, zn, zd);
-  hipLaunchKernelGGL(gp_total<F>, dim3(g), dim3(1024), 0, s, nq, zd, dt);
-  const bool fork = side.s2 && nq > 4ull * SCAN_THREADS;  // the scans are long enough to hide it
+  const bool three = nq > 4ull * SCAN_THREADS;
+  if (three)
+    hipLaunchKernelGGL(gp_block_reduce<F>, dim3((uint32_t)nb, g), dim3(SCAN_THREADS), 0, s, nq, zn, zd,
+                       tn, td);
+  if (three)
+    hipLaunchKernelGGL(gp_total<F>, dim3(g), dim3(TOT_T), 0, s, nb, td, dt);
+  else
+    hipLaunchKernelGGL(gp_total<F>, dim3(g), dim3(TOT_T), 0, s, nq, zd, dt);
+  const bool fork = side.s2 && three;  // the scans are long enough to hide it
   if (fork) {
     if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
@@ -374,11 +385,9 @@ hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_
   if (fork && (e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;
   if (nq <= 64) {
     hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nq, zn, zd, seed, sn);
-  } else if (nq <= 4ull * SCAN_THREADS) {
+  } else if (!three) {
     hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, seed, sn);
   } else {
-    hipLaunchKernelGGL(gp_block_reduce<F>, dim3((uint32_t)nb, g), dim3(SCAN_THREADS), 0, s, nq, zn, zd,
-                       tn, td);
     if (nb <= 64)
       hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nb, tn, td, seed, sn);
     else

@@ -41,7 +41,7 @@ constexpr int LO = 1024;   // low table
 constexpr uint32_t ROW_BITS = 29;  // mapping entries: (column << 29) | instance-relative row
 
 struct Params {
-  uint64_t omega[4], delta[4], beta[4];
+  uint64_t omega[4], delta[4], beta[4], gamma[4];
 };
 
 template <class F>
@@ -55,11 +55,14 @@ __device__ Fe pow_u64(Fe b, uint64_t e) {
   return r;
 }
 
-// OL[c][lo] = delta^c w^lo, BL[c][lo] = beta OL[c][lo] (c < 8, lo < 1024); OH[h] = w^(1024 h)
+// OL[c][lo] = delta^c w^lo, BL[c][lo] = beta OL[c][lo] (c < 8, lo < 1024); OH[h] = w^(1024 h);
+// G = gamma (Montgomery form, converted once here rather than per row)
 template <class F>
 __global__ __launch_bounds__(256) void pm_table_kernel(Params prm, uint64_t n_hi, Fe* __restrict__ OL,
-                                                       Fe* __restrict__ BL, Fe* __restrict__ OH) {
+                                                       Fe* __restrict__ BL, Fe* __restrict__ OH,
+                                                       Fe* __restrict__ G) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) G[0] = field::to_mont<F>(field::load_words(prm.gamma));
   const Fe w = field::to_mont<F>(field::load_words(prm.omega));
   if (i < (uint64_t)NCOL * LO) {
     const uint32_t c = (uint32_t)(i / LO), lo = (uint32_t)(i % LO);
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* 
                                                         uint64_t total_rows, uint64_t row0,
                                                         uint64_t usable, uint32_t chunk_len,
                                                         const Fe* __restrict__ BL,
-                                                        const Fe* __restrict__ OH, Params prm_gamma,
+                                                        const Fe* __restrict__ OH, const Fe* __restrict__ G,
                                                         Fe* __restrict__ num, Fe* __restrict__ den) {
   const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (r >= usable) return;
@@ -144,10 +147,10 @@ __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* 
   const uint32_t j0 = set * chunk_len, j1 = j0 + chunk_len < (uint32_t)NCOL ? j0 + chunk_len : NCOL;
   num += (uint64_t)set * gp::elems(usable);
   den += (uint64_t)set * gp::elems(usable);
-  const Fe gamma = field::to_mont<F>(field::load_words(prm_gamma.beta));  // gamma rides in .beta
+  const Fe gamma = G[0];
   const uint32_t ii = inst_of(I.start, I.n, r);
   const uint64_t used = I.start[I.n];
-  Fe n = field::one<F>(), d = field::one<F>();
+  Fe n, d;  // the first column's factors, then one product per further column
 #pragma unroll 1
   for (uint32_t j = j0; j < j1; j++) {
     // advice column a_{j+1}; cells past the circuit's instances are unassigned (zero)
@@ -156,8 +159,10 @@ __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* 
     uint32_t c2;
     uint64_t r2;
     mapped(I, pool, ii, j, r, c2, r2);
-    n = field::mul<F>(n, field::add<F>(vg, dw<F>(BL, OH, j, r)));
-    d = field::mul<F>(d, field::add<F>(vg, dw<F>(BL, OH, c2, r2)));
+    const Fe fn = field::add<F>(vg, dw<F>(BL, OH, j, r));
+    const Fe fd = field::add<F>(vg, dw<F>(BL, OH, c2, r2));
+    n = j == j0 ? fn : field::mul<F>(n, fn);
+    d = j == j0 ? fd : field::mul<F>(d, fd);
   }
   const uint64_t sl = gp::slot_of(r, gp::n_chunks(usable));  // chunk-interleaved (b2f_gprod.h)
   num[sl] = n;
@@ -172,6 +177,7 @@ struct Carve {
   Fe* den;
   Fe* zs;
   Fe* seed;  // chained grand products: closing values and seeds, NCOL each
+  Fe* gm;    // gamma, Montgomery form
   size_t total;
 };
 
@@ -194,6 +200,7 @@ Carve carve(void* base, uint32_t k, uint64_t usable, uint32_t sets) {
   m.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * sets);
   m.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * sets);
   m.seed = (Fe*)take(sizeof(Fe) * 2 * sets);
+  m.gm = (Fe*)take(sizeof(Fe));
   m.total = off;
   return m;
 }
@@ -209,16 +216,14 @@ hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0
   const uint64_t n_rows = 1ull << k, n_hi = n_rows / LO;
   const uint64_t tab = n_hi > (uint64_t)NCOL * LO ? n_hi : (uint64_t)NCOL * LO;
   hipLaunchKernelGGL(pm_table_kernel<F>, dim3((uint32_t)((tab + 255) / 256)), dim3(256), 0, s, prm,
-                     n_hi, m.OL, m.BL, m.OH);
+                     n_hi, m.OL, m.BL, m.OH, m.gm);
   if (d_sigma)
     hipLaunchKernelGGL(pm_sigma_kernel<F>, dim3((uint32_t)((n_rows + 255) / 256)), dim3(256), 0, s, I,
                        d_pool, n_rows, m.OL, m.OH, mont, d_sigma, out_rows);
-  Params pg;
-  for (int i = 0; i < 4; i++) pg.beta[i] = gamma[i];
   // every column set's factors in one launch, then their grand products side by side,
   // chained (set c starts where set c - 1 closed)
   hipLaunchKernelGGL(pm_factor_kernel<F>, dim3((uint32_t)((usable + 255) / 256), sets), dim3(256), 0, s,
-                     I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, pg, m.num,
+                     I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, m.gm, m.num,
                      m.den);
   hipError_t e = gp::run<F>(sets, usable, mont, d_z, out_rows * 4, m.num, m.den, m.zs, nullptr,
                             nullptr, s, m.seed, sticky, side);
@@ -246,6 +251,7 @@ hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uin
     prm.omega[i] = omega[i];
     prm.delta[i] = delta[i];
     prm.beta[i] = beta[i];
+    prm.gamma[i] = gamma[i];
   }
   Inst I;
   I.start = d_inst;
