@@ -47,6 +47,10 @@ using i32x4 = b2f_i32x4;
 constexpr int FW = 64;            // lanes per wave
 constexpr int WAVES = 4;          // waves per workgroup
 constexpr int STR = 208;          // staged rows per column (a half-round tile)
+// the half-round launches' staging column: HPRE rows in front of the tile's 208 (the previous
+// tile's last seven quads, which the fused kernel stores with its own: line ownership), so a
+// column is HSTR = 236 words apart and row -HPRE .. -1 of column c is column c - 1's rows 208 ..
+constexpr int HPRE = 28, HSTR = STR + HPRE;
 constexpr uint32_t HR_Q = 52, INIT_Q = 41, FINAL_Q = 16, PAD_Q = 64;
 constexpr int NSTAGE = 11;        // staged columns a_0 .. a_9 and the fixed column
 constexpr int FXC = 10;           // staging column of the fixed cells
@@ -124,13 +128,16 @@ static_assert(L_IV % 2 == 0 && L_WAVE % 4 == 0, "aligned carve");
 static_assert(L_WORDS * 4 * 4 <= 160 * 1024, "four fused workgroups per CU");
 
 // The staged cells of one wave's tile: column c (a_0 .. a_8) at tile row r.
-struct WaveTile {
+template <int ST>
+struct WaveTileS {
   const uint32_t* S;
-  __device__ __forceinline__ uint32_t at(int c, uint32_t r) const { return S[c * STR + r]; }
+  __device__ __forceinline__ uint32_t at(int c, uint32_t r) const { return S[c * ST + r]; }
   __device__ __forceinline__ uint4 quad(int c, uint32_t r) const {
-    return *reinterpret_cast<const uint4*>(S + c * STR + r);
+    return *reinterpret_cast<const uint4*>(S + c * ST + r);
   }
 };
+using WaveTile = WaveTileS<STR>;   // the edge path's staging
+using HrTile = WaveTileS<HSTR>;    // the half-round launches' staging
 
 // The written trace from row `base` on, cells past the trace reading 0 (LAYOUT.md §6).
 struct GlobalRows {
@@ -170,37 +177,6 @@ struct Ctx {
   uint32_t kind, inst, rounds, hr, nq;
   uint64_t off, st, row0;  // instance offset, its first state index, first row of the tile
 };
-
-[[maybe_unused]] __device__ __forceinline__ Ctx make_ctx(uint64_t t, uint64_t t_inst, const uint4& raw,
-                                        uint64_t used_rows, uint64_t total_rows) {
-  Ctx c;
-  c.inst = __builtin_amdgcn_readfirstlane(raw.x);
-  const uint32_t j = __builtin_amdgcn_readfirstlane(raw.y);
-  c.rounds = __builtin_amdgcn_readfirstlane(raw.z);
-  c.st = __builtin_amdgcn_readfirstlane(raw.w);
-  c.off = 20ull * c.inst + 208ull * c.st;  // off_i = 228 i + 416 sum(rounds), st = 2 sum + i
-  c.hr = 0;
-  if (t >= t_inst) {
-    c.kind = T_PAD;
-    c.row0 = used_rows + (uint64_t)PAD_Q * 4 * (t - t_inst);
-    const uint64_t left = c.row0 < total_rows ? (total_rows - c.row0) >> 2 : 0;
-    c.nq = (uint32_t)(left < PAD_Q ? left : PAD_Q);
-  } else if (j == 0) {
-    c.kind = T_INIT;
-    c.row0 = c.off;
-    c.nq = INIT_Q;
-  } else if (j <= 2 * c.rounds) {
-    c.kind = T_HR;
-    c.hr = j - 1;
-    c.row0 = c.off + INIT_ROWS + 208ull * c.hr;
-    c.nq = HR_Q;
-  } else {
-    c.kind = T_FINAL;
-    c.row0 = c.off + INIT_ROWS + (uint64_t)ROUND_ROWS * c.rounds;
-    c.nq = FINAL_Q;
-  }
-  return c;
-}
 
 // Operand words of one lane for a tile, loaded one tile ahead of their use. Every lane loads
 // all seven words unconditionally from a per-lane address (a harmless in-bounds word where the
@@ -259,13 +235,8 @@ __device__ __forceinline__ Ops load_ops(const Ctx& c, uint32_t lane, const b2f_i
       p[6] = x->m + Sg[16 * ((c.hr >> 1) % 10) + 2 * ((lane >> 3) + 4 * (c.hr & 1u)) + ((lane >> 2) & 1u)];
   }
   Ops o;
-#ifdef B2F_FZ_NOLOAD  // diagnostics: operand words without memory traffic (wrong trace)
-#pragma unroll
-  for (int k = 0; k < 7; k++) o.w[k] = reinterpret_cast<uint64_t>(p[k]) * 0x9E3779B97F4A7C15ull;
-#else
 #pragma unroll
   for (int k = 0; k < 7; k++) o.w[k] = *p[k];
-#endif
   return o;
 }
 
@@ -392,98 +363,6 @@ __device__ __forceinline__ void store_staged(const uint32_t* S, uint32_t lane, u
   for (int col = 0; col < NSTAGE; col++)
     tile_store((col < 10 ? adv + (uint64_t)col * total_rows : fixed) + row0, nq, lane,
                *reinterpret_cast<const uint4*>(S + col * STR + 4 * l));
-}
-
-// A round quad (position p of its G), column by column: the fill's quad_round (LAYOUT.md §4
-// blocks ADD3/ADD2/XOR/XOR24/XOR63 from one recipe), each column emitted as soon as it is
-// known so the quad's 44 cells are never all live at once.
-template <int MODE>
-__device__ __forceinline__ void emit_round_quad(uint32_t* S, uint32_t lane, uint64_t qrow,
-                                                uint64_t a, uint64_t b, uint64_t c, uint64_t d,
-                                                uint64_t mx, uint64_t my, uint32_t p,
-                                                const uint32_t* __restrict__ rows, uint32_t* adv,
-                                                uint32_t* fixed, uint64_t total_rows,
-                                                const Inject& inj) {
-  const uint64_t a1 = a + b + mx;
-  const uint64_t d1 = rotr64(d ^ a1, 32);
-  const uint64_t c1 = c + d1;
-  const uint64_t b1 = rotr64(b ^ c1, 24);
-  const uint64_t a2 = a1 + b1 + my;
-  const uint64_t d2 = rotr64(d1 ^ a2, 16);
-  const uint64_t c2 = c1 + d2;
-  const uint32_t st = step_of_quad(p);
-  const uint64_t X = st == 0 ? a : st == 1 ? d : st == 2 ? c : st == 3 ? b
-                   : st == 4 ? a1 : st == 5 ? d1 : st == 6 ? c1 : b1;
-  const uint64_t Y = st == 0 ? b : st == 1 ? a1 : st == 2 ? d1 : st == 3 ? c1
-                   : st == 4 ? b1 : st == 5 ? a2 : st == 6 ? d2 : c2;
-  const uint64_t M = st == 0 ? mx : st == 4 ? my : 0ull;
-  const uint64_t s1 = X + Y, Sm = s1 + M;
-  const uint32_t carry = (uint32_t)(s1 < X) + (uint32_t)(Sm < s1);
-  const uint64_t Z = X ^ Y, O = X & Y;
-  const uint64_t Wd = st == 3 ? rotr64(Z, 24) : rotr64(Z, 63);
-  const uint4 e = *reinterpret_cast<const uint4*>(rows + 4 * p);
-  const uint32_t sd = rows[4 * G_QUADS + p];
-  uint32_t v[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const uint32_t ej = comp(e, j);
-    const uint32_t srcw = (ej >> 2) & 3u, mcode = (ej >> 5) & 3u;
-    const uint64_t V = srcw == 0 ? Sm : srcw == 1 ? Z : O;
-    v[j] = (uint32_t)(V >> (16 * (ej & 3u) + 8 * ((ej >> 4) & 1u))) &
-           (mcode == 0 ? 0xffffu : mcode == 1 ? 0xffu : 0x7fffu);
-  }
-  emit<MODE>(S, A0, lane, qrow, tag16(v[0]), tag16(v[1]), tag16(v[2]), tag16(v[3]), adv, fixed, total_rows, inj, true);
-  emit<MODE>(S, A1, lane, qrow, v[0], v[1], v[2], v[3], adv, fixed, total_rows, inj, true);
-  emit<MODE>(S, A2, lane, qrow, spread16(v[0]), spread16(v[1]), spread16(v[2]), spread16(v[3]), adv, fixed, total_rows, inj, true);
-  // operand slots A and B (at most two rows of a quad hold spread operand limbs)
-  const uint32_t jA = sd & 3u, shA = 16 * ((sd >> 2) & 3u), jB = (sd >> 5) & 3u, shB = 16 * ((sd >> 7) & 3u);
-  const bool vA = (sd >> 4) & 1u, vB = (sd >> 9) & 1u, has_w = (sd >> 10) & 1u, has_z = (sd >> 11) & 1u;
-  const bool dense = (sd >> 12) & 1u, has_m = (sd >> 13) & 1u;
-  auto slot = [&](uint64_t Wv, int j, uint32_t fA, uint32_t fB) -> uint32_t {
-    (void)Wv;
-    return (vA && jA == (uint32_t)j) ? fA : (vB && jB == (uint32_t)j) ? fB : 0u;
-  };
-  {
-    const uint32_t sA = spread16((uint32_t)(X >> shA) & 0xffffu), sB = spread16((uint32_t)(X >> shB) & 0xffffu);
-    uint32_t o[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) o[j] = dense ? (uint32_t)(X >> (16 * j)) & 0xffffu : slot(X, j, sA, sB);
-    emit<MODE>(S, A3, lane, qrow, o[0], o[1], o[2], o[3], adv, fixed, total_rows, inj, true);
-  }
-  {
-    const uint32_t sA = spread16((uint32_t)(Y >> shA) & 0xffffu), sB = spread16((uint32_t)(Y >> shB) & 0xffffu);
-    uint32_t o[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) o[j] = dense ? (uint32_t)(Y >> (16 * j)) & 0xffffu : slot(Y, j, sA, sB);
-    emit<MODE>(S, A4, lane, qrow, o[0], o[1], o[2], o[3], adv, fixed, total_rows, inj, true);
-  }
-  {
-    uint32_t o[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) o[j] = has_m ? (uint32_t)(M >> (16 * j)) & 0xffffu : 0u;
-    emit<MODE>(S, A5, lane, qrow, o[0], o[1], o[2], o[3], adv, fixed, total_rows, inj, true);
-  }
-  {
-    const uint32_t zA = ((uint32_t)(Z >> shA) & 0xffffu) >> 15, zB = ((uint32_t)(Z >> shB) & 0xffffu) >> 15;
-    uint32_t o[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) o[j] = has_z ? slot(Z, j, zA, zB) : 0u;
-    emit<MODE>(S, A6, lane, qrow, o[0], o[1], o[2], o[3], adv, fixed, total_rows, inj, true);
-  }
-  {
-    const uint32_t wA = (uint32_t)(Wd >> shA) & 0xffffu, wB = (uint32_t)(Wd >> shB) & 0xffffu;
-    uint32_t o[4], q[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      o[j] = has_w ? slot(Wd, j, wA, wB) : 0u;
-      q[j] = has_w ? slot(Wd, j, spread16(wA), spread16(wB)) : 0u;
-    }
-    emit<MODE>(S, A7, lane, qrow, o[0], o[1], o[2], o[3], adv, fixed, total_rows, inj, true);
-    emit<MODE>(S, A8, lane, qrow, q[0], q[1], q[2], q[3], adv, fixed, total_rows, inj, true);
-  }
-  emit<MODE>(S, A9, lane, qrow, (e.x >> 12) & 1u ? carry : 0u, (e.y >> 12) & 1u ? carry : 0u,
-             (e.z >> 12) & 1u ? carry : 0u, (e.w >> 12) & 1u ? carry : 0u, adv, fixed, total_rows, inj, true);
-  emit<MODE>(S, FXC, lane, qrow, e.x >> 16, e.y >> 16, e.z >> 16, e.w >> 16, adv, fixed, total_rows, inj, true);
 }
 
 // A built quad (init / final / zero rows): every column emitted.
@@ -634,7 +513,7 @@ __device__ __forceinline__ void edge_tile(uint32_t* S, uint32_t* accw, const uin
 // message words (the last use of the loaded operands): a1 (x) at +0 and a2 (y) at +28 of
 // every G, lanes 0..31
 template <int MODE, bool REC>
-__device__ __forceinline__ void hr_msg_copies(Fails<REC>& F, const WaveTile& T, uint32_t lane,
+__device__ __forceinline__ void hr_msg_copies(Fails<REC>& F, const HrTile& T, uint32_t lane,
                                               const Ctx& c, uint64_t mw, const uint8_t* Sg,
                                               const Inject& inj) {
   if ((MODE & FZ_COPIES) && lane < 32) {
@@ -654,7 +533,7 @@ __device__ __forceinline__ void hr_msg_copies(Fails<REC>& F, const WaveTile& T, 
 // `ct`: the HrChecks entries of the tile's parity; `state(w, k, spread)`: limb k of state word w
 // as its producer assigned it (dense or spread).
 template <int MODE, bool REC, class StateLimb>
-__device__ __forceinline__ void hr_checks(Fails<REC>& F, const WaveTile& T, uint32_t lane,
+__device__ __forceinline__ void hr_checks(Fails<REC>& F, const HrTile& T, uint32_t lane,
                                           const Ctx& c, const uint32_t* ct, const StateLimb& state,
                                           const Inject& inj, uint64_t* defer, uint32_t defer_cap) {
   const uint32_t nq = c.nq;
@@ -745,190 +624,18 @@ __device__ __forceinline__ void hr_checks(Fails<REC>& F, const WaveTile& T, uint
   }
 }
 
-// PART: the tiles one launch walks. PART_HR: the half-round tiles (96 % of the quads) -- the
-// init / final / zero-row paths compiled out, so this kernel's register budget is the
-// half-round path's alone (no spills: a spill reload is a vector memory load, which would wait
-// for every store the wave has in flight); PART_EDGE: the init and final tiles and the zero
-// rows past the last instance. Both walk their own descriptor list (tile_desc_kernel).
-enum { PART_HR = 1, PART_EDGE = 2 };
-
-template <int MODE, int PART>
-__global__ void __launch_bounds__(FW * WAVES, PART == PART_HR ? B2F_FUSED_WAVES : 3)
-fused_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
-             uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
-             uint32_t* __restrict__ fixed, const TileDesc* __restrict__ desc,
-             b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
-             uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk) {
-  __shared__ __attribute__((aligned(16))) uint32_t L[L_WORDS];
-  uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
-  auto tick = [&](int k) {
-    if (MODE & FZ_CLOCK) {
-      const uint64_t now = __builtin_amdgcn_s_memtime();
-      if (k >= 0) ck[k] += now - tp;
-      tp = now;
-    }
-  };
-  const int tid = threadIdx.x;
-  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
-  if (tid < 22) L[L_ACC + tid] = 0;
-  if (tid == 22) *reinterpret_cast<uint64_t*>(L + L_ACC + 20) = ~0ull;
-  if (tid < 16) L[L_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
-  if (tid < 40) L[L_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
-  if (tid < ROW_TABLE_WORDS) L[L_ROWS + tid] = (&c_rows.r[0][0])[tid];
-  for (int i = tid; i < 2 * HR_CHECKS; i += FW * WAVES) L[L_CT + i] = (&c_hr_checks.e[0][0])[i];
-  __syncthreads();
-  EvalAcc A{L + L_ACC};
-  const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + L_IV);
-  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + L_SG);
-  const uint32_t* rows = L + L_ROWS;
-  uint32_t* S = L + L_WAVE + wv * WAVE_WORDS;  // this wave's staging
-  const WaveTile T{S};
-  uint64_t* prod = reinterpret_cast<uint64_t*>(S + S_PROD);
-
-  if (*status == 0) {  // the record kernel accepted the layout
-    const uint64_t used_rows = off[n];
-    const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
-    const uint64_t t_inst = PART == PART_HR ? n_hr : 2ull * n;
-    const uint64_t t_all = PART == PART_HR ? n_hr : t_inst + ((total_rows - used_rows) / 4 + PAD_Q - 1) / PAD_Q;
-    const uint64_t W = (uint64_t)gridDim.x * WAVES;
-    // wave-uniform tile index: descriptors come in by scalar loads (lgkmcnt), never queued
-    // behind the wave's vector stores
-    uint64_t t = (uint64_t)blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(wv);
-
-    const TileDesc* dsc = PART == PART_EDGE ? desc + n_hr : desc;  // this part's list
-    auto raw_desc = [&](uint64_t tt) -> uint4 {
-      const uint64_t ti = tt < t_inst ? tt : 0;
-      const uint4 v = dsc[ti].v;
-      return tt < t_inst ? v : make_uint4(0, 0, 0, 0);
-    };
-    // software pipeline: operands one tile ahead, descriptors two tiles ahead (every load of
-    // an iteration is issued before its stores: vmcnt retires loads and stores in order)
-    auto ctx_of = [&](uint64_t tt, const uint4& raw) {
-      Ctx k = make_ctx(tt, t_inst, raw, used_rows, total_rows);
-      if (PART == PART_HR) k.kind = T_HR;  // lets the compiler drop the other tile kinds' paths
-      return k;
-    };
-    Ctx c = ctx_of(t, raw_desc(t));
-    Ops P{};
-    if (t < t_all) P = load_ops(c, lane, in, rec, Sg);
-    // the first tile's operands arrive before the loop: otherwise the compiler cannot prove at
-    // the loop header that P is never pending and waits for vmcnt(0) -- every store in flight
-    // -- at P's first use in every iteration
-    settle(P);
-    uint4 dn = raw_desc(t + W);
-    for (; t < t_all; t += W) {
-      tick(-1);
-      const Ctx cn = ctx_of(t + W, dn);
-      const Ops Pn = load_ops(cn, lane, in, rec, Sg);  // past the end: harmless loads
-      dn = raw_desc(t + 2 * W);
-      tick(0);  // next tile's context and loads issued
-      const uint32_t nq = c.nq;
-      const bool qlane = lane < nq;
-      const uint64_t qrow = c.row0 + 4ull * lane;  // this lane's first row
-
-      if (c.kind == T_HR) {
-        // ---- a half-round: 4 G's, lane = quad; lanes 52..55 the previous half-round's G's
-        const uint32_t gg = lane / G_QUADS, p = lane - G_QUADS * gg;
-        if (lane >= HR_Q && lane < HR_Q + 4) producer_words(prod, P, lane - HR_Q, c.hr == 0, c.hr - 1, IV);
-        tick(1);  // producers
-        if (qlane)
-          emit_round_quad<MODE>(S, lane, qrow, P.w[0], P.w[1], P.w[2], P.w[3], P.w[4], P.w[5], p, rows,
-                                adv, fixed, total_rows, inj);
-        tick(2);  // cells computed and staged
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staging is complete
-        __builtin_amdgcn_wave_barrier();
-        Fails<false> F{A, false};
-        hr_msg_copies<MODE, false>(F, T, lane, c, P.w[6], Sg, inj);
-        tick(3);  // staging visible, message copies
-        settle(Pn);
-        tick(4);  // the next tile's operands arrived
-        store_staged<MODE>(S, lane, nq, c.row0, adv, fixed, total_rows);
-        tick(5);  // stores issued
-        const uint32_t* ct = L + L_CT + (c.hr & 1u) * HR_CHECKS;
-        auto state = [&](uint32_t w, uint32_t k, uint32_t sp) {
-          const uint32_t lv = limb(prod[w], k);
-          return sp ? spread16(lv) : lv;
-        };
-        hr_checks<MODE, false>(F, T, lane, c, ct, state, inj, defer, defer_cap);
-        tick(6);  // lookups, fixed column, gates, copies
-        if (__builtin_amdgcn_ballot_w64(F.bad)) {  // rare: a failure in this tile, record it exactly
-          Fails<true> R{A, false};
-          hr_msg_copies<MODE, true>(R, T, lane, c, P.w[6], Sg, inj);
-          hr_checks<MODE, true>(R, T, lane, c, ct, state, inj, defer, defer_cap);
-        }
-      } else if (PART == PART_EDGE && (c.kind == T_INIT || c.kind == T_FINAL)) {
-        settle(Pn);
-#ifndef B2F_FZ_NOEDGE  // diagnostics: the register budget of the half-round path alone
-        edge_tile<MODE>(S, L + L_ACC, IV, inj, adv, fixed, total_rows, defer, defer_cap, c, P, lane);
-#endif
-      } else if (PART == PART_EDGE) {
-        // ---- the zero rows past the last instance: written and checked from registers (a
-        // selector here can only come from the test hook, and its gate is deferred)
-        Quad Q;
-        zero(Q);
-        if (MODE & FZ_INJECT) {
-          if ((inj.row >> 2) == (qrow >> 2)) {
-            const uint32_t j = (uint32_t)inj.row & 3u;
-#pragma unroll
-            for (int jj = 0; jj < 4; jj++) {
-#pragma unroll
-              for (int cc = 0; cc < 10; cc++)
-                if ((uint32_t)cc == inj.col && (uint32_t)jj == j) Q.c[cc][jj] ^= inj.mask;
-              if (inj.col == 10 && (uint32_t)jj == j) Q.fx[jj] ^= inj.mask;
-            }
-          }
-        }
-        settle(Pn);
-        if (MODE & FZ_STORE) {
-#pragma unroll
-          for (int cc = 0; cc < 11; cc++)
-            tile_store((cc < 10 ? adv + (uint64_t)cc * total_rows : fixed) + c.row0, nq, lane,
-                       cc < 10 ? make_uint4(Q.c[cc][0], Q.c[cc][1], Q.c[cc][2], Q.c[cc][3])
-                               : make_uint4(Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]));
-        }
-        if (qlane) {
-          const uint4 fx = make_uint4(Q.fx[0], Q.fx[1], Q.fx[2], Q.fx[3]);
-          if (MODE & FZ_LOOKUP)
-            check_lookups(A, make_uint4(Q.c[A0][0], Q.c[A0][1], Q.c[A0][2], Q.c[A0][3]),
-                          make_uint4(Q.c[A1][0], Q.c[A1][1], Q.c[A1][2], Q.c[A1][3]),
-                          make_uint4(Q.c[A2][0], Q.c[A2][1], Q.c[A2][2], Q.c[A2][3]), qrow);
-          if (MODE & FZ_GATES) {
-            check_fixed(A, fx, make_uint4(0, 0, 0, 0), qrow);
-            defer_rows(fx, qrow, defer, defer_cap);
-          }
-        }
-      }
-      // the staging is rewritten by the next tile: keep the compiler from hoisting those writes
-      // above this tile's reads (the wave's LDS operations execute in order)
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      tick(7);  // copies (and init / final / tail tiles, whole)
-      c = cn;
-      P = Pn;
-    }
-  }
-  if ((MODE & FZ_CLOCK) && lane == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; k++) atomicAdd(&clk[8 * wv + k], (unsigned long long)ck[k]);
-  }
-  __syncthreads();
-  flush_report(A, rep, tid);
-}
-
 // The first tile of wave wv of workgroup b in a persistent grid of `grid` workgroups that takes
 // WAVES * grid consecutive tiles per round. XCD-aware: workgroups are dispatched to the 8 XCDs
 // round-robin (b % 8), so XCD x takes the x-th eighth of every round as one contiguous run --
 // neighbouring tiles (which share boundary cache lines, the previous half-round's state cells and
 // the instance's message rows) sit behind the same L2.
 __device__ __forceinline__ uint64_t first_tile(uint32_t b, uint32_t wv, uint32_t grid) {
-#ifndef B2F_NO_XCD_DEAL
   if (grid % 8 == 0) return ((uint64_t)(b % 8) * (grid / 8) + b / 8) * WAVES + wv;
-#endif
   return (uint64_t)b * WAVES + wv;
 }
 
 // ============================================================================================
-// The half-round launch (PART_HR), second form: a lane's quad position p inside its G never
+// The half-round launch (fused_hr_kernel): a lane's quad position p inside its G never
 // changes from tile to tile, so everything that depends on p alone -- which bytes of which
 // operand word land in every cell, which cells every check reads -- is resolved once per lane
 // before the tile loop (v_perm_b32 byte selectors and LDS byte addresses in registers). Per tile:
@@ -941,7 +648,8 @@ __device__ __forceinline__ uint64_t first_tile(uint32_t b, uint32_t wv, uint32_t
 //      previous half-round's G outputs (the state words' producer values), and every lane
 //      builds one (word, limb) entry of the limb table the copy checks read (dense and spread);
 //   3. cells: a_1 rows and every operand slot by v_perm byte selection, spreads and tags, staged;
-//   4. stores (as the first form);
+//   4. stores: 11 raw buffer stores per tile, each covering whole 128-byte lines (line ownership,
+//      see the store loop);
 //   5. fast checks, every one a 32-bit bitwise accumulation (acc |= lhs ^ rhs): lookups, the
 //      fixed column, all XOR/XOR24/XOR63 limb identities in ONE pass (64 lanes = 64 limb items),
 //      the 16 additions as carry chains, the 256 + 32 copies as pure LDS compares. They assume
@@ -1058,44 +766,32 @@ constexpr bool qprogs_ok() {
 static_assert(qprogs_ok(), "quad programs match the row recipes");
 __constant__ QuadProgs c_qprogs = make_qprogs();
 
-// wave LDS (words): staging [11][STR]; limb table LT: [0, 64) dense, [64, 128) spread limb k of
-// state word w at 4 w + k; MW: the tile's 8 message words (u64, 2 gg + i).
-constexpr int H_LT = NSTAGE * STR;
+// wave LDS (words), relative to S = row 0 of staging column a_0: staging [11][HSTR] from row -HPRE
+// (the region starts HPRE words before S); limb table LT: [0, 64) dense, [64, 128) spread limb k
+// of state word w at 4 w + k; MW: the tile's 8 message words (u64, 2 gg + i).
+constexpr int H_LT = NSTAGE * HSTR - HPRE;
 constexpr int H_MW = H_LT + 128;
-constexpr int HW_WORDS = H_MW + 16;
+constexpr int HW_WORDS = HPRE + H_MW + 16;  // the region
 // transient, inside staging columns a_9 and fixed: WD 56 u64 ([0, 16) state words of the tile
 // in G order, [16, 24) the producers' message words, [24, 40) previous state words in G order,
-// [40, 56) scratch), GS 4 x 16 u64 (the published chains), PG 16 u64 (producer outputs, G order)
-constexpr int T_WD = A9 * STR;
+// [40, 56) scratch), GS 4 x 16 u64 (the published chains), PG 16 u64 (producer outputs, G order),
+// GP 16 u64 (the chain of the previous half-round's G 3, published by producer lane HR_Q + 3 for
+// the tail lanes TAIL0 .. TAIL0 + 6, which recompute its quads 6-12 into rows -28 .. -1)
+constexpr int T_WD = A9 * HSTR;
 constexpr int T_GS = T_WD + 112;
 constexpr int T_PG = T_GS + 128;
-static_assert(T_PG + 32 <= NSTAGE * STR, "transient words inside columns a_9 and fixed");
-// workgroup LDS (words)
-// H_SPT: the byte spread table (256 x u16, spread8(i) at byte 2 i), read by spread_t
-#ifdef B2F_HR_SPT
-constexpr int SPT_WORDS = 128;
-#else
-constexpr int SPT_WORDS = 0;
-#endif
-constexpr int H_ACC = 0, H_IV = 24, H_SG = H_IV + 16, H_SPT = H_SG + 40, H_WAVE = H_SPT + SPT_WORDS;
-constexpr int H_WORDS = H_WAVE + WAVES * HW_WORDS;
-static_assert(H_WAVE % 4 == 0 && HW_WORDS % 4 == 0 && T_WD % 4 == 0 && T_GS % 4 == 0 && T_PG % 4 == 0,
-              "16-byte aligned carve");
-static_assert(H_WORDS * 4 * 4 <= 160 * 1024, "four workgroups per CU");
-static_assert(4 * H_WORDS < 65536, "LDS byte addresses fit 16 bits");
-// The fused launch's wave LDS adds TL [11][TL_ROWS] after the eval layout: the previous tile's last
-// seven quads (G 3, quads 6-12), recomputed by lanes TAIL0 .. TAIL0 + 6 from the chain the
-// producer lane HR_Q + 3 publishes at T_GP, so that the wave's stores start on a 128-byte line
-// (fused_hr_kernel, step 5).
-constexpr int TL_ROWS = 28, TAIL0 = 56;
-constexpr int H_TL = HW_WORDS;
-constexpr int HW_WORDS_F = H_TL + NSTAGE * TL_ROWS;
-constexpr int H_WORDS_F = H_WAVE + WAVES * HW_WORDS_F;
 constexpr int T_GP = T_PG + 32;
-static_assert(T_GP + 32 <= NSTAGE * STR, "the producer chain record inside columns a_9 and fixed");
-static_assert(HW_WORDS_F % 4 == 0 && T_GP % 4 == 0, "16-byte aligned carve");
-static_assert(H_WORDS_F * 4 * 3 <= 160 * 1024, "three workgroups per CU");
-static_assert(4 * H_WORDS_F < 65536, "LDS byte addresses fit 16 bits");
+constexpr int TAIL0 = 56;
+static_assert(T_GP + 32 <= H_LT, "transient words inside columns a_9 and fixed");
+static_assert(HSTR % 4 == 0 && HPRE == 4 * 7, "16-byte quads; seven tail quads in front");
+// workgroup LDS (words)
+constexpr int H_ACC = 0, H_IV = 24, H_SG = H_IV + 16, H_WAVE = H_SG + 40;
+constexpr int H_WORDS = H_WAVE + WAVES * HW_WORDS;
+static_assert(H_WAVE % 4 == 0 && HW_WORDS % 4 == 0 && T_WD % 4 == 0 && T_GS % 4 == 0 && T_PG % 4 == 0 &&
+                  T_GP % 4 == 0,
+              "16-byte aligned carve");
+static_assert(H_WORDS * 4 * 3 <= 160 * 1024, "three workgroups per CU");
+static_assert(4 * H_WORDS < 65536, "LDS byte addresses fit 16 bits");
 // the quad whose program a lane holds: its own (lanes 0-51), the previous tile's quads 45-51 (the
 // tail lanes), quads 0-3 / 11 again (the producer lanes, lane 63: duplicate checks)
 __host__ __device__ constexpr uint32_t lane_quad(uint32_t lane) {
@@ -1137,18 +833,6 @@ __device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) { return (uin
 // tag of a 16-bit value (0: < 2^8, 1: < 2^15, 2: otherwise), branch-free
 __device__ __forceinline__ uint32_t tag_of(uint32_t x) { return ((x + 0xff00u) >> 16) + (x >> 15); }
 __device__ __forceinline__ uint32_t sel32(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
-// spread16 of x (< 2^16) -- optionally (B2F_HR_SPT) by two lookups in a byte spread table at LDS
-// byte address `tb` (4 VALU + 2 LDS reads instead of 8-12 VALU for the shift/mask interleave)
-__device__ __forceinline__ uint32_t spread_t(uint32_t tb, uint32_t x) {
-#ifndef B2F_HR_SPT  // the table form measured 1-7 % slower in the fused kernel (more LDS traffic)
-  return spread16(x);  // x < 2^16 here, or a check whose (x & 0xffff0000) term already flags it
-#else
-  const uint32_t lo = ld16(tb + ((x & 0xffu) << 1));
-  const uint32_t hi = ld16(tb + ((x >> 7) & 0x1feu));
-  return lo | (hi << 16);
-#endif
-}
-
 // A tile as the wave sees it (wave-uniform).
 struct HCtx {
   uint32_t inst, rounds, hr, st;
@@ -1186,11 +870,7 @@ __device__ __forceinline__ uint64_t load_word(const HCtx& c, uint32_t lane, cons
   if (grp < 2 || (ps && grp < 6 && h != 0)) p = rec + 16ull * (c.st + sh) + word;
   else if (grp == 2 || (pm && h != 0)) p = x->m + sidx;
   else if (ps && grp < 6) p = role == 0 ? x->h + gl : role == 1 ? x->h + gl + 4 : (role == 3 && gl < 2) ? x->t + gl : fw;
-#ifdef B2F_FZ_NOLOAD  // diagnostics: the word without memory traffic (wrong trace)
-  return reinterpret_cast<uint64_t>(p) * 0x9E3779B97F4A7C15ull;
-#else
   return *p;
-#endif
 }
 
 // The per-lane constants of the tile loop (resolved once).
@@ -1266,20 +946,20 @@ __device__ __forceinline__ Lane make_lane(uint32_t lane, uint32_t Sb) {
     if (lane < 32) {
       const uint32_t blk = lane >> 2, r = 52 * (blk >> 1) + ((blk & 1u) ? 32u : 4u);
       b = r + 2 * k;
-      E = A1 * STR + b;
-      F = A1 * STR + b;
+      E = A1 * HSTR + b;
+      F = A1 * HSTR + b;
       kind = 0;
     } else if (lane < 48) {
       const uint32_t r = 52 * ((lane - 32) >> 2) + 16;
       b = r + 3 * k;
-      E = A1 * STR + r + 3 * ((k + 1) & 3u) + 1;
-      F = A1 * STR + r + 3 * ((k + 2) & 3u);
+      E = A1 * HSTR + r + 3 * ((k + 1) & 3u) + 1;
+      F = A1 * HSTR + r + 3 * ((k + 2) & 3u);
       kind = 1;
     } else {
       const uint32_t r = 52 * ((lane - 48) >> 2) + 44;
       b = r + 2 * k;
-      E = A6 * STR + r + 2 * ((k + 3) & 3u);
-      F = A1 * STR + b;
+      E = A6 * HSTR + r + 2 * ((k + 3) & 3u);
+      F = A1 * HSTR + b;
       kind = 2;
     }
     L.gb = Sb + 4 * b;
@@ -1307,10 +987,10 @@ __device__ __forceinline__ Lane make_lane(uint32_t lane, uint32_t Sb) {
     for (int it = 0; it < HR_CHECKS / FW; it++) {
       const uint32_t e = c_hr_checks.e[par][it * FW + lane];
       const uint32_t dr = e & 255u, dc = (e >> 8) & 3u;
-      const uint32_t dst = Sb + 4 * ((A3 + dc) * STR + dr);
+      const uint32_t dst = Sb + 4 * ((A3 + dc) * HSTR + dr);
       uint32_t src;
       if (!((e >> 10) & 1u)) {
-        src = Sb + 4 * (wcol((e >> 19) & 3u) * STR + ((e >> 11) & 255u));
+        src = Sb + 4 * (wcol((e >> 19) & 3u) * HSTR + ((e >> 11) & 255u));
       } else {
         const uint32_t w = (e >> 11) & 15u, k = (e >> 15) & 3u, sp = (e >> 17) & 1u;
         src = Sb + 4 * (H_LT + 64 * sp + 4 * w + k);
@@ -1320,14 +1000,14 @@ __device__ __forceinline__ Lane make_lane(uint32_t lane, uint32_t Sb) {
   {  // message copy (lanes 32-63 repeat lanes 0-31)
     const uint32_t l = lane & 31u, mg = l >> 3, which = (l >> 2) & 1u, k = l & 3u;
     const uint32_t dr = 52 * mg + (which ? 28u : 0u) + k;
-    L.cm = (Sb + 4 * (A5 * STR + dr)) | ((Sb + 4 * H_MW + 8 * (2 * mg + which) + 2 * k) << 16);
+    L.cm = (Sb + 4 * (A5 * HSTR + dr)) | ((Sb + 4 * H_MW + 8 * (2 * mg + which) + 2 * k) << 16);
   }
   return L;
 }
 
 }  // namespace hr2
 
-// The fast checks of a staged half-round tile (see the second form's comment): lookups, the fixed
+// The fast checks of a staged half-round tile (see the half-round launch's comment): lookups, the fixed
 // column, every canonical gate block, the 256 state-word / in-tile copies (sources: the staging
 // and the limb table), the lane's message copy against `msrc` (the message limb its producer or
 // the trace holds, read where it is used). Returns the OR of every identity's lhs ^ rhs: 0 iff all hold (given the
@@ -1337,8 +1017,8 @@ __device__ __forceinline__ uint32_t hr_fast_checks(const hr2::Lane& K, uint32_t 
   using namespace hr2;
   uint32_t acc = 0;
   if (MODE & (FZ_LOOKUP | FZ_GATES)) {
-    const uint4 q0 = ld128(K.aQ + 4 * A0 * STR), q1 = ld128(K.aQ + 4 * A1 * STR), q2 = ld128(K.aQ + 4 * A2 * STR);
-    const uint4 fx = ld128(K.aQ + 4 * FXC * STR);
+    const uint4 q0 = ld128(K.aQ + 4 * A0 * HSTR), q1 = ld128(K.aQ + 4 * A1 * HSTR), q2 = ld128(K.aQ + 4 * A2 * HSTR);
+    const uint4 fx = ld128(K.aQ + 4 * FXC * HSTR);
     if (MODE & FZ_LOOKUP) {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
@@ -1351,12 +1031,12 @@ __device__ __forceinline__ uint32_t hr_fast_checks(const hr2::Lane& K, uint32_t 
   if (MODE & FZ_GATES) {
     {  // XOR / XOR24 / XOR63 limb item
       const uint32_t gb = K.gb;
-      const uint32_t x3 = ld32(gb + 4 * A3 * STR), x4 = ld32(gb + 4 * A4 * STR);
-      const uint32_t s0 = ld32(gb + 4 * A2 * STR), s1v = ld32(gb + 4 * (A2 * STR + 1)), s2v = ld32(gb + 4 * (A2 * STR + 2));
-      const uint32_t z6 = ld32(gb + 4 * A6 * STR), t0 = ld32(gb), t1 = ld32(gb + 4);
-      const uint32_t w7 = ld32(gb + 4 * A7 * STR), w8 = ld32(gb + 4 * A8 * STR);
-      const uint32_t E = ld32(K.ge), E2 = ld32(K.ge + 4 * (A2 - A1) * STR);
-      const uint32_t F = ld32(K.gf), H = ld32(K.gf + 4 * (A2 - A1) * STR);
+      const uint32_t x3 = ld32(gb + 4 * A3 * HSTR), x4 = ld32(gb + 4 * A4 * HSTR);
+      const uint32_t s0 = ld32(gb + 4 * A2 * HSTR), s1v = ld32(gb + 4 * (A2 * HSTR + 1)), s2v = ld32(gb + 4 * (A2 * HSTR + 2));
+      const uint32_t z6 = ld32(gb + 4 * A6 * HSTR), t0 = ld32(gb), t1 = ld32(gb + 4);
+      const uint32_t w7 = ld32(gb + 4 * A7 * HSTR), w8 = ld32(gb + 4 * A8 * HSTR);
+      const uint32_t E = ld32(K.ge), E2 = ld32(K.ge + 4 * (A2 - A1) * HSTR);
+      const uint32_t F = ld32(K.gf), H = ld32(K.gf + 4 * (A2 - A1) * HSTR);
       const uint32_t R = s0 + perm(0u, s1v, K.gsel) + ((z6 << 30) & K.gm63) + 2 * sel32(K.gm24, s2v, s1v);
       acc |= (x3 + x4) ^ R;
       acc |= (t0 | (t1 & K.gm24) | (z6 & K.gm63)) & K.gnl;
@@ -1364,9 +1044,9 @@ __device__ __forceinline__ uint32_t hr_fast_checks(const hr2::Lane& K, uint32_t 
       acc |= (((E + (F << K.gsF)) ^ w7) | ((G + (H << K.gsH)) ^ w8)) & K.grs;
     }
     {  // ADD block (lanes 16-63 repeat lanes 0-15)
-      const uint4 s = ld128(K.ar + 4 * A1 * STR), x = ld128(K.ar + 4 * A3 * STR);
-      const uint4 y = ld128(K.ar + 4 * A4 * STR), z = ld128(K.ar + 4 * A5 * STR);
-      const uint32_t a9 = ld32(K.ar + 4 * A9 * STR);
+      const uint4 s = ld128(K.ar + 4 * A1 * HSTR), x = ld128(K.ar + 4 * A3 * HSTR);
+      const uint4 y = ld128(K.ar + 4 * A4 * HSTR), z = ld128(K.ar + 4 * A5 * HSTR);
+      const uint32_t a9 = ld32(K.ar + 4 * A9 * HSTR);
       int32_t cy = 0;
 #pragma unroll
       for (int k = 0; k < 4; k++) {
@@ -1397,7 +1077,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
                 b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
                 uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk) {
   using namespace hr2;
-  __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS_F];
+  __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS];
   uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
   auto tick = [&](int k) {
     if (MODE & FZ_CLOCK) {
@@ -1412,17 +1092,12 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
   if (tid == 22) *reinterpret_cast<uint64_t*>(L + H_ACC + 20) = ~0ull;
   if (tid < 16) L[H_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
   if (tid < 40) L[H_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
-#ifdef B2F_HR_SPT
-  reinterpret_cast<uint16_t*>(L + H_SPT)[tid & 255] = (uint16_t)spread16((uint32_t)tid & 255u);
-#endif
   __syncthreads();
   EvalAcc A{L + H_ACC};
   const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + H_IV);
   const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + H_SG);
-  uint32_t* S = L + H_WAVE + wv * HW_WORDS_F;  // this wave's staging
-  uint32_t* TLp = S + H_TL;                      // ... and the previous tile's tail quads
+  uint32_t* S = L + H_WAVE + wv * HW_WORDS + HPRE;  // this wave's staging (row 0 of column a_0)
   const uint32_t Sb = lds_byte(S);
-  const uint32_t TB = lds_byte(L + H_SPT);
   const Lane K = make_lane(lane, Sb);
   const bool qlane = lane < HR_Q, p0 = qlane && (lane % G_QUADS) == 0;
   const bool plane = lane >= HR_Q && lane < HR_Q + 4;
@@ -1431,17 +1106,9 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
 
   if (*status == 0) {  // the record kernel accepted the layout
     const uint64_t used_rows = off[n];
-#ifdef B2F_XCD_REGION  // diagnostics: XCD x owns the x-th eighth of the tiles as one region
-    const uint64_t n_all = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
-    const uint64_t W = (uint64_t)(gridDim.x / 8) * WAVES;
-    const uint64_t R8 = (n_all + 7) / 8, lo8 = (uint64_t)(blockIdx.x % 8) * R8;
-    const uint64_t n_hr = lo8 + R8 < n_all ? lo8 + R8 : n_all;
-    uint64_t t = lo8 + (uint64_t)(blockIdx.x / 8) * WAVES + __builtin_amdgcn_readfirstlane(wv);
-#else
     const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
     const uint64_t W = (uint64_t)gridDim.x * WAVES;
     uint64_t t = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
-#endif
     auto raw_desc = [&](uint64_t tt) -> uint4 {
       const uint64_t ti = tt < n_hr ? tt : 0;
       const uint4 v = desc[ti].v;
@@ -1450,23 +1117,14 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
     HCtx c = hctx(raw_desc(t));
     uint64_t P = 0;
     if (t < n_hr) P = load_word(c, lane, in, rec, Sg);
-    asm volatile("" ::"v"(P));  // settled before the loop (see the first form)
-#ifdef B2F_HR_PF2  // the word two tiles ahead in flight: the settle waits only for stores two tiles old
-    HCtx cn = hctx(raw_desc(t + W));
-    uint64_t Pn = load_word(cn, lane, in, rec, Sg);
-    uint4 dn = raw_desc(t + 2 * W);
-#else
+    // settled before the loop: otherwise the compiler cannot prove at the loop header that P is
+    // never pending and waits for vmcnt(0) -- every store in flight -- at its first use
+    asm volatile("" ::"v"(P));
     uint4 dn = raw_desc(t + W);
-#endif
     for (; t < n_hr; t += W) {
       tick(-1);
-#ifdef B2F_HR_PF2
-      const HCtx cnn = hctx(dn);
-      const uint64_t Pnn = load_word(cnn, lane, in, rec, Sg);  // past the end: a harmless load
-#else
       const HCtx cn = hctx(dn);
       const uint64_t Pn = load_word(cn, lane, in, rec, Sg);  // past the end: a harmless load
-#endif
       // ---- 1. the tile's words into the wave's LDS
       st64(K.aWD, P);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1512,11 +1170,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
-#ifdef B2F_HR_PF2
-      dn = raw_desc(t + 3 * W);  // scalar load; retires during the assignment
-#else
       dn = raw_desc(t + 2 * W);  // scalar load; retires during the assignment
-#endif
       tick(1);
       // ---- 3. operands of the lane's quad, the lane's limb-table entry
       const uint64_t X = ld64(K.aXY), Y = ld64(K.aXY + 24), M = ld64(K.aM);
@@ -1524,7 +1178,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       const uint32_t pv = ld32(par ? K.aLTs >> 16 : K.aLTs & 0xffffu);
       const uint32_t lv = (pv >> K.ltsh) & 0xffffu;
       st32(K.aLTd, lv);
-      st32(K.aLTd + 256, spread_t(TB, lv));
+      st32(K.aLTd + 256, spread16(lv));
       // ---- 4. the cells
       const uint64_t s1 = X + Y, Sm = s1 + M;
       const uint32_t carry = (uint32_t)(s1 < X) + (uint32_t)(Sm < s1);
@@ -1543,19 +1197,18 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       const uint32_t wA = perm(Wh, Wl, K.slA) & K.mhw, wB = perm(Wh, Wl, K.slB) & K.mhw;
       const uint32_t zA = (perm(hi32(Z), lo32(Z), K.slA) >> 15) & K.mhz;
       const uint32_t zB = (perm(hi32(Z), lo32(Z), K.slB) >> 15) & K.mhz;
-      const uint32_t P3 = sel32(K.madd, hi32(X), spread_t(TB, xB)), Q3 = sel32(K.madd, lo32(X), spread_t(TB, xA));
-      const uint32_t P4 = sel32(K.madd, hi32(Y), spread_t(TB, yB)), Q4 = sel32(K.madd, lo32(Y), spread_t(TB, yA));
-      const uint32_t swA = spread_t(TB, wA), swB = spread_t(TB, wB);
-      if (qlane || tlane) {  // tail lanes: the previous tile's quads 45-51, into TL
-        const uint64_t qrow = qlane ? c.row0 + 4ull * lane : c.row0 - TL_ROWS + 4ull * (lane - TAIL0);
-        uint32_t* const q = qlane ? S + 4 * lane : TLp + 4 * (lane - TAIL0);
-        const int qs = qlane ? STR : TL_ROWS;
+      const uint32_t P3 = sel32(K.madd, hi32(X), spread16(xB)), Q3 = sel32(K.madd, lo32(X), spread16(xA));
+      const uint32_t P4 = sel32(K.madd, hi32(Y), spread16(yB)), Q4 = sel32(K.madd, lo32(Y), spread16(yA));
+      const uint32_t swA = spread16(wA), swB = spread16(wB);
+      if (qlane || tlane) {  // tail lanes: the previous tile's quads 45-51, into rows -28 .. -1
+        const uint64_t qrow = qlane ? c.row0 + 4ull * lane : c.row0 - HPRE + 4ull * (lane - TAIL0);
+        uint32_t* const q = S + 4 * (qlane ? (int)lane : (int)lane - (TAIL0 + 7));  // rows -28 ..
         auto put = [&](int col, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
-          emit_at<MODE>(q + col * qs, col, qrow, v0, v1, v2, v3, inj);
+          emit_at<MODE>(q + col * HSTR, col, qrow, v0, v1, v2, v3, inj);
         };
         put(A0, tag_of(v[0]), tag_of(v[1]), tag_of(v[2]), tag_of(v[3]));
         put(A1, v[0], v[1], v[2], v[3]);
-        put(A2, spread_t(TB, v[0]), spread_t(TB, v[1]), spread_t(TB, v[2]), spread_t(TB, v[3]));
+        put(A2, spread16(v[0]), spread16(v[1]), spread16(v[2]), spread16(v[3]));
         put(A3, perm(P3, Q3, K.slot[0]), perm(P3, Q3, K.slot[1]), perm(P3, Q3, K.slot[2]),
             perm(P3, Q3, K.slot[3]));
         put(A4, perm(P4, Q4, K.slot[0]), perm(P4, Q4, K.slot[1]), perm(P4, Q4, K.slot[2]),
@@ -1575,9 +1228,6 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       tick(2);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staging is complete
       __builtin_amdgcn_wave_barrier();
-#ifdef B2F_HR_SETTLE_EARLY  // diagnostics: the first form's placement (waits for the previous stores)
-      asm volatile("" ::"v"(Pn));
-#endif
       // ---- 5. stores, then the wait for the next tile's word: vmcnt counts loads and stores
       // in issue order, so placed after this tile's 11 stores it is vmcnt(11) -- the load and
       // the PREVIOUS tile's stores, issued a tile ago -- never a wait for these stores
@@ -1586,7 +1236,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       // 128-byte lines, and a line written half by one wave and half by another was measured
       // 15-25 % slower to store (tools/store_probe.hip, profiles/r03i_store_probe_align.jsonl).
       // Each tile but an instance's first therefore also stores the previous tile's last kc
-      // quads (the head of the line its first row sits in, kc = 0..7 per column, from TL), and
+      // quads (the head of the line its first row sits in, kc = 0..7 per column, rows -4 kc ..), and
       // each tile but an instance's last leaves its last tc quads (the head of the line the next
       // tile starts in) to the next tile: every line inside the instance's half-rounds is
       // written by one store instruction of one wave.
@@ -1594,39 +1244,27 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       const uint32_t r4 = 4u * (uint32_t)c.row0, tr4 = 4u * (uint32_t)total_rows;
       const uint32_t adv_lo = (uint32_t)reinterpret_cast<uintptr_t>(adv) + r4;
       const uint32_t fix_lo = (uint32_t)reinterpret_cast<uintptr_t>(fixed) + r4;
-      auto store_cols = [&](int lo, int hi) {
 #pragma unroll
-        for (int col = 0; col < NSTAGE; col++) {
-          if (col < lo || col >= hi) continue;
-          uint32_t* base = (col < 10 ? adv + (uint64_t)col * total_rows : fixed) + c.row0;
-          // the line offset needs only the address's low bits
-          const uint32_t ba = col < 10 ? adv_lo + (uint32_t)col * tr4 : fix_lo;
-          const uint32_t kc = own_head ? (ba >> 4) & 7u : 0u;
-          const uint32_t tc = own_tail ? 0u : ((ba + 16u * HR_Q) >> 4) & 7u;
-          const int32_t sq = (int32_t)lane - (int32_t)kc;  // the staged quad this lane stores
-          const uint32_t* src = sq < 0 ? TLp + col * TL_ROWS + 4 * (7 + sq) : S + col * STR + 4 * sq;
-          const uint4 v = *reinterpret_cast<const uint4*>(src);
-          if (MODE & FZ_STORE) tile_store(base - 4 * kc, HR_Q + kc - tc, lane, v);
-        }
-      };
-#ifndef B2F_HR_SPLITST
-#define B2F_HR_SPLITST NSTAGE
-#endif
-      // diagnostics: B2F_HR_SPLITST < 11 stores the first columns before the checks and the rest
-      // between the gate checks and the copies (a store stream spread over the checks)
-      constexpr int SPLIT = B2F_HR_SPLITST;
-      store_cols(0, SPLIT);
+      for (int col = 0; col < NSTAGE; col++) {
+        uint32_t* base = (col < 10 ? adv + (uint64_t)col * total_rows : fixed) + c.row0;
+        // the line offset needs only the address's low bits
+        const uint32_t ba = col < 10 ? adv_lo + (uint32_t)col * tr4 : fix_lo;
+        const uint32_t kc = own_head ? (ba >> 4) & 7u : 0u;
+        const uint32_t tc = own_tail ? 0u : ((ba + 16u * HR_Q) >> 4) & 7u;
+        const int32_t sq = (int32_t)lane - (int32_t)kc;  // the staged quad this lane stores
+        const uint32_t* src = S + col * HSTR + 4 * sq;  // sq < 0: the rows in front
+        const uint4 v = *reinterpret_cast<const uint4*>(src);
+        if (MODE & FZ_STORE) tile_store(base - 4 * kc, HR_Q + kc - tc, lane, v);
+      }
       tick(4);
-#ifndef B2F_HR_SETTLE_EARLY
-      if (SPLIT == NSTAGE) asm volatile("" ::"v"(Pn));
-#endif
+      asm volatile("" ::"v"(Pn));
       tick(7);
       // the lookup and fixed checks read the lane's quad (lane_quad: its K program)
       const uint32_t ls = lane_quad(lane);
-      const uint4 cq0 = *reinterpret_cast<const uint4*>(S + A0 * STR + 4 * ls);
-      const uint4 cq1 = *reinterpret_cast<const uint4*>(S + A1 * STR + 4 * ls);
-      const uint4 cq2 = *reinterpret_cast<const uint4*>(S + A2 * STR + 4 * ls);
-      const uint4 cfx = *reinterpret_cast<const uint4*>(S + FXC * STR + 4 * ls);
+      const uint4 cq0 = *reinterpret_cast<const uint4*>(S + A0 * HSTR + 4 * ls);
+      const uint4 cq1 = *reinterpret_cast<const uint4*>(S + A1 * HSTR + 4 * ls);
+      const uint4 cq2 = *reinterpret_cast<const uint4*>(S + A2 * HSTR + 4 * ls);
+      const uint4 cfx = *reinterpret_cast<const uint4*>(S + FXC * HSTR + 4 * ls);
       // ---- 6. fast checks: acc |= (every identity's lhs ^ rhs) -- hr_fast_checks, kept inline
       // here: called as a function it moved the register allocation (hot-loop spill reloads)
       uint32_t acc = 0;
@@ -1634,18 +1272,18 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           const uint32_t de = comp(cq1, j);
-          acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(cq0, j)) | (spread_t(TB, de) ^ comp(cq2, j));
+          acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(cq0, j)) | (spread16(de) ^ comp(cq2, j));
         }
       }
       if (MODE & FZ_GATES) {
         {  // XOR / XOR24 / XOR63 limb item
           const uint32_t gb = K.gb;
-          const uint32_t x3 = ld32(gb + 4 * A3 * STR), x4 = ld32(gb + 4 * A4 * STR);
-          const uint32_t s0 = ld32(gb + 4 * A2 * STR), s1v = ld32(gb + 4 * (A2 * STR + 1)), s2v = ld32(gb + 4 * (A2 * STR + 2));
-          const uint32_t z6 = ld32(gb + 4 * A6 * STR), t0 = ld32(gb), t1 = ld32(gb + 4);
-          const uint32_t w7 = ld32(gb + 4 * A7 * STR), w8 = ld32(gb + 4 * A8 * STR);
-          const uint32_t E = ld32(K.ge), E2 = ld32(K.ge + 4 * (A2 - A1) * STR);
-          const uint32_t F = ld32(K.gf), H = ld32(K.gf + 4 * (A2 - A1) * STR);
+          const uint32_t x3 = ld32(gb + 4 * A3 * HSTR), x4 = ld32(gb + 4 * A4 * HSTR);
+          const uint32_t s0 = ld32(gb + 4 * A2 * HSTR), s1v = ld32(gb + 4 * (A2 * HSTR + 1)), s2v = ld32(gb + 4 * (A2 * HSTR + 2));
+          const uint32_t z6 = ld32(gb + 4 * A6 * HSTR), t0 = ld32(gb), t1 = ld32(gb + 4);
+          const uint32_t w7 = ld32(gb + 4 * A7 * HSTR), w8 = ld32(gb + 4 * A8 * HSTR);
+          const uint32_t E = ld32(K.ge), E2 = ld32(K.ge + 4 * (A2 - A1) * HSTR);
+          const uint32_t F = ld32(K.gf), H = ld32(K.gf + 4 * (A2 - A1) * HSTR);
           const uint32_t R = s0 + perm(0u, s1v, K.gsel) + ((z6 << 30) & K.gm63) + 2 * sel32(K.gm24, s2v, s1v);
           acc |= (x3 + x4) ^ R;
           acc |= (t0 | (t1 & K.gm24) | (z6 & K.gm63)) & K.gnl;
@@ -1653,9 +1291,9 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
           acc |= (((E + (F << K.gsF)) ^ w7) | ((G + (H << K.gsH)) ^ w8)) & K.grs;
         }
         {  // ADD block (c_add_blk: each lane one of the 16, 4 lanes per block)
-          const uint4 s = ld128(K.ar + 4 * A1 * STR), x = ld128(K.ar + 4 * A3 * STR);
-          const uint4 y = ld128(K.ar + 4 * A4 * STR), z = ld128(K.ar + 4 * A5 * STR);
-          const uint32_t a9 = ld32(K.ar + 4 * A9 * STR);
+          const uint4 s = ld128(K.ar + 4 * A1 * HSTR), x = ld128(K.ar + 4 * A3 * HSTR);
+          const uint4 y = ld128(K.ar + 4 * A4 * HSTR), z = ld128(K.ar + 4 * A5 * HSTR);
+          const uint32_t a9 = ld32(K.ar + 4 * A9 * HSTR);
           int32_t cy = 0;
 #pragma unroll
           for (int k = 0; k < 4; k++) {
@@ -1665,10 +1303,6 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
           }
           acc |= (uint32_t)cy ^ a9;
         }
-      }
-      if (SPLIT < NSTAGE) {
-        store_cols(SPLIT, NSTAGE);
-        asm volatile("" ::"v"(Pn));
       }
       if (MODE & FZ_GATES) acc |= (cfx.x ^ K.fx0) | cfx.y | cfx.z | cfx.w;
       if (MODE & FZ_COPIES) {
@@ -1694,7 +1328,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
         c1.off = c.off;
         c1.st = c.st;
         c1.row0 = c.row0;
-        const WaveTile T{S};
+        const HrTile T{S};
         const uint32_t* LT = S + H_LT;
         const uint64_t* MW = reinterpret_cast<const uint64_t*>(S + H_MW);
         auto state = [&](uint32_t w, uint32_t k, uint32_t sp) { return LT[64 * sp + 4 * w + k]; };
@@ -1709,10 +1343,6 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       tick(6);
       c = cn;
       P = Pn;
-#ifdef B2F_HR_PF2
-      cn = cnn;
-      Pn = Pnn;
-#endif
     }
   }
   if ((MODE & FZ_CLOCK) && lane == 0) {
@@ -1724,13 +1354,13 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
 }
 
 // ============================================================================================
-// The edge launch (PART_EDGE), second form: ONE wave tile per instance holds both of its edge
+// The edge launch (fused_edge_kernel): ONE wave tile per instance holds both of its edge
 // regions -- the init region on lanes 0-40 (INW h / m / t, FMASK, CONST IV, XOR v12..v14) and the
 // final region on lanes 41-56 (XOR3 + digest), so the init region's h cells (the XOR3 H operands'
 // copy sources) are staged in the same tile; lanes 57-60 recompute the final state from the last
 // half-round (the XOR3 V / U operands' producer values). The zero rows past the last instance
 // follow as 64-quad tiles. Fast 32-bit checks as in the half-round launch; a flagged tile is done
-// again, region by region, by the first form's edge path (assignment, stores, exact checks).
+// again, region by region, by the exact edge path (edge_tile: assignment, stores, exact checks).
 namespace edge2 {
 constexpr uint32_t NQ_I = INIT_Q, NQ_F = FINAL_Q, NQ = INIT_Q + FINAL_Q;  // 41, 16, 57
 constexpr int STR_E = 232;  // staged rows per column: init rows 0-163, final rows 164-227
@@ -1813,12 +1443,12 @@ static_assert(make_edge_checks().e[0] != 0xffffffffu, "120 edge copy checks");
 __constant__ EdgeChecks c_echecks = make_edge_checks();
 
 // wave LDS (words): staging [11][STR_E], limb table (spread limbs of the final state, 4 w + k),
-// producer outputs (16 u64 by word). The first form's edge path reuses the same words with its own
-// carve (staging [11][208], prod, canonical flags), inside this one.
+// producer outputs (16 u64 by word). The exact edge path (edge_tile, in edge_redo_kernel) reuses the same words with
+// its own carve (staging [11][208], prod, canonical flags), inside this one.
 constexpr int E_LT = NSTAGE * STR_E;
 constexpr int E_PROD = E_LT + 64;
 constexpr int EW_WORDS = E_PROD + 32;
-static_assert(EW_WORDS >= WAVE_WORDS, "the first form's edge carve fits");
+static_assert(EW_WORDS >= WAVE_WORDS, "the exact edge path's carve fits");
 constexpr int E_ACC = 0, E_IV = 24, E_SG = E_IV + 16, E_WAVE = E_SG + 40;
 constexpr int E_WORDS = E_WAVE + WAVES * EW_WORDS;
 static_assert(E_WAVE % 4 == 0 && EW_WORDS % 4 == 0 && E_PROD % 2 == 0, "aligned carve");
@@ -2122,7 +1752,7 @@ fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* 
         bool bad = acc != 0;
         if (MODE & FZ_INJECT)  // the test hook: its instance is checked exactly
           bad |= inj.row >= c.off && inj.row < c.off + FIXED_ROWS + (uint64_t)ROUND_ROWS * c.rounds;
-        // rare: the instance goes to the redo list (edge_redo_kernel: the first form's edge path,
+        // rare: the instance goes to the redo list (edge_redo_kernel: the exact edge path,
         // exact bookkeeping); a list slot per instance, so it cannot overflow
         if (__builtin_amdgcn_ballot_w64(bad) && lane == 0) {
           const uint32_t slot = atomicAdd(redo, 1u);
@@ -2180,8 +1810,8 @@ fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* 
   flush_report(A, rep, tid);
 }
 
-// The edge regions of the instances the edge launch flagged, done again by the first form's
-// edge path (assignment and stores repeated with the same values, every check recorded exactly).
+// The edge regions of the instances the edge launch flagged, done again by the exact edge
+// path (assignment and stores repeated with the same values, every check recorded exactly).
 template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES)
 edge_redo_kernel(const b2f_input* __restrict__ in, const uint64_t* __restrict__ off,
@@ -2297,7 +1927,7 @@ constexpr uint32_t EV_BAND = B2F_EVAL_HR_BAND;
 __device__ __forceinline__ uint32_t carry_addr(uint32_t lane, uint32_t Sb, uint32_t par) {
   const Canon cs = canon_state(lane >> 2, 1 + par);  // rows of half-round par of round 0
   const uint32_t ri = cs.row(lane & 3u) - INIT_ROWS - 208 * par;
-  return (Sb + 4 * (cs.dcol * STR + ri)) | ((Sb + 4 * (cs.scol * STR + ri)) << 16);
+  return (Sb + 4 * (cs.dcol * HSTR + ri)) | ((Sb + 4 * (cs.scol * HSTR + ri)) << 16);
 }
 template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES, B2F_EVAL_WAVES_HR)
@@ -2309,13 +1939,10 @@ eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fi
   const int tid = threadIdx.x;
   const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
   if (tid < 40) L[H_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
-#ifdef B2F_HR_SPT
-  reinterpret_cast<uint16_t*>(L + H_SPT)[tid & 255] = (uint16_t)spread16((uint32_t)tid & 255u);
-#endif
   __syncthreads();
   if (*status) return;  // a rejected row map: the eval kernel reports it
   const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + H_SG);
-  uint32_t* S = L + H_WAVE + wv * HW_WORDS;
+  uint32_t* S = L + H_WAVE + wv * HW_WORDS + HPRE;
   const Lane K = make_lane(lane, lds_byte(S));
   const bool qlane = lane < HR_Q;
   const uint32_t lq = qlane ? lane : 0;
@@ -2354,17 +1981,17 @@ eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fi
     asm volatile("" ::: "memory");  // read before the tile's cells overwrite the staging
     if (qlane) {
       uint4* q = reinterpret_cast<uint4*>(S + 4 * lane);
-      q[0 * STR / 4] = cur.c0;
-      q[1 * STR / 4] = cur.c1;
-      q[2 * STR / 4] = cur.c2;
-      q[3 * STR / 4] = cur.c3;
-      q[4 * STR / 4] = cur.c4;
-      q[5 * STR / 4] = cur.c5;
-      q[6 * STR / 4] = cur.c6;
-      q[7 * STR / 4] = cur.c7;
-      q[8 * STR / 4] = cur.c8;
-      q[9 * STR / 4] = cur.c9;
-      q[10 * STR / 4] = cur.c10;
+      q[0 * HSTR / 4] = cur.c0;
+      q[1 * HSTR / 4] = cur.c1;
+      q[2 * HSTR / 4] = cur.c2;
+      q[3 * HSTR / 4] = cur.c3;
+      q[4 * HSTR / 4] = cur.c4;
+      q[5 * HSTR / 4] = cur.c5;
+      q[6 * HSTR / 4] = cur.c6;
+      q[7 * HSTR / 4] = cur.c7;
+      q[8 * HSTR / 4] = cur.c8;
+      q[9 * HSTR / 4] = cur.c9;
+      q[10 * HSTR / 4] = cur.c10;
     }
     S[H_LT + lane] = ltd;
     S[H_LT + 64 + lane] = lts;
@@ -2490,26 +2117,6 @@ __global__ void deferred_gates_kernel(const uint32_t* __restrict__ adv, const ui
 
 constexpr uint32_t DEFER_CAP = 4096;
 
-// the half-round launch: the second form (fused_hr_kernel); -DB2F_FUSED_V1 builds the first
-// (-DB2F_EDGE_V1: the second-form half-round launch with the first-form edge launch)
-#ifdef B2F_FUSED_V1
-#define B2F_HR_KERNEL(M) (fused_kernel<M, PART_HR>)
-#else
-#define B2F_HR_KERNEL(M) (fused_hr_kernel<M>)
-#endif
-#if defined(B2F_FUSED_V1) || defined(B2F_EDGE_V1)
-#define B2F_EDGE_FIRST_FORM 1
-#define B2F_EDGE_KERNEL(M) (fused_kernel<M, PART_EDGE>)
-#define B2F_EDGE_ARG desc
-#define B2F_EDGE_REDO(M)
-#else
-#define B2F_EDGE_KERNEL(M) (fused_edge_kernel<M>)
-#define B2F_EDGE_ARG redo
-#define B2F_EDGE_REDO(M)                                                                          \
-  hipLaunchKernelGGL(edge_redo_kernel<M>, dim3(cu_count), dim3(FW * WAVES), 0, s, d_in, d_off,     \
-                     total_rows, rec, d_adv, d_fixed, redo, d_rep, d_status, inj, defer, DEFER_CAP);
-#endif
-
 }  // namespace
 
 namespace b2f {
@@ -2604,22 +2211,18 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   static int per_cu[2] = {0, 0};
   if (!per_cu[0]) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, B2F_HR_KERNEL(FZ_FULL), FW * WAVES, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fused_hr_kernel<FZ_FULL>, FW * WAVES, 0) !=
             hipSuccess || nb < 1)
       nb = 2;
     per_cu[0] = nb;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, B2F_EDGE_KERNEL(FZ_FULL), FW * WAVES, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fused_edge_kernel<FZ_FULL>, FW * WAVES, 0) !=
             hipSuccess || nb < 1)
       nb = 2;
     per_cu[1] = nb;
   }
-  // the edge tiles (first form: 2 per instance, second form: 1) plus the zero rows; no more
-  // workgroups than they fill (the zero-row count here is an upper bound)
-#ifdef B2F_EDGE_FIRST_FORM
-  const uint64_t edge_tiles = 2ull * n + ((total_rows / 4) + PAD_Q - 1) / PAD_Q;
-#else
+  // the edge tiles (one per instance) plus the zero rows; no more workgroups than they fill
+  // (the zero-row count here is an upper bound)
   const uint64_t edge_tiles = (uint64_t)n + ((total_rows / 4) + PAD_Q - 1) / PAD_Q;
-#endif
   const uint64_t edge_wgs = (edge_tiles + WAVES - 1) / WAVES;
   // Fewer half-round workgroups than fit: 2 per CU (8 waves) write the trace faster than 4 per CU
   // (16 waves) -- a narrower front of tiles in flight (same-process A/B 11.78 vs 12.54 ms)
@@ -2642,13 +2245,15 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   switch (mode) {
 #define B2F_FUSED(M)                                                                               \
   case M:                                                                                          \
-    hipLaunchKernelGGL(B2F_HR_KERNEL(M), dim3(grid), dim3(FW * WAVES), 0, s, d_in, n,              \
-                       d_off, total_rows, rec, d_adv, d_fixed, desc, d_rep, d_status, inj, defer,  \
+    hipLaunchKernelGGL(fused_hr_kernel<M>, dim3(grid), dim3(FW * WAVES), 0, s, d_in, n, d_off,     \
+                       total_rows, rec, d_adv, d_fixed, desc, d_rep, d_status, inj, defer, DEFER_CAP, \
+                       clk);                                                                       \
+    hipLaunchKernelGGL(fused_edge_kernel<M>, dim3(grid_e), dim3(FW * WAVES), 0, s, d_in, n, d_off, \
+                       total_rows, rec, d_adv, d_fixed, redo, d_rep, d_status, inj, defer,         \
                        DEFER_CAP, clk);                                                            \
-    hipLaunchKernelGGL(B2F_EDGE_KERNEL(M), dim3(grid_e), dim3(FW * WAVES), 0, s, d_in, n,           \
-                       d_off, total_rows, rec, d_adv, d_fixed, B2F_EDGE_ARG, d_rep, d_status, inj,  \
-                       defer, DEFER_CAP, clk);                                                     \
-    B2F_EDGE_REDO(M)                                                                               \
+    hipLaunchKernelGGL(edge_redo_kernel<M>, dim3(cu_count), dim3(FW * WAVES), 0, s, d_in, d_off,   \
+                       total_rows, rec, d_adv, d_fixed, redo, d_rep, d_status, inj, defer,         \
+                       DEFER_CAP);                                                                 \
     break;
 #ifdef B2F_DIAG
     B2F_FUSED(0) B2F_FUSED(2) B2F_FUSED(3) B2F_FUSED(10) B2F_FUSED(18) B2F_FUSED(8) B2F_FUSED(16)
