@@ -19,13 +19,14 @@ def main():
     ap.add_argument("--circuits", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--form", type=int, default=1)
+    ap.add_argument("--lib", default=None, help="a variant library (A/B), default the product")
     args = ap.parse_args()
     import torch
 
     import b2f
     from b2f import synth
 
-    eng = b2f.Engine(0)
+    eng = b2f.Engine(0) if not args.lib else b2f.Engine(0, lib_path=args.lib)
     batch = b2f.DeviceBatch(synth.batch(args.instances, rounds=12))
     batch.fill(eng)
     s = torch.cuda.current_stream().cuda_stream
@@ -49,7 +50,7 @@ def main():
     ms, cnt = eng.kernel_times()["lookup"]
     per = ms / cnt
     rows = nc * args.usable
-    print(json.dumps({"circuits": nc, "usable_rows": args.usable, "rows": rows,
+    print(json.dumps({"lib": args.lib or "product", "circuits": nc, "usable_rows": args.usable, "rows": rows,
                       "ms_per_call": round(per, 3), "rows_per_s": round(rows / per * 1e3),
                       "algorithmic_GBps": round(rows * 176 / per / 1e6, 1),
                       "note": "176 B/row algorithmic (16 B read, 160 B written)"}))

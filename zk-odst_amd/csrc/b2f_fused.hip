@@ -278,7 +278,7 @@ __device__ __forceinline__ void producer_words(uint64_t* prod, const Ops& P, uin
 #define B2F_FUSED_WAVES 2
 #endif
 #ifndef B2F_FUSED_HR_PER_CU
-#define B2F_FUSED_HR_PER_CU 2  // half-round launch: workgroups per CU (at most what fits)
+#define B2F_FUSED_HR_PER_CU 3  // half-round launch: workgroups per CU (at most what fits)
 #endif
 enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16, FZ_FULL = 27,
        FZ_CLOCK = 128 };  // per-phase s_memtime totals per wave slot (diagnostics, b2f_debug_clock)
@@ -2224,8 +2224,9 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   // (the zero-row count here is an upper bound)
   const uint64_t edge_tiles = (uint64_t)n + ((total_rows / 4) + PAD_Q - 1) / PAD_Q;
   const uint64_t edge_wgs = (edge_tiles + WAVES - 1) / WAVES;
-  // Fewer half-round workgroups than fit: 2 per CU (8 waves) write the trace faster than 4 per CU
-  // (16 waves) -- a narrower front of tiles in flight (same-process A/B 11.78 vs 12.54 ms)
+  // Fewer half-round workgroups than fit: 3 per CU (12 waves) write the trace faster than 2 or 4
+  // per CU (same-process A/B 11.48 vs 12.89 / 12.91 ms, profiles/r03o_ab_percu.txt): enough
+  // waves to overlap one tile's stores with another's compute, a narrow front of tiles in flight
   int hr_per_cu = per_cu[0] < B2F_FUSED_HR_PER_CU ? per_cu[0] : B2F_FUSED_HR_PER_CU;
 #ifdef B2F_DIAG  // diagnostics: workgroups per CU of the half-round launch
   if (const char* v = getenv("B2F_FUSED_PERCU")) {

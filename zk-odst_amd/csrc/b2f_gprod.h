@@ -207,12 +207,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void gp_block_reduce(uint64_t nq, con
 }
 
 // K_q = KB[b] * (exclusive in-block prefix of zn) * (exclusive in-block suffix of zd), KB[b] the
-// block's K from gp_scan over the block totals. Work-efficient: DOWN_T threads, each owning
-// DOWN_PER consecutive chunks of the block -- thread totals, a DOWN_T-wide scan of them, then a
-// backward pass that leaves each chunk's exclusive zd suffix in zd (not read after this pass) and a
-// forward pass that writes K -- about 90 products per thread instead of a 1,024-wide
-// Hillis-Steele scan's 22 per chunk.
-constexpr int DOWN_T = 64, DOWN_PER = SCAN_THREADS / DOWN_T;
+// block's K from gp_scan over the block totals. DOWN_T threads, each owning DOWN_PER consecutive
+// chunks of the block -- thread totals, a DOWN_T-wide scan of them, then a backward pass that
+// leaves each chunk's exclusive zd suffix in zd (not read after this pass) and a forward pass that
+// writes K -- about 36 products per thread. (64 threads x 16 chunks: ~90 products per thread on
+// one wave per block, 123 us for 64 lookup circuits; a 1,024-wide Hillis-Steele scan: 22 per chunk.)
+constexpr int DOWN_T = 256, DOWN_PER = SCAN_THREADS / DOWN_T;
 template <class F>
 __global__ __launch_bounds__(DOWN_T) void gp_block_down(uint64_t nq, Fe* __restrict__ zn,
                                                         Fe* __restrict__ zd,

@@ -160,7 +160,8 @@ __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* 
     uint64_t r2;
     mapped(I, pool, ii, j, r, c2, r2);
     const Fe fn = field::add<F>(vg, dw<F>(BL, OH, j, r));
-    const Fe fd = field::add<F>(vg, dw<F>(BL, OH, c2, r2));
+    // a cell on no copy cycle maps to itself (about 2/3 of the cells): sigma = delta^j w^r
+    const Fe fd = (c2 == j && r2 == r) ? fn : field::add<F>(vg, dw<F>(BL, OH, c2, r2));
     n = j == j0 ? fn : field::mul<F>(n, fn);
     d = j == j0 ? fd : field::mul<F>(d, fd);
   }
