@@ -289,8 +289,9 @@ enum { FZ_LOOKUP = 1, FZ_STORE = 2, FZ_INJECT = 4, FZ_GATES = 8, FZ_COPIES = 16,
 // the compiler's vmcnt bookkeeping exact: a branch that might skip a tile's stores would make
 // every later wait for an older load wait for those stores too (vmcnt is in order).
 #ifndef B2F_BUF_POLICY
-#define B2F_BUF_POLICY 0  // default (write-back) policy: at 2 workgroups per CU 2.9 % faster than
-                          // non-temporal (2; it had been neutral at 4 per CU), sc0 (1) in between
+#define B2F_BUF_POLICY 2  // non-temporal: at 3 workgroups per CU with line-owned stores 10.93 vs
+                          // 11.24 ms (default write-back) / 11.27 (sc0), profiles/r03t_*; at 2 per
+                          // CU before line ownership the default had been 2.9 % faster
 #endif
 constexpr int BUF_NT = B2F_BUF_POLICY;  // gfx94x/gfx950 cache-policy bits: 1 sc0, 2 non-temporal
 #ifndef B2F_EDGE_BUF_POLICY
@@ -1244,8 +1245,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       const uint32_t r4 = 4u * (uint32_t)c.row0, tr4 = 4u * (uint32_t)total_rows;
       const uint32_t adv_lo = (uint32_t)reinterpret_cast<uintptr_t>(adv) + r4;
       const uint32_t fix_lo = (uint32_t)reinterpret_cast<uintptr_t>(fixed) + r4;
-#pragma unroll
-      for (int col = 0; col < NSTAGE; col++) {
+      auto store_col = [&](int col) {
         uint32_t* base = (col < 10 ? adv + (uint64_t)col * total_rows : fixed) + c.row0;
         // the line offset needs only the address's low bits
         const uint32_t ba = col < 10 ? adv_lo + (uint32_t)col * tr4 : fix_lo;
@@ -1255,10 +1255,9 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
         const uint32_t* src = S + col * HSTR + 4 * sq;  // sq < 0: the rows in front
         const uint4 v = *reinterpret_cast<const uint4*>(src);
         if (MODE & FZ_STORE) tile_store(base - 4 * kc, HR_Q + kc - tc, lane, v);
-      }
-      tick(4);
-      asm volatile("" ::"v"(Pn));
-      tick(7);
+      };
+#pragma unroll
+      for (int col = 0; col < NSTAGE; col++) store_col(col);
       // the lookup and fixed checks read the lane's quad (lane_quad: its K program)
       const uint32_t ls = lane_quad(lane);
       const uint4 cq0 = *reinterpret_cast<const uint4*>(S + A0 * HSTR + 4 * ls);
@@ -1275,6 +1274,9 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
           acc |= (de & 0xffff0000u) | (tag_of(de) ^ comp(cq0, j)) | (spread16(de) ^ comp(cq2, j));
         }
       }
+      tick(4);
+      asm volatile("" ::"v"(Pn));
+      tick(7);
       if (MODE & FZ_GATES) {
         {  // XOR / XOR24 / XOR63 limb item
           const uint32_t gb = K.gb;
