@@ -1884,6 +1884,9 @@ __global__ void eval_desc_kernel(const uint64_t* __restrict__ off, uint32_t n, T
 // The loads of one eval tile (see eval_hr_kernel): the tile's 11 cells of the lane's quad, the
 // lane's limb-table entry (dense, spread) and its message-copy source. Named members, no array:
 // a register array carried across the tile loop was kept in scratch by the compiler.
+// (loaded non-temporally -- __builtin_nontemporal_load -- the pass ran 13 % slower: 11.00 vs
+// 9.70 ms same process, profiles/r03v_ab_eval.txt)
+__device__ __forceinline__ uint4 ev_ld(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
 struct EvCells {
   uint4 c0, c1, c2, c3, c4, c5, c6, c7, c8, c9, c10;
   uint32_t d, sp, mc;
@@ -1894,17 +1897,17 @@ __device__ __forceinline__ EvCells ev_load(const hr2::HCtx& c, uint32_t lane, ui
                                            bool gath) {
   EvCells v;
   const uint32_t* p = adv + c.row0 + 4 * lq;
-  v.c0 = *reinterpret_cast<const uint4*>(p);
-  v.c1 = *reinterpret_cast<const uint4*>(p + total_rows);
-  v.c2 = *reinterpret_cast<const uint4*>(p + 2 * total_rows);
-  v.c3 = *reinterpret_cast<const uint4*>(p + 3 * total_rows);
-  v.c4 = *reinterpret_cast<const uint4*>(p + 4 * total_rows);
-  v.c5 = *reinterpret_cast<const uint4*>(p + 5 * total_rows);
-  v.c6 = *reinterpret_cast<const uint4*>(p + 6 * total_rows);
-  v.c7 = *reinterpret_cast<const uint4*>(p + 7 * total_rows);
-  v.c8 = *reinterpret_cast<const uint4*>(p + 8 * total_rows);
-  v.c9 = *reinterpret_cast<const uint4*>(p + 9 * total_rows);
-  v.c10 = *reinterpret_cast<const uint4*>(fixed + c.row0 + 4 * lq);
+  v.c0 = ev_ld(p);
+  v.c1 = ev_ld(p + total_rows);
+  v.c2 = ev_ld(p + 2 * total_rows);
+  v.c3 = ev_ld(p + 3 * total_rows);
+  v.c4 = ev_ld(p + 4 * total_rows);
+  v.c5 = ev_ld(p + 5 * total_rows);
+  v.c6 = ev_ld(p + 6 * total_rows);
+  v.c7 = ev_ld(p + 7 * total_rows);
+  v.c8 = ev_ld(p + 8 * total_rows);
+  v.c9 = ev_ld(p + 9 * total_rows);
+  v.c10 = ev_ld(fixed + c.row0 + 4 * lq);
   // the limb-table gather only when the previous half-round's tile is not the wave's previous tile
   // (otherwise a read of the tile's own first cells: lines this wave loads anyway, value unused)
   const Canon cs = canon_state(lane >> 2, c.hr);
