@@ -1,0 +1,52 @@
+"""Fp export throughput A/B (b2f_export_fp_dev): 2^25 rows of a filled 12-round trace exported
+in pasta Montgomery and BN254 Montgomery form by each library given, interleaved rep by rep in
+one process (HIP-event kernel time). Diagnostic only:
+    python tools/bench_export.py [--libs a.so,b.so] [--rows N]"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "zk-odst_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", default="", help="variant libraries besides the product")
+    ap.add_argument("--rows", type=int, default=1 << 25)
+    ap.add_argument("--instances", type=int, default=1 << 13)
+    ap.add_argument("--reps", type=int, default=4)
+    args = ap.parse_args()
+    import torch
+
+    import b2f
+    from b2f import synth
+
+    batch = b2f.DeviceBatch(synth.batch(args.instances, rounds=12))
+    prod = b2f.Engine(0)
+    s = torch.cuda.current_stream().cuda_stream
+    batch.fill(prod, s)
+    prod.sync(s)
+    nr = min(args.rows, batch.total_rows)
+    engines = [("product", prod)] + [(os.path.basename(p), b2f.Engine(0, lib_path=os.path.join(ROOT, p)))
+                                     for p in args.libs.split(",") if p]
+    out = torch.empty((10, nr, 4), dtype=torch.int64, device=batch.advice.device)
+    res = {}
+    for rep in range(args.reps):
+        for name, eng in engines:
+            for form in (b2f.FP_MONTGOMERY, b2f.FP_BN254_MONTGOMERY):
+                eng.set_timing(True)
+                batch.export_fp(eng, nrows=nr, out=out, form=form, stream=s)
+                eng.sync(s)
+                tot, cnt = eng.kernel_times()["export"]
+                res.setdefault((name, form), []).append(tot / max(cnt, 1))
+    nbytes = nr * 10 * 36
+    for (name, form), v in res.items():
+        best = min(v[1:]) if len(v) > 1 else v[0]
+        print(json.dumps({"lib": name, "form": form, "ms": round(best, 4),
+                          "GBs": round(nbytes / best / 1e6, 1), "all": [round(x, 3) for x in v]}))
+
+
+if __name__ == "__main__":
+    main()
