@@ -33,11 +33,10 @@ sys.path.insert(0, os.path.join(ROOT, "zk-odst_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # The prover columns are bound by 256-bit Montgomery products: tools/mulbench.hip measures 114 G
 # products/s chip-wide for the CIOS product b2f_field.h uses. Products per row:
-# lookup = 2 (permute: num, den factors) + 4 (grand product); permutation = 8 (sigma) + 32 (four
-# per column: two coset values, num and den accumulation) + 3 sets x 4 (grand products).
+# lookup = 2 (permute: num, den factors) + 4 (grand product); permutation: counted per call
+# from the circuit's copy cycles (the permutation leg below).
 MULBENCH_GPS = 114.0
 LOOKUP_PRODUCTS_PER_ROW = 6
-PERM_PRODUCTS_PER_ROW = 52
 # 1 in BN254 Fr Montgomery form (R mod r) as four little-endian int64 limbs
 FR_ONE_MONT = [int.from_bytes((0x0e0a77c19a07df2f666ea36f7879462e36fc76959f60cd29ac96341c4ffffffb
                                >> (64 * i) & (2**64 - 1)).to_bytes(8, "little"), "little", signed=True)
@@ -45,6 +44,52 @@ FR_ONE_MONT = [int.from_bytes((0x0e0a77c19a07df2f666ea36f7879462e36fc76959f60cd2
 ADVICE_COLS = 10
 ROW_BYTES = 4 * (ADVICE_COLS + 1)  # 10 advice u32 + 1 fixed u32
 INPUT_BYTES = 216
+
+
+class ExtrasWatchdog:
+    """After the headline of an N > 1 run: if the legs that follow (all collective) are not done
+    within `timeout` seconds -- one rank failed where the others wait in a collective -- rank 0
+    prints the headline's JSON line with "extras" marked timed out and every rank ends with
+    exit code 0 (each rank runs its own timer, started at the same barrier). timeout 0: off."""
+
+    def __init__(self, timeout, rank, headline, exit_fn=None, out=None):
+        import threading
+
+        self._lock = threading.Lock()
+        self._done = False
+        self._rank = rank
+        self._headline = headline
+        self._exit = exit_fn or os._exit
+        self._out = out or sys.stdout
+        self._timeout = timeout
+        self._timer = None
+        if timeout > 0:
+            self._timer = threading.Timer(timeout, self._fire)
+            self._timer.daemon = True
+            self._timer.start()
+
+    def _fire(self):
+        with self._lock:
+            if self._done:
+                return
+            self._done = True
+            if self._rank == 0:
+                line = self._headline()
+                line["extras"] = {"error": "timed out after %g s; the headline fields are "
+                                           "complete" % self._timeout}
+                self._out.write(json.dumps(line) + "\n")
+                self._out.flush()
+        self._exit(0)
+
+    def finish(self):
+        """True if the caller prints the line (the watchdog did not fire)."""
+        with self._lock:
+            if self._done:
+                return False
+            self._done = True
+        if self._timer is not None:
+            self._timer.cancel()
+        return True
 
 
 def log(*a):
@@ -181,6 +226,11 @@ def main():
                     help="treat every rank as having at most this much free HBM when deciding "
                          "whether a witness gather fits (0 = the real free memory; rehearses "
                          "the skip branch)")
+    ap.add_argument("--extras-timeout", type=float, default=600.0,
+                    help="N > 1: seconds allowed for everything after the headline (collectives "
+                         "timed alone, witness gathers, the config-4 leg); past it rank 0 prints "
+                         "the headline line with the extras marked timed out and every rank exits "
+                         "(0 = no limit)")
     ap.add_argument("--aux-steps", type=int, default=5,
                     help="steps of the other path timed after the headline loop (0 = skip)")
     ap.add_argument("--floor-reps", type=int, default=3,
@@ -371,29 +421,6 @@ def main():
     value = total_n * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
 
-    collectives = None
-    witness = None
-    if world > 1:
-        collectives = collectives_alone(batch, info, args.steps)
-        if global_n:
-            witness = witness_gather(batch.advice, batch.fixed, info["rows"],
-                                     "the step's own trace (%d instances)" % global_n)
-        elif args.witness_gather > 0:
-            try:
-                nw = args.witness_gather
-                xr = synth.rounds_of(world * nw, rounds=args.rounds, rounds_mix=mix)
-                wshards = [(r * nw, (r + 1) * nw) for r in range(world)]
-                wrows, _ = bdist.shard_rows(xr, wshards)
-                xw = synth.batch(nw, rounds=args.rounds, rounds_mix=mix, first=rank * nw)
-                wb = b2f.DeviceBatch(xw, device=device, total_rows=bdist.trace_window(wrows))
-                wb.fill(eng, stream)
-                eng.sync(stream)
-                witness = witness_gather(wb.advice, wb.fixed, wrows,
-                                         "a separate %d-instance batch per rank" % nw)
-                del wb
-            except Exception as e:
-                witness = {"error": repr(e)}
-
     # roofline: algorithmic bytes per launch / average launch duration (HIP events)
     n = n_local
     fill_bytes = n * INPUT_BYTES + rows * ROW_BYTES      # inputs read + trace written
@@ -427,6 +454,59 @@ def main():
         pass
     roof = {"bound": "hbm", "achieved": kern[dom]["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": kern[dom]["frac"], "traffic": traffic, "kernel": dom}
+
+    def headline():
+        """The contract's fields of the JSON line, complete once the headline loop is done."""
+        if global_n:
+            workload = ("%d x %s-round BLAKE2f compressions sharded over %d GPUs (row-balanced): "
+                        "Table16 witness fill + constraint eval (LAYOUT v1)"
+                        % (global_n, "{1,4,12}-mixed" if mix else args.rounds, world))
+        else:
+            workload = ("%d x %s-round BLAKE2f compressions per GPU: Table16 witness fill + "
+                        "constraint eval (LAYOUT v1)"
+                        % (n, "{1,4,12}-mixed" if mix else args.rounds))
+        return {"metric": "BLAKE2f compressions/sec (witness+constraint eval), 2^18 batch, "
+                          "1/2/4/8 GPU",
+                "value": round(value, 1), "unit": "compressions/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+                "higher_is_better": True, "scaling": "strong" if global_n else "weak",
+                "vs_baseline": None, "dtype": "u32",
+                "data": "synthetic (seeded splitmix64 h/m/t/f)",
+                "config": {"workload": workload, "batch_per_gpu": n, "global_batch": total_n,
+                           "rounds": "mix{1,4,12}" if mix else args.rounds,
+                           "rows_per_gpu": rows, "trace_bytes_per_gpu": rows * ROW_BYTES,
+                           "path": args.path,
+                           "parallelism": "dp%d (instance shards)" % world},
+                "roofline": roof, "cpu_baseline": None, "kernels": kern}
+
+    # N > 1: the legs after the headline use collectives; one that hangs (a rank failing where
+    # the others wait) must not cost the headline line, so a watchdog prints it and ends every
+    # rank once the extras run past --extras-timeout (ExtrasWatchdog)
+    watchdog = ExtrasWatchdog(args.extras_timeout if world > 1 else 0, rank, headline)
+
+    collectives = None
+    witness = None
+    if world > 1:
+        collectives = collectives_alone(batch, info, args.steps)
+        if global_n:
+            witness = witness_gather(batch.advice, batch.fixed, info["rows"],
+                                     "the step's own trace (%d instances)" % global_n)
+        elif args.witness_gather > 0:
+            try:
+                nw = args.witness_gather
+                xr = synth.rounds_of(world * nw, rounds=args.rounds, rounds_mix=mix)
+                wshards = [(r * nw, (r + 1) * nw) for r in range(world)]
+                wrows, _ = bdist.shard_rows(xr, wshards)
+                xw = synth.batch(nw, rounds=args.rounds, rounds_mix=mix, first=rank * nw)
+                wb = b2f.DeviceBatch(xw, device=device, total_rows=bdist.trace_window(wrows))
+                wb.fill(eng, stream)
+                eng.sync(stream)
+                witness = witness_gather(wb.advice, wb.fixed, wrows,
+                                         "a separate %d-instance batch per rank" % nw)
+                del wb
+            except Exception as e:
+                witness = {"error": repr(e)}
+
 
     # same-box floors, from the diagnostics library (libb2f_diag.so; the product library has
     # no diagnostic variants): the fill with its stores but no cell computation
@@ -566,11 +646,19 @@ def main():
             closes = bool(z[-1, usable].eq(torch.tensor(FR_ONE_MONT, dtype=torch.int64,
                                                         device=z.device)).all().item())
             rows = 1 << k
-            gps = rows * PERM_PRODUCTS_PER_ROW / (avg * 1e-3) / 1e9
+            # products this call executes: sigma 8 per row of the 2^k domain; per usable row 8
+            # num coset values, 10 accumulations (sets of 3, 3, 2 columns) and 4 per set of
+            # grand product, plus one den coset value per cell on a copy cycle (the others map
+            # to themselves and reuse the num value)
+            mp = b2f.permutation_mapping(12)
+            ident = ((mp >> 29) == np.arange(8, dtype=np.uint32)[:, None]) & \
+                ((mp & ((1 << 29) - 1)) == np.arange(mp.shape[1], dtype=np.uint32)[None, :])
+            products = rows * 8 + usable * 30 + int((~ident).sum()) * n_inst
+            gps = products / (avg * 1e-3) / 1e9
             perm = {"k": k, "instances": n_inst, "chunk_len": 3, "sets": 3,
                     "field": "bn254 Fr montgomery", "avg_ms": round(avg, 4),
                     "rows_per_s": round(rows / (avg * 1e-3)),
-                    "products_per_row": PERM_PRODUCTS_PER_ROW,
+                    "products_per_row": round(products / rows, 2),
                     "roofline": {"bound": "field products", "achieved": round(gps, 1),
                                  "peak": MULBENCH_GPS, "unit": "G products/s",
                                  "frac": round(gps / MULBENCH_GPS, 4)},
@@ -633,33 +721,16 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.rounds, mix, args.cpu_seconds, args.cpu_threads)
 
+    out = headline()
+    out.update({"cpu_baseline": cpu, "floors": floors, "other_path": aux,
+                "collectives": collectives, "witness_gather": witness, "config4": config4,
+                "fp_export": fp_export, "fp_export_bn254": fp_export_bn254,
+                "lookup_columns": lookup, "permutation_columns": perm, "hasher": hasher_aux,
+                "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
+                "gpu_vs_cpu_threads": cpu["cores"] if cpu else None})
+    if not watchdog.finish():
+        return  # the watchdog printed the line and is ending the process
     if rank == 0:
-        if global_n:
-            workload = ("%d x %s-round BLAKE2f compressions sharded over %d GPUs (row-balanced): "
-                        "Table16 witness fill + constraint eval (LAYOUT v1)"
-                        % (global_n, "{1,4,12}-mixed" if mix else args.rounds, world))
-        else:
-            workload = ("%d x %s-round BLAKE2f compressions per GPU: Table16 witness fill + "
-                        "constraint eval (LAYOUT v1)"
-                        % (n, "{1,4,12}-mixed" if mix else args.rounds))
-        out = {"metric": "BLAKE2f compressions/sec (witness+constraint eval), 2^18 batch, "
-                         "1/2/4/8 GPU",
-               "value": round(value, 1), "unit": "compressions/s", "n_gpus": world,
-               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-               "higher_is_better": True, "scaling": "strong" if global_n else "weak",
-               "vs_baseline": None, "dtype": "u32",
-               "data": "synthetic (seeded splitmix64 h/m/t/f)",
-               "config": {"workload": workload, "batch_per_gpu": n, "global_batch": total_n,
-                          "rounds": "mix{1,4,12}" if mix else args.rounds,
-                          "rows_per_gpu": rows, "trace_bytes_per_gpu": rows * ROW_BYTES,
-                          "path": args.path,
-                          "parallelism": "dp%d (instance shards)" % world},
-               "roofline": roof, "cpu_baseline": cpu, "kernels": kern, "floors": floors,
-               "other_path": aux,
-               "collectives": collectives, "witness_gather": witness, "config4": config4,
-               "fp_export": fp_export, "fp_export_bn254": fp_export_bn254, "lookup_columns": lookup, "permutation_columns": perm, "hasher": hasher_aux,
-               "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
-               "gpu_vs_cpu_threads": cpu["cores"] if cpu else None}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
