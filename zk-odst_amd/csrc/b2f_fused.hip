@@ -165,7 +165,7 @@ __device__ __forceinline__ uint32_t inj_at(const Inject& inj, uint64_t row, uint
 
 enum : uint32_t { T_INIT = 0, T_HR, T_FINAL, T_PAD };
 
-union TileDesc {  // 16 B, written by tile_desc_kernel
+union TileDesc {  // 16 B, written by eval_desc_kernel
   struct {
     uint32_t inst, j, rounds, st;
   } f;
@@ -772,7 +772,15 @@ __constant__ QuadProgs c_qprogs = make_qprogs();
 // of state word w at 4 w + k; MW: the tile's 8 message words (u64, 2 gg + i).
 constexpr int H_LT = NSTAGE * HSTR - HPRE;
 constexpr int H_MW = H_LT + 128;
-constexpr int HW_WORDS = HPRE + H_MW + 16;  // the region
+// carried from tile to tile by the half-round launch (a wave walks an instance's half-rounds in
+// order): OUT [2][16] u64 -- by parity, the G outputs of the wave's previous tile in its G order
+// (the state as this tile starts, and the copy sources of its state-word cells); GP [2][16] u64 --
+// by parity, the previous tile's G 3 chain record (the tail lanes'); IN [27] u64 -- the
+// instance's input record (h, m, t, rounds | f)
+constexpr int H_OUT = H_MW + 16;
+constexpr int H_GP = H_OUT + 64;
+constexpr int H_IN = H_GP + 64;
+constexpr int HW_WORDS = HPRE + H_IN + 56;  // the region
 // transient, inside staging columns a_9 and fixed: WD 56 u64 ([0, 16) state words of the tile
 // in G order, [16, 24) the producers' message words, [24, 40) previous state words in G order,
 // [40, 56) scratch), GS 4 x 16 u64 (the published chains), PG 16 u64 (producer outputs, G order),
@@ -789,7 +797,7 @@ static_assert(HSTR % 4 == 0 && HPRE == 4 * 7, "16-byte quads; seven tail quads i
 constexpr int H_ACC = 0, H_IV = 24, H_SG = H_IV + 16, H_WAVE = H_SG + 40;
 constexpr int H_WORDS = H_WAVE + WAVES * HW_WORDS;
 static_assert(H_WAVE % 4 == 0 && HW_WORDS % 4 == 0 && T_WD % 4 == 0 && T_GS % 4 == 0 && T_PG % 4 == 0 &&
-                  T_GP % 4 == 0,
+                  T_GP % 4 == 0 && H_OUT % 4 == 0 && H_GP % 4 == 0 && H_IN % 4 == 0,
               "16-byte aligned carve");
 static_assert(H_WORDS * 4 * 3 <= 160 * 1024, "three workgroups per CU");
 static_assert(4 * H_WORDS < 65536, "LDS byte addresses fit 16 bits");
@@ -851,35 +859,13 @@ __device__ __forceinline__ HCtx hctx(const uint4& raw) {
   return c;
 }
 
-// The one word lane `lane` loads for tile c (see the WD layout; lanes 16-23 fill MW).
-__device__ __forceinline__ uint64_t load_word(const HCtx& c, uint32_t lane, const b2f_input* __restrict__ in,
-                                              const uint64_t* __restrict__ rec, const uint8_t* Sg) {
-  const b2f_input* x = in + c.inst;
-  const uint64_t* fw = reinterpret_cast<const uint64_t*>(&x->rounds);  // rounds | f << 32
-  const uint32_t h = c.hr, hp = h ? h - 1 : 0;
-  const uint32_t grp = lane >> 3, gl = (lane >> 2) & 3u, role = lane & 3u;
-  const uint32_t gm = (lane >> 1) & 3u, i = lane & 1u;
-  // message lanes: this tile's (16-23) or the producers' half-round (24-31)
-  const bool pm = grp == 3;
-  const uint32_t mh = pm ? hp : h;
-  const uint32_t sidx = Sg[16 * ((mh >> 1) % 10) + 2 * (gm + 4 * (mh & 1u)) + i];
-  // state lanes: the tile's half-round (0-15) or the previous one (32-47)
-  const bool ps = grp >= 4;
-  const uint32_t sh = ps ? hp : h;
-  const uint32_t word = 4 * role + ((gl + role * (sh & 1u)) & 3u);
-  const uint64_t* p = fw;
-  if (grp < 2 || (ps && grp < 6 && h != 0)) p = rec + 16ull * (c.st + sh) + word;
-  else if (grp == 2 || (pm && h != 0)) p = x->m + sidx;
-  else if (ps && grp < 6) p = role == 0 ? x->h + gl : role == 1 ? x->h + gl + 4 : (role == 3 && gl < 2) ? x->t + gl : fw;
-  return *p;
-}
-
 // The per-lane constants of the tile loop (resolved once).
 struct Lane {
   // assignment
   uint32_t selL[4], selH[4], slot[4], slA, slB;
   uint32_t madd, mzm, mhz, mhw, mswap, rsh, fx0;
   uint32_t aWD, aAB, aMX, aGS, aXY, aM, aPG, aLTs, aLTd, ltsh;
+  uint32_t oW;  // lanes 0-15: byte offsets in an OUT slot of the state word (hr 0 | even | odd)
   // checks
   uint32_t aQ;                        // the lane's quad (lane_quad), column a_0
   uint32_t gb, ge, gf, gsel, gm24, gm63, gnl, grs, gsF, gsH;  // XOR-family limb item
@@ -926,16 +912,23 @@ __device__ __forceinline__ Lane make_lane(uint32_t lane, uint32_t Sb) {
   L.aGS = Sb + 4 * T_GS + 128 * gg;
   L.aXY = L.aGS + 8 * st;
   L.aM = Sb + 4 * T_GS + 128 * gg + 8 * mi;
-  if (lane == HR_Q + 3) L.aGS = Sb + 4 * T_GP;  // publishes the previous half-round's G 3 chain
-  if (lane >= TAIL0 && lane < TAIL0 + 7) {      // ... which the tail lanes read
-    L.aXY = Sb + 4 * T_GP + 8 * st;
-    L.aM = Sb + 4 * T_GP + 8 * mi;
+  if (lane >= TAIL0 && lane < TAIL0 + 7) {  // the previous tile's G 3 chain record (GP slot 0)
+    L.aXY = Sb + 4 * H_GP + 8 * st;
+    L.aM = Sb + 4 * H_GP + 8 * mi;
+  }
+  {  // state word (a, b, c, d)[role] of G gl, in the previous tile's G order q = (hr - 1) & 1:
+     // natural word w = 4 role + j is output (G (j - role q) & 3, role) of the previous half-round
+    const uint32_t gl = (lane >> 2) & 3u, role = lane & 3u;
+    const uint32_t i0 = 4 * gl + role;                           // hr 0: the initial vector, q = 0
+    const uint32_t i1 = 4 * ((gl - role) & 3u) + role;           // hr even: w = 4 role + gl, q = 1
+    const uint32_t i2 = 4 * ((gl + role) & 3u) + role;           // hr odd: w = 4 role + (gl + role), q = 0
+    L.oW = 8 * i0 | (8 * i1) << 8 | (8 * i2) << 16;
   }
   L.aPG = Sb + 4 * T_PG + 32 * (lane - HR_Q);  // producer lanes only
   {  // limb table entry lane = 4 w + k, read from the producer outputs in G order (parity 0 / 1)
     const uint32_t w = lane >> 2, k = lane & 3u, role = w >> 2, pos = w & 3u;
     const uint32_t i0 = 4 * pos + role, i1 = 4 * ((pos - role) & 3u) + role;
-    const uint32_t a0 = Sb + 4 * T_PG + 8 * i0 + 4 * (k >> 1), a1 = Sb + 4 * T_PG + 8 * i1 + 4 * (k >> 1);
+    const uint32_t a0 = Sb + 4 * H_OUT + 8 * i0 + 4 * (k >> 1), a1 = Sb + 4 * H_OUT + 8 * i1 + 4 * (k >> 1);
     L.aLTs = a0 | (a1 << 16);
     L.ltsh = 16 * (k & 1u);
     L.aLTd = Sb + 4 * H_LT + 4 * lane;
@@ -1101,37 +1094,79 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
   const uint32_t Sb = lds_byte(S);
   const Lane K = make_lane(lane, Sb);
   const bool qlane = lane < HR_Q, p0 = qlane && (lane % G_QUADS) == 0;
-  const bool plane = lane >= HR_Q && lane < HR_Q + 4;
   const bool tlane = lane >= TAIL0 && lane < TAIL0 + 7;
-  const uint32_t pg = lane - HR_Q;
 
   if (*status == 0) {  // the record kernel accepted the layout
-    const uint64_t used_rows = off[n];
-    const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
+    // Instances dealt to waves (XCD-aware, first_tile), each walked half-round by half-round:
+    // the state a tile starts from is the G outputs of the wave's previous tile (OUT), so no
+    // tile reads a recorded state. The next instance's input record is loaded one instance
+    // ahead, a word per lane (27 lanes), every tile (the same address: L2 after the first) and
+    // settled inside the tile like every other load.
     const uint64_t W = (uint64_t)gridDim.x * WAVES;
-    uint64_t t = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
-    auto raw_desc = [&](uint64_t tt) -> uint4 {
-      const uint64_t ti = tt < n_hr ? tt : 0;
-      const uint4 v = desc[ti].v;
-      return tt < n_hr ? v : make_uint4(0, 0, 0, 0);
+    uint64_t* const INW = reinterpret_cast<uint64_t*>(S + H_IN);
+    const uint32_t aIN = Sb + 4 * H_IN;
+    auto rec_word = [&](uint32_t i) -> uint64_t {  // lane's word of instance i's input record
+      const uint64_t* x = reinterpret_cast<const uint64_t*>(in + (i < n ? i : 0));
+      return x[lane < 27 ? lane : 26];
     };
-    HCtx c = hctx(raw_desc(t));
-    uint64_t P = 0;
-    if (t < n_hr) P = load_word(c, lane, in, rec, Sg);
-    // settled before the loop: otherwise the compiler cannot prove at the loop header that P is
+    // the instance after `i` in this wave's sequence that has half-rounds (scalar loads)
+    auto next_inst = [&](uint32_t i) -> uint32_t {
+      uint64_t j = (uint64_t)i + W;
+      while (j < n && in[j].rounds == 0) j += W;
+      return j < n ? (uint32_t)j : n;
+    };
+    uint32_t inst;
+    {
+      const uint64_t f = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
+      inst = f < n ? (in[f].rounds ? (uint32_t)f : next_inst((uint32_t)f)) : n;
+    }
+    uint64_t Pi = rec_word(inst);  // the current instance's record word
+    // settled before the loop: otherwise the compiler cannot prove at the loop header that Pi is
     // never pending and waits for vmcnt(0) -- every store in flight -- at its first use
-    asm volatile("" ::"v"(P));
-    uint4 dn = raw_desc(t + W);
-    for (; t < n_hr; t += W) {
+    asm volatile("" ::"v"(Pi));
+    HCtx c;
+    uint32_t ninst = 0;
+    c.hr = 0;
+    for (; inst < n;) {
       tick(-1);
-      const HCtx cn = hctx(dn);
-      const uint64_t Pn = load_word(cn, lane, in, rec, Sg);  // past the end: a harmless load
-      // ---- 1. the tile's words into the wave's LDS
-      st64(K.aWD, P);
+      if (c.hr == 0) {  // an instance's first tile: its context, its record into IN, the initial
+                        // work vector (h, IV, IV ^ (t0, t1, fmask)) into OUT slot 0 in column-G order
+        const uint64_t o = off[inst];
+        c.inst = inst;
+        c.rounds = in[inst].rounds;
+        c.st = (uint32_t)((o - 20ull * inst) / 208);
+        c.off = o;
+        ninst = next_inst(inst);
+        if (lane < 27) st64(aIN + 8 * lane, Pi);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 16) {
+          const uint32_t g = lane >> 2, k = lane & 3u;
+          const uint64_t fw = INW[26];
+          const uint64_t tw = g < 2 ? INW[24 + g] : (g == 2 ? ((fw >> 32) ? ~0ull : 0ull) : 0ull);
+          const uint64_t v = k == 0 ? INW[g] : k == 1 ? INW[g + 4] : k == 2 ? IV[g] : (IV[g + 4] ^ tw);
+          st64(Sb + 4 * H_OUT + 8 * lane, v);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+      }
+      c.row0 = c.off + INIT_ROWS + 208ull * c.hr;
+      const uint32_t ob = 128u * (c.hr & 1u), nb = 128u - ob;  // this tile's OUT / GP slot, the next's
+      const uint64_t Pn = rec_word(ninst);  // the next instance's record word (past the end: harmless)
+      // ---- 1. the tile's words into the wave's LDS: the state words (lanes 0-15) from OUT, the
+      // message words (16-23) from IN
+      {
+        const uint32_t h = c.hr;
+        const uint32_t sh = h == 0 ? 0u : (h & 1u) ? 16u : 8u;
+        const uint32_t gm = (lane >> 1) & 3u, i = lane & 1u;
+        const uint32_t sidx = Sg[16 * ((h >> 1) % 10) + 2 * (gm + 4 * (h & 1u)) + i];
+        const uint32_t src = lane < 16 ? Sb + 4 * H_OUT + ob + ((K.oW >> sh) & 255u) : aIN + 8 * (8 + sidx);
+        if (lane < 24) st64(K.aWD, ld64(src));
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
       tick(0);
-      // ---- 2. chains: quad lanes their G of half-round hr, producer lanes G pg of hr - 1
+      // ---- 2. chains: quad lanes their G of half-round hr
       const uint4 ab = ld128(K.aAB), cd = ld128(K.aAB + 16), mm = ld128(K.aMX);
       const uint64_t a = mk64(ab.x, ab.y), b = mk64(ab.z, ab.w), cc = mk64(cd.x, cd.y), d = mk64(cd.z, cd.w);
       const uint64_t mx = mk64(mm.x, mm.y), my = mk64(mm.z, mm.w);
@@ -1142,41 +1177,46 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       const uint64_t a2 = a1 + b1 + my;
       const uint64_t d2 = rotr64(d1 ^ a2, 16);
       const uint64_t c2 = c1 + d2;
-      if (p0 || lane == HR_Q + 3) {
-        const uint32_t g = K.aGS;  // this G's chain record (lane HR_Q + 3: G 3 of hr - 1, T_GP)
-        st128(g, make_uint4(lo32(a), hi32(a), lo32(d), hi32(d)));
-        st128(g + 16, make_uint4(lo32(cc), hi32(cc), lo32(b), hi32(b)));
-        st128(g + 32, make_uint4(lo32(a1), hi32(a1), lo32(d1), hi32(d1)));
-        st128(g + 48, make_uint4(lo32(c1), hi32(c1), lo32(b1), hi32(b1)));
-        st128(g + 64, make_uint4(lo32(a2), hi32(a2), lo32(d2), hi32(d2)));
-        st128(g + 80, make_uint4(lo32(c2), hi32(c2), lo32(mx), hi32(mx)));
-        st128(g + 96, make_uint4(lo32(my), hi32(my), 0u, 0u));
-      }
-      if (plane) {
-        uint64_t o0, o1, o2, o3;
-        if (c.hr == 0) {  // the initial work vector: h, IV, v12..v14 = IV ^ (t0, t1, fmask)
-          o0 = a;
-          o1 = b;
-          o2 = IV[pg];
-          const uint64_t tw = pg < 2 ? d : (pg == 2 ? ((d >> 32) ? ~0ull : 0ull) : 0ull);
-          o3 = IV[pg + 4] ^ tw;
-        } else {
-          o0 = a2;
-          o1 = rotr64(b1 ^ c2, 63);
-          o2 = c2;
-          o3 = d2;
+      if (p0) {
+        const uint32_t g = K.aGS;  // this G's chain record
+        const uint4 r0 = make_uint4(lo32(a), hi32(a), lo32(d), hi32(d));
+        const uint4 r1 = make_uint4(lo32(cc), hi32(cc), lo32(b), hi32(b));
+        const uint4 r2 = make_uint4(lo32(a1), hi32(a1), lo32(d1), hi32(d1));
+        const uint4 r3 = make_uint4(lo32(c1), hi32(c1), lo32(b1), hi32(b1));
+        const uint4 r4 = make_uint4(lo32(a2), hi32(a2), lo32(d2), hi32(d2));
+        const uint4 r5 = make_uint4(lo32(c2), hi32(c2), lo32(mx), hi32(mx));
+        const uint4 r6 = make_uint4(lo32(my), hi32(my), 0u, 0u);
+        st128(g, r0);
+        st128(g + 16, r1);
+        st128(g + 32, r2);
+        st128(g + 48, r3);
+        st128(g + 64, r4);
+        st128(g + 80, r5);
+        st128(g + 96, r6);
+        // the next tile's state / copy sources: this G's outputs into the other OUT slot
+        const uint64_t o1 = rotr64(b1 ^ c2, 63);
+        const uint32_t go = Sb + 4 * H_OUT + nb + 32 * (lane / G_QUADS);
+        st128(go, make_uint4(lo32(a2), hi32(a2), lo32(o1), hi32(o1)));
+        st128(go + 16, make_uint4(lo32(c2), hi32(c2), lo32(d2), hi32(d2)));
+        if (lane == 3 * G_QUADS) {  // G 3's chain record for the next tile's tail lanes
+          const uint32_t gp = Sb + 4 * H_GP + nb;
+          st128(gp, r0);
+          st128(gp + 16, r1);
+          st128(gp + 32, r2);
+          st128(gp + 48, r3);
+          st128(gp + 64, r4);
+          st128(gp + 80, r5);
+          st128(gp + 96, r6);
         }
-        st128(K.aPG, make_uint4(lo32(o0), hi32(o0), lo32(o1), hi32(o1)));
-        st128(K.aPG + 16, make_uint4(lo32(o2), hi32(o2), lo32(o3), hi32(o3)));
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
-      dn = raw_desc(t + 2 * W);  // scalar load; retires during the assignment
       tick(1);
       // ---- 3. operands of the lane's quad, the lane's limb-table entry
-      const uint64_t X = ld64(K.aXY), Y = ld64(K.aXY + 24), M = ld64(K.aM);
-      const uint32_t par = c.hr ? ((c.hr & 1u) ^ 1u) : 0u;  // G order of the producer outputs
-      const uint32_t pv = ld32(par ? K.aLTs >> 16 : K.aLTs & 0xffffu);
+      const uint32_t gofs = tlane ? ob : 0u;  // tail lanes: the previous tile's G 3 (GP slot)
+      const uint64_t X = ld64(K.aXY + gofs), Y = ld64(K.aXY + gofs + 24), M = ld64(K.aM + gofs);
+      const uint32_t par = c.hr ? ((c.hr & 1u) ^ 1u) : 0u;  // G order of the previous tile's outputs
+      const uint32_t pv = ld32((par ? K.aLTs >> 16 : K.aLTs & 0xffffu) + ob);
       const uint32_t lv = (pv >> K.ltsh) & 0xffffu;
       st32(K.aLTd, lv);
       st32(K.aLTd + 256, spread16(lv));
@@ -1343,8 +1383,13 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       asm volatile("" ::: "memory");
       __builtin_amdgcn_wave_barrier();
       tick(6);
-      c = cn;
-      P = Pn;
+      if (c.hr + 1 < 2 * c.rounds) {
+        c.hr++;
+      } else {
+        c.hr = 0;
+        inst = ninst;
+        Pi = Pn;
+      }
     }
   }
   if ((MODE & FZ_CLOCK) && lane == 0) {
@@ -2081,22 +2126,6 @@ eval_edge_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ 
   if (__builtin_amdgcn_ballot_w64(bad) && lane == 0) *dirty = 1u;
 }
 
-// Per-tile descriptors {instance, tile index inside it, rounds, first state index}: thread per
-// instance, 2 rounds + 2 tiles each (init, half-rounds, final).
-__global__ void tile_desc_kernel(const uint64_t* __restrict__ off, const b2f_input* __restrict__ in,
-                                 uint32_t n, TileDesc* __restrict__ desc, const int* __restrict__ status) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || *status) return;
-  const uint32_t rounds = in[i].rounds;
-  const uint64_t st = 2 * ((off[i] - (uint64_t)FIXED_ROWS * i) / ROUND_ROWS) + i;
-  // the half-round tiles first (instance i's at 2 sum(rounds before i) = st - i), then the
-  // init / final pairs (at n_hr + 2 i)
-  const uint64_t n_hr = (off[n] - (uint64_t)FIXED_ROWS * n) / 208;
-  for (uint32_t j = 1; j <= 2 * rounds; j++) desc[st - i + j - 1].v = make_uint4(i, j, rounds, (uint32_t)st);
-  desc[n_hr + 2ull * i].v = make_uint4(i, 0, rounds, (uint32_t)st);
-  desc[n_hr + 2ull * i + 1].v = make_uint4(i, 2 * rounds + 1, rounds, (uint32_t)st);
-}
-
 // Gates of selector rows the fused kernel deferred (their gate reads rows past the tile that
 // assigned them), on the written trace: all selector bits of each listed row.
 __global__ void deferred_gates_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fixed,
@@ -2203,7 +2232,6 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(redo, 0, 4, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(tile_desc_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d_off, d_in, n, desc, d_status);
   Inject inj;
   inj.row = inj_row;
   inj.col = inj_col;

@@ -105,7 +105,8 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
                                                       uint64_t* __restrict__ h_out,
                                                       int* __restrict__ status,
                                                       int* __restrict__ sticky,
-                                                      b2f_eval_report* __restrict__ rep) {
+                                                      b2f_eval_report* __restrict__ rep,
+                                                      bool lite) {
   const uint32_t gt = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t i = gt >> 2, c = gt & 3u;  // the quad's four lanes share instance i
   if (i >= n) return;
@@ -148,7 +149,16 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
   __shared__ __attribute__((aligned(16))) uint64_t Tq[BLOCK / 4][16];
   uint64_t* tq = Tq[threadIdx.x >> 2];
   uint64_t* s = rec + st * 16 + 4 * c;
+  // lite (the fused path, whose half-round launch carries the state from tile to tile): only the
+  // last two states -- the edge launch's final state and its producers' last half-round -- of the
+  // 2 rounds + 1
+  uint32_t k = 0;
+  const uint32_t keep = lite ? (rounds ? 2 * rounds - 1 : 0) : 0;
   auto dump = [&](void) {
+    if (k++ < keep) {
+      s += 16;
+      return;
+    }
     tq[c] = va;
     tq[4 + c] = vb;
     tq[8 + c] = vc;
@@ -1110,7 +1120,7 @@ namespace {
 // b2f_fill_eval_dev.
 int fill_prologue(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const uint64_t* d_offsets,
                   uint64_t total_rows, uint32_t* d_advice, uint32_t* d_fixed, uint64_t* d_h_out,
-                  b2f_eval_report* d_report, hipStream_t s) {
+                  b2f_eval_report* d_report, hipStream_t s, bool lite = false) {
   if (!d_in || !d_offsets || !d_advice || !d_fixed || n == 0)
     return set_err(ctx, B2F_ERR_ARG, "fill: null buffer or empty batch");
   if (n > 0xffffffffull) return set_err(ctx, B2F_ERR_ARG, "fill: more than 2^32 instances");
@@ -1143,7 +1153,7 @@ int fill_prologue(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const uint64_t*
   int tk = timed_begin(ctx, B2F_KERNEL_RECORD, s);
   hipLaunchKernelGGL(record_kernel, dim3((uint32_t)((4ull * nn + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, d_in, nn,
                      d_offsets, total_rows, ctx->rec_cap, ctx->d_rec, d_h_out, ctx->d_status,
-                     ctx->d_status + 2, d_report);
+                     ctx->d_status + 2, d_report, lite);
   HIPCHK(ctx, hipGetLastError());
   timed_end(ctx, tk, s);
   return B2F_OK;
@@ -1204,7 +1214,9 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
   if (!ctx) return B2F_ERR_ARG;
   if (!d_report) return set_err(ctx, B2F_ERR_ARG, "fill_eval: null report");
   hipStream_t s = (hipStream_t)stream;
-  int rc = fill_prologue(ctx, d_in, n, d_offsets, total_rows, d_advice, d_fixed, d_h_out, d_report, s);
+  // lite record: the half-round launch carries the state from tile to tile; only the edge launch
+  // reads recorded states (the last two of each instance)
+  int rc = fill_prologue(ctx, d_in, n, d_offsets, total_rows, d_advice, d_fixed, d_h_out, d_report, s, true);
   if (rc) return rc;
   const uint64_t tiles = fused_instance_tiles(total_rows, n);
   rc = ensure_fused_scratch(ctx, fused_scratch_bytes(tiles), s);
