@@ -1,33 +1,30 @@
 // b2f_fused.hip -- the fused witness fill + constraint evaluation (b2f_fill_eval_dev).
 //
-// One persistent kernel assigns every cell of a batch (the fill kernel's work) and checks the
-// trace it assigns (the eval kernel's work) before the cells leave the CU: each cell is written
-// to HBM once and never read back. The result is the same trace, h' and verdict as
-// b2f_fill_dev followed by b2f_eval_dev -- MockProver::run (synthesize, blake2f.rs:301) then
-// verify (:302) over the same assignment -- at the HBM cost of the fill alone.
+// The launches assign every cell of a batch (the fill kernel's work) and check the trace they
+// assign (the eval kernel's work) before the cells leave the CU: each cell is written to HBM
+// once and never read back. The result is the same trace, h' and verdict as b2f_fill_dev
+// followed by b2f_eval_dev -- MockProver::run (synthesize, blake2f.rs:301) then verify (:302)
+// over the same assignment -- at the HBM cost of the fill alone.
 //
-// Work layout: the WAVE is the unit. The trace is cut at block boundaries into tiles: per
-// instance the init region (41 quads), one tile per half-round (4 G's = 52 quads; every gate
-// block lies inside its G) and the final region (16 quads); then 64-quad tiles of the zero rows
-// past the last instance. Tile j of instance i is global tile T_i + j with
-// T_i = 2 sum(rounds before i) + 2 i (tile_desc_kernel writes {i, j, rounds, state index}).
-// Tiles are dealt round-robin to the waves of a persistent grid (wave w takes w, w + W, ...),
-// so at any moment the chip writes one narrow band of every column -- the fill kernel's store
-// pattern (tools/store_probe.hip: 8.8 ms for the 60 GB 2^18 x 12-round trace, the same as
-// 1024-row workgroup tiles; per-wave instance ownership drops to 12.1 ms).
-//
-// A wave assigns its tile (lane = quad), stages the cells into its own LDS region, stores them
-// (16-byte non-temporal column stores) and then checks the tile out of LDS: lookups per row,
-// every canonical gate block by kind (one evaluator per lane group: adds, XORs, XOR24 and
-// XOR63 limbs), every copy constraint whose operand cell lies in the tile, the fixed column
-// against the keygen structure. No workgroup barrier: waves never share data. Copy sources in
-// earlier tiles are the previous half-round's G outputs and the init region's words; the wave
-// recomputes them from the producer side -- the previous half-round's four G chains from the
-// record kernel's state at ITS start (four otherwise idle lanes), the init words from the input
-// record -- so every copy compares the staged operand cell with the value its producer
-// assigned (the test-only injection is applied to recomputed cells too). A selector row whose
-// gate would read past the tile (only a corrupted fixed column has one) goes to a short list
-// that a follow-up kernel evaluates on the written trace (deferred_gates_kernel).
+// Work layout: the WAVE is the unit; a tile is a block-aligned piece of one instance, assigned
+// lane = quad, staged in the wave's own LDS region, stored (16-byte non-temporal column stores,
+// each 128-byte line by one store instruction) and checked out of LDS: lookups per row, every
+// canonical gate block, every copy constraint whose operand cell lies in the tile, the fixed
+// column against the keygen structure. No workgroup barrier: waves never share data.
+//   fused_hr_kernel: the half-round tiles (4 G's = 52 quads, 96 % of the rows). A wave takes
+//     whole instances and walks their half-rounds in order, carrying the state in LDS: the G
+//     outputs of its previous tile are this tile's state words and the copy sources of its
+//     state-word cells, so no tile reads a recorded state (the record kernel writes only the
+//     two states per instance the edge launch reads).
+//   fused_edge_kernel: per instance the init region (41 quads) and the final region (16
+//     quads) in one wave tile, then 64-quad tiles of the zero rows past the last instance; the
+//     final region's copy sources in the last half-round are recomputed from the recorded state
+//     at its start (four otherwise idle lanes).
+// Checks are 32-bit identities that assume the ranges the other checks of the same pass
+// establish, so a clean pass proves a clean tile; a flagged tile is re-checked exactly (the
+// eval kernel's counters, first failing row). A selector row whose gate would read past the
+// tile (only a corrupted fixed column has one) goes to a short list that a follow-up kernel
+// evaluates on the written trace (deferred_gates_kernel).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -640,14 +637,15 @@ __device__ __forceinline__ uint64_t first_tile(uint32_t b, uint32_t wv, uint32_t
 // changes from tile to tile, so everything that depends on p alone -- which bytes of which
 // operand word land in every cell, which cells every check reads -- is resolved once per lane
 // before the tile loop (v_perm_b32 byte selectors and LDS byte addresses in registers). Per tile:
-//   1. each lane loads ONE 8-byte word (the tile's 16 state words and 8 message words in G
-//      order, the previous half-round's 16 state words and 8 message words for the producers)
-//      and writes it to the wave's LDS;
+//   1. lanes 0-15 copy the tile's 16 state words in G order out of OUT (the wave's previous tile's
+//      G outputs, or the initial work vector at an instance's first tile), lanes 16-23 its 8
+//      message words out of the instance record in LDS;
 //   2. every lane runs the G chain of its G; one lane per G publishes the chain
 //      (a d c b a1 d1 c1 b1 a2 d2 c2 mx my 0), so a quad's operands X = s[step], Y = s[step+3]
-//      and M are three LDS reads instead of select chains; the four producer lanes publish the
-//      previous half-round's G outputs (the state words' producer values), and every lane
-//      builds one (word, limb) entry of the limb table the copy checks read (dense and spread);
+//      and M are three LDS reads instead of select chains, and writes its G's outputs into the
+//      other OUT slot (the next tile's state); G 3's chain also goes to the other GP slot (the
+//      next tile's tail lanes, which recompute this tile's last seven quads); every lane builds
+//      one (word, limb) entry of the limb table the copy checks read, from this tile's OUT slot;
 //   3. cells: a_1 rows and every operand slot by v_perm byte selection, spreads and tags, staged;
 //   4. stores: 11 raw buffer stores per tile, each covering whole 128-byte lines (line ownership,
 //      see the store loop);
