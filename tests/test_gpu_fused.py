@@ -50,8 +50,12 @@ def _fused(engine, x, total_rows=None, inject=None):
 
 @pytest.mark.parametrize("rounds_choices,n,seed", [((12,), 23, 31), ((0, 1, 4, 12, 13), 71, 32),
                                                    ((1,), 200, 33), ((0,), 9, 35),
-                                                   ((2, 3), 1000, 36)])
+                                                   ((2, 3), 1000, 36), ((12,), 1, 37), ((1,), 1, 38),
+                                                   ((25, 0), 50, 39), ((100,), 2, 40)])
 def test_fused_equals_oracle(engine, orc, rounds_choices, n, seed):
+    """Single instances and runs of zero-round instances included: the half-round launch walks
+    whole instances (a wave skips instances without half-rounds and carries the state from tile
+    to tile)."""
     x = random_inputs(n, rounds_choices, seed)
     batch = _fused(engine, x)
     adv, fixed = batch.host_trace()
