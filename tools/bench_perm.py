@@ -16,13 +16,14 @@ def main():
     ap.add_argument("--chunk", type=int, default=3)
     ap.add_argument("--forms", default="1,3")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--lib", default=None, help="a variant library (A/B), default the product")
     args = ap.parse_args()
     import torch
 
     import b2f
     from b2f import synth
 
-    eng = b2f.Engine(0)
+    eng = b2f.Engine(0) if not args.lib else b2f.Engine(0, lib_path=args.lib)
     n_rows = 1 << args.k
     usable = n_rows - 7
     n_inst = usable // 5220
