@@ -44,13 +44,16 @@ FR_ONE_MONT = [int.from_bytes((0x0e0a77c19a07df2f666ea36f7879462e36fc76959f60cd2
 ADVICE_COLS = 10
 ROW_BYTES = 4 * (ADVICE_COLS + 1)  # 10 advice u32 + 1 fixed u32
 INPUT_BYTES = 216
+EXIT_EXTRAS_TIMEOUT = 3  # ExtrasWatchdog fired: headline printed, an extra leg hung
 
 
 class ExtrasWatchdog:
     """After the headline of an N > 1 run: if the legs that follow (all collective) are not done
     within `timeout` seconds -- one rank failed where the others wait in a collective -- rank 0
     prints the headline's JSON line with "extras" marked timed out and every rank ends with
-    exit code 0 (each rank runs its own timer, started at the same barrier). timeout 0: off."""
+    exit code EXIT_EXTRAS_TIMEOUT: the headline is complete, but a hung collective is a real
+    failure and a launcher or CI must see it (each rank runs its own timer, started at the same
+    barrier). timeout 0: off."""
 
     def __init__(self, timeout, rank, headline, exit_fn=None, out=None):
         import threading
@@ -79,7 +82,7 @@ class ExtrasWatchdog:
                                            "complete" % self._timeout}
                 self._out.write(json.dumps(line) + "\n")
                 self._out.flush()
-        self._exit(0)
+        self._exit(EXIT_EXTRAS_TIMEOUT)
 
     def finish(self):
         """True if the caller prints the line (the watchdog did not fire)."""
@@ -233,8 +236,8 @@ def main():
                          "(0 = no limit)")
     ap.add_argument("--aux-steps", type=int, default=5,
                     help="steps of the other path timed after the headline loop (0 = skip)")
-    ap.add_argument("--floor-reps", type=int, default=3,
-                    help="launches of each diagnostic floor variant (0 = skip)")
+    ap.add_argument("--floor-reps", type=int, default=10,
+                    help="interleaved reps of the floor variants and product kernels (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
     args = ap.parse_args()
@@ -416,8 +419,24 @@ def main():
     log("rank %d: %d instances, %d rows, trace %.1f GB"
         % (rank, n_local, rows, batch.total_rows * ROW_BYTES / 1e9))
 
-    elapsed, ktimes, rep = timed_loop(batch, info, args.path, args.steps, args.warmup, global_n)
     total_n = global_n if global_n else world * n_local
+    # the headline's config, captured once from the batch it times (later legs have their own
+    # sizes and must not leak into it)
+    if global_n:
+        workload = ("%d x %s-round BLAKE2f compressions sharded over %d GPUs (row-balanced): "
+                    "Table16 witness fill + constraint eval (LAYOUT v1)"
+                    % (global_n, "{1,4,12}-mixed" if mix else args.rounds, world))
+    else:
+        workload = ("%d x %s-round BLAKE2f compressions per GPU: Table16 witness fill + "
+                    "constraint eval (LAYOUT v1)"
+                    % (n_local, "{1,4,12}-mixed" if mix else args.rounds))
+    head_config = {"workload": workload, "batch_per_gpu": n_local, "global_batch": total_n,
+                   "rounds": "mix{1,4,12}" if mix else args.rounds,
+                   "rows_per_gpu": rows, "trace_bytes_per_gpu": rows * ROW_BYTES,
+                   "path": args.path,
+                   "parallelism": "dp%d (instance shards)" % world}
+
+    elapsed, ktimes, rep = timed_loop(batch, info, args.path, args.steps, args.warmup, global_n)
     value = total_n * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
 
@@ -457,14 +476,6 @@ def main():
 
     def headline():
         """The contract's fields of the JSON line, complete once the headline loop is done."""
-        if global_n:
-            workload = ("%d x %s-round BLAKE2f compressions sharded over %d GPUs (row-balanced): "
-                        "Table16 witness fill + constraint eval (LAYOUT v1)"
-                        % (global_n, "{1,4,12}-mixed" if mix else args.rounds, world))
-        else:
-            workload = ("%d x %s-round BLAKE2f compressions per GPU: Table16 witness fill + "
-                        "constraint eval (LAYOUT v1)"
-                        % (n, "{1,4,12}-mixed" if mix else args.rounds))
         return {"metric": "BLAKE2f compressions/sec (witness+constraint eval), 2^18 batch, "
                           "1/2/4/8 GPU",
                 "value": round(value, 1), "unit": "compressions/s", "n_gpus": world,
@@ -472,11 +483,7 @@ def main():
                 "higher_is_better": True, "scaling": "strong" if global_n else "weak",
                 "vs_baseline": None, "dtype": "u32",
                 "data": "synthetic (seeded splitmix64 h/m/t/f)",
-                "config": {"workload": workload, "batch_per_gpu": n, "global_batch": total_n,
-                           "rounds": "mix{1,4,12}" if mix else args.rounds,
-                           "rows_per_gpu": rows, "trace_bytes_per_gpu": rows * ROW_BYTES,
-                           "path": args.path,
-                           "parallelism": "dp%d (instance shards)" % world},
+                "config": dict(head_config),
                 "roofline": roof, "cpu_baseline": None, "kernels": kern}
 
     # N > 1: the legs after the headline use collectives; one that hangs (a rank failing where
@@ -511,34 +518,52 @@ def main():
     # same-box floors, from the diagnostics library (libb2f_diag.so; the product library has
     # no diagnostic variants): the fill with its stores but no cell computation
     # (B2F_DIAG_FILL=2) and the eval with its loads, staging and lookups but no gates or copies
-    # (B2F_DIAG_EVAL=1). Boxes differ by up to ~25 % on the store-bound fill, so the
-    # achieved/floor ratio is the comparable number.
+    # (B2F_DIAG_EVAL=1). Boxes differ by up to ~25 % in store rate, so the achieved/floor ratio
+    # is the comparable number. Each rep launches floor and product kernels back to back
+    # (fill floor, fused pass, split fill, eval floor, split eval), so drifts in the box's
+    # store rate hit both sides alike; min and median over the reps are reported.
     floors = None
     if world == 1 and args.floor_reps > 0:
         try:
             deng = b2f.Engine(local, diag=True)
-            floors = {}
-            for var, val, kname in (("B2F_DIAG_FILL", "2", "fill"), ("B2F_DIAG_EVAL", "1", "eval")):
-                os.environ[var] = val
+            samples = {"fill_floor": [], "fill_eval": [], "fill": [], "eval_floor": [],
+                       "eval": []}
+
+            def one(e, fn, kname, var=None, val=None):
+                if var:
+                    os.environ[var] = val
                 try:
-                    deng.set_timing(True)
-                    for _ in range(args.floor_reps):
-                        if kname == "fill":
-                            batch.fill(deng, stream)
-                        else:
-                            batch.evaluate(deng, stream)
-                    tot, cnt = deng.kernel_times()[kname]
+                    e.set_timing(True)
+                    fn(e, stream)
+                    tot, cnt = e.kernel_times()[kname]
                 finally:
-                    os.environ.pop(var, None)
-                floors[kname + "_floor_ms"] = round(tot / max(cnt, 1), 4)
-                floors[kname + "_over_floor"] = round(kern[kname]["avg_ms"] / (tot / max(cnt, 1)), 4) \
-                    if kname in kern else None
-                if kname == "fill" and "fill_eval" in kern:  # the fused pass writes the same trace
-                    floors["fill_eval_over_fill_floor"] = round(kern["fill_eval"]["avg_ms"] / (tot / max(cnt, 1)), 4)
+                    if var:
+                        os.environ.pop(var, None)
+                return tot / max(cnt, 1)
+
+            for _ in range(args.floor_reps):
+                samples["fill_floor"].append(one(deng, batch.fill, "fill", "B2F_DIAG_FILL", "2"))
+                samples["fill_eval"].append(one(eng, batch.fill_evaluate, "fill_eval"))
+                samples["fill"].append(one(eng, batch.fill, "fill"))
+                samples["eval_floor"].append(one(deng, batch.evaluate, "eval", "B2F_DIAG_EVAL", "1"))
+                samples["eval"].append(one(eng, batch.evaluate, "eval"))
             deng.sync(stream)
             deng.close()
             batch.fill(eng, stream)  # leave a real trace behind
             eng.sync(stream)
+            med = {k: float(np.median(v)) for k, v in samples.items()}
+            mn = {k: float(np.min(v)) for k, v in samples.items()}
+            floors = {"reps": args.floor_reps, "interleaved": True,
+                      "median_ms": {k: round(v, 4) for k, v in med.items()},
+                      "min_ms": {k: round(v, 4) for k, v in mn.items()},
+                      "max_ms": {k: round(float(np.max(v)), 4) for k, v in samples.items()},
+                      "fill_floor_ms": round(med["fill_floor"], 4),
+                      "eval_floor_ms": round(med["eval_floor"], 4),
+                      "fill_over_floor": round(med["fill"] / med["fill_floor"], 4),
+                      "eval_over_floor": round(med["eval"] / med["eval_floor"], 4),
+                      "fill_eval_over_fill_floor": round(med["fill_eval"] / med["fill_floor"], 4),
+                      "fill_eval_over_fill_floor_min": round(mn["fill_eval"] / mn["fill_floor"], 4),
+                      "note": "ratios of medians (and of minima) over interleaved reps"}
         except (OSError, b2f.B2FError) as e:
             floors = {"error": repr(e)}
 
@@ -633,7 +658,12 @@ def main():
         try:
             k = args.perm_k
             usable = (1 << k) - 7
-            n_inst = min(batch.n, usable // 5220)
+            # the circuit holds the batch's first instances whose rows fit the usable rows
+            # (selected by cumulative rows, so any rounds mix works)
+            n_inst = int(np.searchsorted(batch.offsets_host[1:], usable, side="right"))
+            n_inst = min(n_inst, batch.n)
+            if n_inst == 0:
+                raise ValueError("no instance fits 2^%d - 7 usable rows" % k)
             beta, gamma = 0x1234567 << 180, 0x89ABCDEF << 170
             for _ in range(2):  # the first call builds the mapping pattern and its scratch
                 eng.set_timing(True)
@@ -645,24 +675,30 @@ def main():
             avg = tot / max(cnt, 1)
             closes = bool(z[-1, usable].eq(torch.tensor(FR_ONE_MONT, dtype=torch.int64,
                                                         device=z.device)).all().item())
-            rows = 1 << k
+            domain = 1 << k
             # products this call executes: sigma 8 per row of the 2^k domain; per usable row 8
             # num coset values, 10 accumulations (sets of 3, 3, 2 columns) and 4 per set of
             # grand product, plus one den coset value per cell on a copy cycle (the others map
-            # to themselves and reuse the num value)
-            mp = b2f.permutation_mapping(12)
-            ident = ((mp >> 29) == np.arange(8, dtype=np.uint32)[:, None]) & \
-                ((mp & ((1 << 29) - 1)) == np.arange(mp.shape[1], dtype=np.uint32)[None, :])
-            products = rows * 8 + usable * 30 + int((~ident).sum()) * n_inst
+            # to themselves and reuse the num value), summed over the instances' rounds
+            on_cycle = 0
+            from b2f import layout as blayout
+            r_of = (np.diff(batch.offsets_host[:n_inst + 1].astype(np.int64))
+                    - blayout.INIT_ROWS - blayout.FINAL_ROWS) // blayout.ROUND_ROWS
+            for r, cnt_r in zip(*np.unique(r_of, return_counts=True)):
+                mp = b2f.permutation_mapping(int(r))
+                ident = ((mp >> 29) == np.arange(8, dtype=np.uint32)[:, None]) & \
+                    ((mp & ((1 << 29) - 1)) == np.arange(mp.shape[1], dtype=np.uint32)[None, :])
+                on_cycle += int((~ident).sum()) * int(cnt_r)
+            products = domain * 8 + usable * 30 + on_cycle
             gps = products / (avg * 1e-3) / 1e9
             perm = {"k": k, "instances": n_inst, "chunk_len": 3, "sets": 3,
                     "field": "bn254 Fr montgomery", "avg_ms": round(avg, 4),
-                    "rows_per_s": round(rows / (avg * 1e-3)),
-                    "products_per_row": round(products / rows, 2),
+                    "rows_per_s": round(domain / (avg * 1e-3)),
+                    "products_per_row": round(products / domain, 2),
                     "roofline": {"bound": "field products", "achieved": round(gps, 1),
                                  "peak": MULBENCH_GPS, "unit": "G products/s",
                                  "frac": round(gps / MULBENCH_GPS, 4)},
-                    "written_GBs": round(rows * 32 * 11 / (avg * 1e-3) / 1e9, 1),
+                    "written_GBs": round(domain * 32 * 11 / (avg * 1e-3) / 1e9, 1),
                     "z_closes_to_one": closes}
             del sig, z
         except Exception as e:  # reported, never masks the headline
@@ -677,10 +713,12 @@ def main():
             buf = np.random.default_rng(3).integers(0, 256, (hm, 1024), dtype=np.uint8)
             msgs = [bytes(r) for r in buf]
             plan = hasher.Plan(msgs)
-            hasher.run_plan(eng, plan)
+            first = {}
+            hasher.run_plan(eng, plan, phases=first)  # allocates the plan's workspace
             torch.cuda.synchronize()
+            phases = {}
             t2 = time.perf_counter()
-            res = hasher.run_plan(eng, plan)
+            res = hasher.run_plan(eng, plan, phases=phases)  # reuses it: no allocation
             el2 = time.perf_counter() - t2
             ok = res.verified and all(res.digests[i] == hashlib.blake2b(msgs[i]).digest()
                                       for i in range(0, hm, max(1, hm // 64)))
@@ -689,8 +727,10 @@ def main():
                           "compressions_per_s": round(int(plan.start[-1]) / el2),
                           "digests_match_hashlib": ok,
                           "path": "fused",
+                          "phases_ms": phases, "first_call_workspace_ms": first.get("workspace_ms"),
                           "note": "wall clock incl. block upload (one async copy from pinned "
-                                  "memory) and the final h' download"}
+                                  "memory) and the final h' download; the workspace made by the "
+                                  "untimed first call is reused"}
         except Exception as e:
             hasher_aux = {"error": repr(e)}
 

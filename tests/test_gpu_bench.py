@@ -1,0 +1,50 @@
+"""bench.py end to end at a small size, in a child process (the driver's contract): one JSON
+line whose config describes the batch the headline timed (a later leg once rebound
+`rows` and the line carried the permutation leg's 2^k instead of the headline's rows)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra,rounds_of", [([], lambda i: 12), (["--mix"], None)])
+def test_bench_line_config_is_the_headline_batch(extra, rounds_of):
+    sys.path.insert(0, os.path.join(ROOT, "zk-odst_amd"))
+    from b2f import layout, synth
+
+    n = 64
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--batch", str(n), "--steps", "2",
+           "--warmup", "1", "--no-cpu", "--perm-k", "14", "--lookup-circuits", "1",
+           "--hasher-messages", "64", "--floor-reps", "2", "--aux-steps", "1",
+           "--export-rows", "4096"] + extra
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    x = synth.batch(n, rounds=12, rounds_mix=[1, 4, 12] if extra else None)
+    want_rows = int(sum(layout.rows(int(r)) for r in x["rounds"]))
+    cfg = line["config"]
+    assert cfg["batch_per_gpu"] == n
+    assert cfg["rows_per_gpu"] == want_rows
+    assert cfg["trace_bytes_per_gpu"] == want_rows * 44
+    assert str(n) in cfg["workload"]
+    assert line["n_gpus"] == 1 and line["steps"] == 2 and line["value"] > 0
+    assert line["roofline"]["bound"] == "hbm" and 0 < line["roofline"]["frac"] < 1.2
+    # the legs beside the headline ran and kept their own sizes
+    perm = line["permutation_columns"]
+    assert "error" not in perm, perm
+    assert perm["k"] == 14 and perm["z_closes_to_one"]
+    lk = line["lookup_columns"]
+    assert "error" not in lk and lk["all_rows_in_table"], lk
+    hs = line["hasher"]
+    assert "error" not in hs and hs["digests_match_hashlib"], hs
+    assert hs["phases_ms"]["workspace_ms"] < 50  # the timed call reuses the first call's buffers
+    fl = line["floors"]
+    assert "error" not in fl and fl["reps"] == 2 and fl["interleaved"], fl
+    assert line["other_path"]["verdict_clean"]

@@ -64,7 +64,7 @@ def test_layouter_row_budget():
 
 def test_bench_extras_watchdog():
     """bench.py's N > 1 guard: past the timeout rank 0 prints the headline line with the extras
-    marked timed out and the process exits 0; finished in time, it stays silent."""
+    marked timed out and the process exits non-zero (a hung collective is a failure); finished in time, it stays silent."""
     import io
     import json
     import os
@@ -77,14 +77,14 @@ def test_bench_extras_watchdog():
     exits, out = [], io.StringIO()
     wd = bench.ExtrasWatchdog(0.2, 0, lambda: {"metric": "m", "value": 1.0}, exit_fn=exits.append, out=out)
     time.sleep(0.6)
-    assert exits == [0]
+    assert exits == [bench.EXIT_EXTRAS_TIMEOUT] and bench.EXIT_EXTRAS_TIMEOUT != 0
     line = json.loads(out.getvalue())
     assert line["value"] == 1.0 and "timed out" in line["extras"]["error"]
     assert wd.finish() is False
     exits2, out2 = [], io.StringIO()
     wd2 = bench.ExtrasWatchdog(0.2, 1, lambda: {"value": 1.0}, exit_fn=exits2.append, out=out2)
     time.sleep(0.6)
-    assert exits2 == [0] and out2.getvalue() == ""  # other ranks exit silently
+    assert exits2 == [bench.EXIT_EXTRAS_TIMEOUT] and out2.getvalue() == ""  # other ranks exit silently
     wd3 = bench.ExtrasWatchdog(5.0, 0, lambda: {"value": 1.0}, exit_fn=exits.append, out=out)
     assert wd3.finish() is True
     wd0 = bench.ExtrasWatchdog(0, 0, lambda: {}, exit_fn=exits.append, out=out)

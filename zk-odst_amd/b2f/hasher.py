@@ -81,7 +81,7 @@ class Plan:
             import torch
 
             def pin(a):
-                a = np.ascontiguousarray(a)
+                a = np.array(a, order="C")  # a writable copy (h0 is a broadcast view)
                 return torch.from_numpy(a.view(np.int64 if a.dtype in (np.uint64, np.int64)
                                                else np.int32)).pin_memory()
 
@@ -139,10 +139,60 @@ def blake2b_batch(engine, messages, digest_size=64, key=b"", path="fused", devic
     return run_plan(engine, Plan(messages, digest_size, key), path, device, stream)
 
 
-def run_plan(engine, plan, path="fused", device="cuda:0", stream=None, _diag=None):
+class Workspace:
+    """Device buffers of a hasher batch: blocks, counters, flags, initial states, every step's
+    h', the step's compression inputs, the trace (advice + fixed) and the per-step reports.
+    Allocated once and reused by every run_plan call whose plan fits (no
+    allocation inside the fill hot calls). A plan keeps the workspace its first run made
+    (Plan.workspace); a caller running many plans can pass one sized for the largest."""
+
+    def __init__(self, n, compressions, steps, device="cuda:0", keep_inputs=False):
+        import torch
+
+        dev = torch.device(device)
+        R = rows(BLAKE2B_ROUNDS)
+        self.device, self.n, self.compressions, self.steps = dev, int(n), int(compressions), int(steps)
+        self.keep_inputs = bool(keep_inputs)
+        self.blocks = torch.empty((self.compressions, 16), dtype=torch.int64, device=dev)
+        self.t = torch.empty((self.compressions, 2), dtype=torch.int64, device=dev)
+        self.f = torch.empty(self.compressions, dtype=torch.int32, device=dev)
+        self.h0 = torch.empty((self.n, 8), dtype=torch.int64, device=dev)
+        self.fin_idx = torch.empty(self.n, dtype=torch.int64, device=dev)
+        self.offsets = torch.arange(self.n + 1, dtype=torch.int64, device=dev) * R
+        # h' of every compression, step-major like the plan: step j's outputs are rows
+        # start[j] .. start[j] + active[j] - 1, and step j + 1 reads its h from that prefix
+        self.hs = torch.empty((self.compressions, 8), dtype=torch.int64, device=dev)
+        self.inputs = torch.empty((self.compressions if keep_inputs else self.n) * 216,
+                                  dtype=torch.uint8, device=dev)
+        # one flat trace buffer: a step over `a` messages uses its first 10 * R * a words as
+        # advice[10][R * a] (column stride R * a) and the fixed column beside it
+        self.advice = torch.empty(_lib.NUM_ADVICE * R * self.n, dtype=torch.int32, device=dev)
+        self.fixed = torch.empty(R * self.n, dtype=torch.int32, device=dev)
+        self.report = torch.empty((self.steps, _lib.REPORT_BYTES // 8), dtype=torch.int64,
+                                  device=dev)
+
+    @classmethod
+    def for_plan(cls, plan, device="cuda:0", keep_inputs=False):
+        return cls(plan.n, int(plan.start[-1]), plan.steps, device, keep_inputs)
+
+    def fits(self, plan, device, keep_inputs=False):
+        import torch
+
+        return (torch.device(device) == self.device and plan.n <= self.n
+                and int(plan.start[-1]) <= self.compressions and plan.steps <= self.steps
+                and (self.keep_inputs or not keep_inputs))
+
+
+def run_plan(engine, plan, path="fused", device="cuda:0", stream=None, workspace=None,
+             phases=None, _diag=None):
     """The device half of blake2b_batch for a prebuilt Plan. The blocks go up in one
     asynchronous copy from page-locked memory (Plan.pinned), every block step runs on the
-    stream, and only the final chaining values come back to the host."""
+    stream, and only the final chaining values come back to the host. Buffers come from
+    `workspace` (a Workspace that fits the plan) or the plan's own, made by its first run.
+    `phases`, a dict, receives the call's phase times in ms: workspace (allocation, 0 when
+    reused), upload and steps (HIP events on the stream), download (host wall clock)."""
+    import time
+
     import torch
 
     if path not in ("split", "fused"):
@@ -155,34 +205,37 @@ def run_plan(engine, plan, path="fused", device="cuda:0", stream=None, _diag=Non
     compute = torch.cuda.ExternalStream(s, device=dev)
     p_blocks, p_t, p_f, p_h0, p_fin = plan.pinned()
     R = rows(BLAKE2B_ROUNDS)
-    # Everything is allocated, copied and launched on the one stream `s`; every host -> device
-    # copy is hipMemcpyAsync from page-locked memory on `s` (engine.copy_h2d_async). No host
-    # synchronize is needed (tests/test_gpu_hasher.py runs batches back to back on alternating
-    # paths, without one).
-    with torch.cuda.stream(compute):
-        d_blocks = torch.empty(p_blocks.shape, dtype=p_blocks.dtype, device=dev)
-        d_t = torch.empty(p_t.shape, dtype=p_t.dtype, device=dev)
-        d_f = torch.empty(p_f.shape, dtype=p_f.dtype, device=dev)
-        # h' of every compression, step-major like the plan: step j's outputs are rows
-        # start[j] .. start[j] + active[j] - 1, and step j + 1 reads its h from that prefix
-        h0 = torch.empty(p_h0.shape, dtype=p_h0.dtype, device=dev)
-        fin_idx = torch.empty(p_fin.shape, dtype=p_fin.dtype, device=dev)
-        offsets = torch.arange(n + 1, dtype=torch.int64, device=dev) * R
-        hs = torch.empty((int(plan.start[-1]), 8), dtype=torch.int64, device=dev)
-        keep = _diag is not None and _diag.get("keep_inputs")
-        inputs_all = torch.empty(int(plan.start[-1]) * 216 if keep else n * 216, dtype=torch.uint8,
-                                 device=dev)
-        advice = torch.empty((_lib.NUM_ADVICE, R * n), dtype=torch.int32, device=dev)
-        fixed = torch.empty(R * n, dtype=torch.int32, device=dev)
-        report = torch.empty((plan.steps, _lib.REPORT_BYTES // 8), dtype=torch.int64, device=dev)
-        # asynchronous DMAs from page-locked memory on `s` itself (engine.copy_h2d_async: torch's
-        # non_blocking copy is not ordered before the library's launches)
-        how = _diag.get("upload", "hip") if _diag is not None else "hip"
-        if how == "hip":
-            for d, p in ((d_blocks, p_blocks), (d_t, p_t), (d_f, p_f), (h0, p_h0), (fin_idx, p_fin)):
-                copy_h2d_async(d, p, s)
-        else:  # diagnostics (tools/hasher_race.py): torch's copy, non-blocking or blocking
-            nb = how != "blocking"
+    keep = _diag is not None and _diag.get("keep_inputs")
+    tw = time.perf_counter()
+    ws = workspace
+    if ws is None:
+        ws = getattr(plan, "workspace", None)
+        if ws is None or not ws.fits(plan, dev, keep):
+            # allocated on the stream `s` so its memory is ordered with the launches below
+            with torch.cuda.stream(compute):
+                ws = Workspace.for_plan(plan, dev, keep)
+            plan.workspace = ws
+    elif not ws.fits(plan, dev, keep):
+        raise _lib.B2FError(_lib.ERR_ARG, "run_plan: workspace too small for the plan")
+    alloc_ms = 1e3 * (time.perf_counter() - tw)
+    total_c = int(plan.start[-1])
+    d_blocks, d_t, d_f = ws.blocks[:total_c], ws.t[:total_c], ws.f[:total_c]
+    h0, fin_idx, hs = ws.h0[:n], ws.fin_idx[:n], ws.hs
+    offsets, inputs_all, advice, fixed, report = ws.offsets, ws.inputs, ws.advice, ws.fixed, ws.report
+    if phases is not None:
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record(compute)
+    # Every host -> device copy is hipMemcpyAsync from page-locked memory on `s` itself
+    # (engine.copy_h2d_async: torch's non_blocking copy is not ordered before the library's
+    # launches), so no host synchronize is needed (tests/test_gpu_hasher.py runs batches back
+    # to back on alternating paths, without one).
+    how = _diag.get("upload", "hip") if _diag is not None else "hip"
+    if how == "hip":
+        for d, p in ((d_blocks, p_blocks), (d_t, p_t), (d_f, p_f), (h0, p_h0), (fin_idx, p_fin)):
+            copy_h2d_async(d, p, s)
+    else:  # diagnostics (tools/hasher_race.py): torch's copy, non-blocking or blocking
+        nb = how != "blocking"
+        with torch.cuda.stream(compute):
             for d, p in ((d_blocks, p_blocks), (d_t, p_t), (d_f, p_f), (h0, p_h0), (fin_idx, p_fin)):
                 d.copy_(p, non_blocking=nb)
     if _diag is not None and _diag.get("sync_upload"):  # diagnostics (tools/hasher_race.py)
@@ -190,6 +243,8 @@ def run_plan(engine, plan, path="fused", device="cuda:0", stream=None, _diag=Non
             compute.synchronize()
         else:
             torch.cuda.synchronize(dev)
+    if phases is not None:
+        ev[1].record(compute)
     for j in range(plan.steps):
         a = int(plan.active[j])
         s0 = int(plan.start[j])
@@ -208,18 +263,26 @@ def run_plan(engine, plan, path="fused", device="cuda:0", stream=None, _diag=Non
                             fixed.data_ptr(), h_out, s)
             engine.eval_dev(advice.data_ptr(), fixed.data_ptr(), offsets.data_ptr(), a, total,
                             report[j].data_ptr(), s)
+    if phases is not None:
+        ev[2].record(compute)
     engine.sync(s)
+    td = time.perf_counter()
     with torch.cuda.stream(compute):
         fin_host = hs.index_select(0, fin_idx).cpu().numpy().view(np.uint64)
-        raw = report.cpu().numpy().view(np.uint64)
+        raw = report[:plan.steps].cpu().numpy().view(np.uint64)
+    if phases is not None:
+        phases.update({"workspace_ms": round(alloc_ms, 3),
+                       "upload_ms": round(ev[0].elapsed_time(ev[1]), 3),
+                       "steps_ms": round(ev[1].elapsed_time(ev[2]), 3),
+                       "download_ms": round(1e3 * (time.perf_counter() - td), 3)})
     reps = [_lib.EvalReport.from_buffer_copy(raw[j].tobytes()).as_dict()
             for j in range(plan.steps)]
     res = ChainResult(plan, reps, fin_host)
     if _diag is not None:  # diagnostics: every step's h' (step-major, sorted order)
-        res.all_h = hs.cpu().numpy().view(np.uint64)
+        res.all_h = hs[:total_c].cpu().numpy().view(np.uint64)
         res.stream = int(s)
         if keep:  # every step's b2f_input records as chain_inputs built them
-            res.all_inputs = inputs_all.cpu().numpy()
+            res.all_inputs = inputs_all[:total_c * 216].cpu().numpy()
     return res
 
 

@@ -269,9 +269,10 @@ __device__ __forceinline__ void producer_words(uint64_t* prod, const Ops& P, uin
 
 // MODE (diagnostics; the product launches FZ_FULL, with FZ_INJECT only under the test hook)
 #ifndef B2F_FUSED_WAVES
-// waves per SIMD the half-round kernel is compiled for (its VGPR budget): 2 -- the launch runs 2
-// workgroups per CU, and the larger budget (153 VGPRs, no scratch) was 1.7 % faster on average
-// over four boxes (-3.8 / -1.3 / +0.9 / -2.5 %, profiles/r02l_ab15-18)
+// minimum waves per SIMD the half-round kernel is compiled for: 2, i.e. a VGPR ceiling of 256.
+// The kernel allocates 159 VGPRs, which leaves room for 3 waves per SIMD, and the launch runs
+// B2F_FUSED_HR_PER_CU = 3 workgroups (of 4 waves) per CU: 3 waves per SIMD. (Forcing a budget
+// of 3 per SIMD at compile time is not needed while the allocation stays <= 168.)
 #define B2F_FUSED_WAVES 2
 #endif
 #ifndef B2F_FUSED_HR_PER_CU
