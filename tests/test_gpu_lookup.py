@@ -156,3 +156,34 @@ def test_spread_table_columns(engine, form):
             want = np.zeros((usable, 4), dtype=np.uint64)
             want[:, 0] = col
         assert np.array_equal(got[c], want), c
+
+
+@pytest.mark.parametrize("form", [1, 3])
+def test_lookup_zero_factor_reported_then_clean(engine, trace, form):
+    """beta = -A[row] makes (A + beta) and (A' + beta) zero for that row's value, so
+    the den total is zero: the call reports B2F_ERR_FIELD at b2f_sync (three-level grand product,
+    inversion on the side stream), and the next call with sound challenges syncs clean and
+    matches the oracle's closing value."""
+    import lookup as lk
+    import torch
+
+    import b2f
+
+    s = torch.cuda.current_stream().cuda_stream
+    usable = (1 << 17) - 7
+    p = _mod(form)
+    theta, _, gamma = _chal(19, form)
+    adv, _ = trace.host_trace()
+    row = 1234
+    a = lk.compress(theta, int(adv[0, row]), int(adv[1, row]), int(adv[2, row]), p)
+    beta = (p - a) % p
+    out, bad = trace.lookup_columns(engine, [0], usable, theta, beta, gamma, form=form)
+    with pytest.raises(b2f.B2FError) as e:
+        engine.sync(s)
+    assert e.value.code == b2f._lib.ERR_FIELD
+    beta = (beta + 1) % p
+    out, bad = trace.lookup_columns(engine, [0], usable, theta, beta, gamma, form=form)
+    engine.sync(s)
+    z = _col_ints(out[0, 4, usable:usable + 1])[0]
+    one = 1 if form in (0, 2) else R256 % p
+    assert z == one  # a valid lookup closes to 1

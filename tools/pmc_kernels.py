@@ -10,8 +10,9 @@ import sys
 
 
 def short(k):
-    k = k.split("(")[0] if "(anonymous namespace)::" not in k else k.split("(anonymous namespace)::")[-1].split("(")[0]
-    return k.split(" ")[-1]
+    if "(anonymous namespace)::" in k:
+        k = k.split("(anonymous namespace)::", 1)[1]
+    return k.split("(")[0].split(" ")[-1]
 
 
 def main():
