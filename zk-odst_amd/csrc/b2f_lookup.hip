@@ -370,33 +370,32 @@ __device__ __forceinline__ uint32_t wave_max_scan(uint32_t v) {
   return v;
 }
 
-constexpr uint32_t PW_ROWS = 1024;  // rows per wave in the permute pass
-#ifndef B2F_LK_WPE
-#define B2F_LK_WPE 1
-#endif
-template <class F>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(B2F_LK_WPE))) void lk_permute_kernel(
-    const uint32_t* __restrict__ adv, uint64_t total_rows, const uint64_t* __restrict__ row_begin,
-    uint32_t c0, uint64_t usable, const Fe* __restrict__ Tx, const Fe* __restrict__ Ts,
-    const uint32_t* __restrict__ pos, const uint32_t* __restrict__ dcnt,
-    const uint32_t* __restrict__ lp, const uint32_t* __restrict__ samp,
-    const uint32_t* __restrict__ srk, const uint32_t* __restrict__ lrk, bool mont,
-    uint64_t* __restrict__ out, uint64_t out_rows, Chal ch, Fe* __restrict__ num,
-    Fe* __restrict__ den) {
+// Rows of a circuit -> (rank of A'[p], rank of S'[p]) into rr[p], a wave per PW_ROWS consecutive
+// rows, 64 at a time: r is the running maximum of srk (a wave max-scan carried from the previous
+// 64 rows), repeated rows are counted by ballot, and the leftover rank of repeated row j is the
+// running maximum of lrk. Two binary searches of pos / LP per wave give the carries at its first
+// row; the wave's srk values and its window of lrk (at most PW_ROWS repeated rows) are loaded up
+// front, so the 64-row steps depend on each other only through LDS and the scans. Integer work
+// only: it runs at full occupancy and leaves the field work to lk_permute_kernel.
+constexpr uint32_t PW_ROWS = 1024, PW_IT = PW_ROWS / 64;
+__global__ __launch_bounds__(256) void lk_rows_kernel(uint64_t usable, const uint32_t* __restrict__ pos,
+                                                      const uint32_t* __restrict__ dcnt,
+                                                      const uint32_t* __restrict__ lp,
+                                                      const uint32_t* __restrict__ samp,
+                                                      const uint32_t* __restrict__ srk,
+                                                      const uint32_t* __restrict__ lrk,
+                                                      uint2* __restrict__ rr) {
   const uint32_t c = blockIdx.y, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
-  const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
-  Fe* nm = num + (uint64_t)c * gp::elems(usable);
-  Fe* dn = den + (uint64_t)c * gp::elems(usable);
-  const uint64_t nq = gp::n_chunks(usable);
-  const Circ k = circ(row_begin, total_rows, usable, c0 + c);
   const uint32_t* P = pos + (uint64_t)c * TROWS;
   const uint32_t* D = dcnt + (uint64_t)c * TROWS;
   const uint32_t* L = lp + (uint64_t)c * TROWS;
-  const uint32_t* SR = srk + (uint64_t)c * mark_stride(usable);
-  const uint32_t* LR = lrk + (uint64_t)c * mark_stride(usable);
+  const uint64_t ms = mark_stride(usable);
+  const uint32_t* SR = srk + (uint64_t)c * ms;
+  const uint32_t* LR = lrk + (uint64_t)c * ms;
+  uint2* RR = rr + (uint64_t)c * ms;
   const uint32_t n_left = (uint32_t)usable - D[TROWS - 1];
   __shared__ uint32_t sP[SAMPLE], sL[SAMPLE];
+  __shared__ uint32_t win[4][PW_ROWS];  // each wave's window of lrk
   {
     const uint4* sa = reinterpret_cast<const uint4*>(samp + (uint64_t)c * 2 * SAMPLE);
     uint4* sp4 = reinterpret_cast<uint4*>(sP);
@@ -409,47 +408,136 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(B2F_LK_WPE)
   __syncthreads();
   const uint64_t b0 = ((uint64_t)blockIdx.x * 4 + wv) * PW_ROWS;
   if (b0 >= usable) return;
-  const uint64_t e0 = b0 + PW_ROWS < usable ? b0 + PW_ROWS : usable;
+  const uint32_t nrows = (uint32_t)(b0 + PW_ROWS < usable ? PW_ROWS : usable - b0);
   // carries at the wave's first row: the run holding b0 (as its mark r + 1), the repeated rows
   // before b0 (jb) and the mark of the leftover rank that repeated row jb takes
   const uint32_t r0 = last_le(P, sP, (uint32_t)b0);
   uint32_t rcar = r0 + 1u;
-  uint32_t jb = (uint32_t)b0 - D[r0] + (P[r0] == (uint32_t)b0 ? 1u : 0u);
-  uint32_t lcar = jb < n_left ? (uint32_t)TROWS - last_le(L, sL, n_left - 1u - jb) : 0u;
-  uint64_t* o = out + (uint64_t)(c0 + c) * 5 * out_rows * 4;
-  for (uint64_t base = b0; base < e0; base += 64) {
-    const uint64_t p = base + lane;
-    const bool in = p < e0;
-    const uint32_t m = in ? SR[p] : 0u;
-    const uint32_t ql = jb + lane < n_left ? LR[jb + lane] : 0u;
+  const uint32_t j0 = (uint32_t)b0 - D[r0] + (P[r0] == (uint32_t)b0 ? 1u : 0u);
+  uint32_t lcar = j0 < n_left ? (uint32_t)TROWS - last_le(L, sL, n_left - 1u - j0) : 0u;
+  uint32_t sm[PW_IT];
+#pragma unroll
+  for (uint32_t i = 0; i < PW_IT; i++) {
+    const uint32_t q = 64u * i + lane;
+    sm[i] = q < nrows ? SR[b0 + q] : 0u;
+    win[wv][q] = j0 + q < n_left ? LR[j0 + q] : 0u;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  uint32_t jo = 0;  // repeated rows of this wave so far (window offset)
+#pragma unroll
+  for (uint32_t i = 0; i < PW_IT; i++) {
+    const uint32_t q = 64u * i + lane;
+    const uint32_t m = sm[i];
     uint32_t rv = wave_max_scan(m);
-    rv = rv > rcar ? rv : rcar;  // the run holding p, as r + 1
+    rv = rv > rcar ? rv : rcar;  // the run holding row b0 + q, as r + 1
     rcar = __builtin_amdgcn_readlane(rv, 63);
-    const bool rep = in && m == 0;
+    const bool rep = q < nrows && m == 0;
     const uint64_t bal = __ballot(rep);
     const uint32_t kr = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
     const uint32_t nrep = (uint32_t)__popcll(bal);
-    uint32_t lv = wave_max_scan(ql);
-    lv = lv > lcar ? lv : lcar;  // lane i: the leftover mark of repeated row jb + i
+    uint32_t lv = wave_max_scan(jo + lane < PW_ROWS ? win[wv][jo + lane] : 0u);
+    lv = lv > lcar ? lv : lcar;  // lane i: the leftover mark of repeated row j0 + jo + i
     const uint32_t lm = __shfl(lv, (int)kr, 64);
     if (nrep) {
       lcar = __builtin_amdgcn_readlane(lv, nrep - 1u);
-      jb += nrep;
+      jo += nrep;
     }
-    if (!in) break;
+    if (q < nrows) RR[b0 + q] = make_uint2(rv - 1u, rep ? (uint32_t)TROWS - lm : rv - 1u);
+  }
+}
+
+// A wave's 64 consecutive 32-byte elements (lane l holds element l) stored through the wave's
+// 2 KiB of LDS so that each store instruction writes 1 KiB contiguous (lane l the 16-byte chunk
+// l): a lane storing its own element writes 16 bytes every 32 per instruction, half of every
+// line it touches, and the permute pass stored at 2.8 TB/s that way.
+__device__ __forceinline__ void wave_stage(uint4* st, uint32_t lane, const Fe& v) {
+  st[2 * lane] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+  st[2 * lane + 1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void wave_unstage_done() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+// elements 0 .. n - 1 of the staged 64 to dst (contiguous)
+__device__ __forceinline__ void wave_store_rows(uint64_t* dst, uint4* st, uint32_t lane, const Fe& v,
+                                                uint32_t n) {
+  wave_stage(st, lane, v);
+  const uint4 x = st[lane], y = st[64 + lane];
+  wave_unstage_done();
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  if ((lane >> 1) < n) d[lane] = x;
+  if (32u + (lane >> 1) < n) d[64 + lane] = y;
+}
+// the staged 64 rows (a 64-row aligned group) to their gp::slot_of slots: 16 runs of 4
+// elements (128 bytes) 512 bytes apart, 8 lanes per run
+__device__ __forceinline__ void wave_store_slots(Fe* slots_base, uint4* st, uint32_t lane, const Fe& v) {
+  wave_stage(st, lane, v);
+  const uint32_t c = lane & 7u, e = c >> 1, h = c & 1u, r = lane >> 3;
+  const uint4 x = st[2 * (16 * e + r) + h], y = st[2 * (16 * e + r + 8) + h];
+  wave_unstage_done();
+  uint4* d = reinterpret_cast<uint4*>(slots_base);  // element (j * 16 + e), half h
+  d[2 * (r * 16 + e) + h] = x;
+  d[2 * ((r + 8) * 16 + e) + h] = y;
+}
+
+// The four columns and the grand product's factors, a lane per row (grid-stride over 64-row
+// groups): A = Tx[x], S = Tx[p] (row 0's value past the table), A' = Ts[r], S' = Ts[r'] from
+// lk_rows_kernel.
+template <class F>
+__global__ __launch_bounds__(256) void lk_permute_kernel(
+    const uint32_t* __restrict__ adv, uint64_t total_rows, const uint64_t* __restrict__ row_begin,
+    uint32_t c0, uint64_t usable, const Fe* __restrict__ Tx, const Fe* __restrict__ Ts,
+    const uint2* __restrict__ rr, bool mont, uint64_t* __restrict__ out, uint64_t out_rows, Chal ch,
+    Fe* __restrict__ num, Fe* __restrict__ den) {
+  __shared__ uint4 stage[4][128];
+  const uint32_t c = blockIdx.y, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint4* st = stage[wv];
+  const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
+  const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
+  Fe* nm = num + (uint64_t)c * gp::elems(usable);
+  Fe* dn = den + (uint64_t)c * gp::elems(usable);
+  const Circ k = circ(row_begin, total_rows, usable, c0 + c);
+  const uint2* RR = rr + (uint64_t)c * mark_stride(usable);
+  uint64_t* o = out + (uint64_t)(c0 + c) * 5 * out_rows * 4;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 + 64 * wv; base < usable; base += stride) {
+    const uint64_t p = base + lane;
+    const bool in = p < usable;
+    const uint32_t nv = (uint32_t)(usable - base < 64 ? usable - base : 64);
     const uint32_t x = p < k.n_in ? (adv[total_rows + k.first + p] & 0xffffu) : 0u;
+    const uint2 r = in ? RR[p] : make_uint2(0u, 0u);
+#ifndef B2F_LK_ABL
+#define B2F_LK_ABL 0  // diagnostics (variant builds only): 1 no gathers, 2 no products, 4 no column stores
+#endif
+#if B2F_LK_ABL & 1
+    Fe a = beta, sv = gamma, ap = beta, sp = gamma;
+    a.w[0] ^= x; sv.w[0] ^= (uint32_t)p; ap.w[0] ^= r.x; sp.w[0] ^= r.y;
+#else
     const Fe a = Tx[x];
     const Fe sv = Tx[p < (uint64_t)TROWS ? (uint32_t)p : 0u];
-    const Fe ap = Ts[rv - 1u];
-    const Fe sp = rep ? Ts[(uint32_t)TROWS - lm] : ap;
-    store(o + 4 * p, out_form<F>(a, mont));
-    store(o + (out_rows + p) * 4, out_form<F>(sv, mont));
-    store(o + (2 * out_rows + p) * 4, out_form<F>(ap, mont));
-    store(o + (3 * out_rows + p) * 4, out_form<F>(sp, mont));
-    // the grand product's factors (A + beta)(S + gamma) / ((A' + beta)(S' + gamma))
-    nm[gp::slot_of(p, nq)] = field::mul<F>(field::add<F>(a, beta), field::add<F>(sv, gamma));
-    dn[gp::slot_of(p, nq)] = field::mul<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma));
+    const Fe ap = Ts[r.x];
+    const Fe sp = Ts[r.y];
+#endif
+    if (!(B2F_LK_ABL & 4)) {
+      wave_store_rows(o + 4 * base, st, lane, out_form<F>(a, mont), nv);
+      wave_store_rows(o + (out_rows + base) * 4, st, lane, out_form<F>(sv, mont), nv);
+      wave_store_rows(o + (2 * out_rows + base) * 4, st, lane, out_form<F>(ap, mont), nv);
+      wave_store_rows(o + (3 * out_rows + base) * 4, st, lane, out_form<F>(sp, mont), nv);
+    }
+    // the grand product's factors (A + beta)(S + gamma) / ((A' + beta)(S' + gamma)); rows past
+    // `usable` land in slots of the last tile that the grand product never reads
+    const uint64_t sb = (base / (gp::ZC * gp::ZC)) * (gp::ZC * gp::ZC) + (base / gp::ZC) % gp::ZC;
+    if (B2F_LK_ABL & 2) {
+      wave_store_slots(nm + sb, st, lane, field::add<F>(field::add<F>(a, beta), field::add<F>(sv, gamma)));
+      wave_store_slots(dn + sb, st, lane, field::add<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma)));
+    } else {
+      wave_store_slots(nm + sb, st, lane, field::mul<F>(field::add<F>(a, beta), field::add<F>(sv, gamma)));
+      wave_store_slots(dn + sb, st, lane, field::mul<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma)));
+    }
   }
 }
 
@@ -469,6 +557,7 @@ struct Carve {
   uint32_t* samp;  // group x 2 x SAMPLE
   uint32_t* srk;   // group x mark_stride(usable): run-start marks
   uint32_t* lrk;   // group x mark_stride(usable): leftover marks
+  uint2* rr;       // group x mark_stride(usable): (rank of A', rank of S') per row
   uint32_t* part;  // group x SC_PARTS x 3 (rank-scan part totals)
   Fe* num;  // group x usable
   Fe* den;
@@ -507,6 +596,7 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.samp = (uint32_t*)take(8ull * SAMPLE * group);
   k.srk = (uint32_t*)take(4ull * mark_stride(usable) * group);
   k.lrk = (uint32_t*)take(4ull * mark_stride(usable) * group);
+  k.rr = (uint2*)take(8ull * mark_stride(usable) * group);
   k.part = (uint32_t*)take(12ull * SC_PARTS * group);
   k.num = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);  // chunk-interleaved (b2f_gprod.h)
   k.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);
@@ -545,12 +635,13 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
     hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
     hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
                        k.part, k.pos, k.dcnt, k.lp, k.samp, k.srk, k.lrk);
-    // permute: PW_ROWS rows per wave, 4 waves per workgroup (the LDS samples for the waves'
-    // two searches staged once per workgroup)
-    const uint32_t px = (uint32_t)((usable_rows + 4 * PW_ROWS - 1) / (4 * PW_ROWS));
+    hipLaunchKernelGGL(lk_rows_kernel, dim3((uint32_t)((usable_rows + 4 * PW_ROWS - 1) / (4 * PW_ROWS)), g),
+                       dim3(256), 0, s, usable_rows, k.pos, k.dcnt, k.lp, k.samp, k.srk, k.lrk, k.rr);
+    // permute: ~4096 rows per workgroup
+    const uint32_t px = (uint32_t)((usable_rows + 4095) / 4096);
     hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
-                       d_row_begin, c0, usable_rows, k.Tx, k.Ts, k.pos, k.dcnt, k.lp, k.samp, k.srk,
-                       k.lrk, mont, d_out, out_rows, ch, k.num, k.den);
+                       d_row_begin, c0, usable_rows, k.Tx, k.Ts, k.rr, mont, d_out, out_rows, ch,
+                       k.num, k.den);
     e = gp::run<F>(g, usable_rows, mont, d_out + ((uint64_t)c0 * 5 + 4) * out_rows * 4,
                    5 * out_rows * 4, k.num, k.den, k.zs, nullptr, nullptr, s, nullptr, sticky, side);
     if (e != hipSuccess) return e;
