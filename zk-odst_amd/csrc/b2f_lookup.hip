@@ -448,6 +448,9 @@ __global__ __launch_bounds__(256) void lk_rows_kernel(uint64_t usable, const uin
   }
 }
 
+#ifndef B2F_LK_NT
+#define B2F_LK_NT 0  // non-temporal stores: 1 the columns, 2 the factors
+#endif
 // A wave's 64 consecutive 32-byte elements (lane l holds element l) stored through the wave's
 // 2 KiB of LDS so that each store instruction writes 1 KiB contiguous (lane l the 16-byte chunk
 // l): a lane storing its own element writes 16 bytes every 32 per instruction, half of every
@@ -469,8 +472,13 @@ __device__ __forceinline__ void wave_store_rows(uint64_t* dst, uint4* st, uint32
   const uint4 x = st[lane], y = st[64 + lane];
   wave_unstage_done();
   uint4* d = reinterpret_cast<uint4*>(dst);
+#if B2F_LK_NT & 1
+  if ((lane >> 1) < n) __builtin_nontemporal_store(x, d + lane);
+  if (32u + (lane >> 1) < n) __builtin_nontemporal_store(y, d + 64 + lane);
+#else
   if ((lane >> 1) < n) d[lane] = x;
   if (32u + (lane >> 1) < n) d[64 + lane] = y;
+#endif
 }
 // the staged 64 rows (a 64-row aligned group) to their gp::slot_of slots: 16 runs of 4
 // elements (128 bytes) 512 bytes apart, 8 lanes per run
@@ -480,8 +488,13 @@ __device__ __forceinline__ void wave_store_slots(Fe* slots_base, uint4* st, uint
   const uint4 x = st[2 * (16 * e + r) + h], y = st[2 * (16 * e + r + 8) + h];
   wave_unstage_done();
   uint4* d = reinterpret_cast<uint4*>(slots_base);  // element (j * 16 + e), half h
+#if B2F_LK_NT & 2
+  __builtin_nontemporal_store(x, d + 2 * (r * 16 + e) + h);
+  __builtin_nontemporal_store(y, d + 2 * ((r + 8) * 16 + e) + h);
+#else
   d[2 * (r * 16 + e) + h] = x;
   d[2 * ((r + 8) * 16 + e) + h] = y;
+#endif
 }
 
 // The four columns and the grand product's factors, a lane per row (grid-stride over 64-row
