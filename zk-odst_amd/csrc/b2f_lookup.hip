@@ -451,6 +451,9 @@ __global__ __launch_bounds__(256) void lk_rows_kernel(uint64_t usable, const uin
 #ifndef B2F_LK_NT
 #define B2F_LK_NT 0  // non-temporal stores: 1 the columns, 2 the factors
 #endif
+__device__ __forceinline__ void nt_store(uint4* p, const uint4& v) {
+  __builtin_nontemporal_store(field::u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<field::u32x4*>(p));
+}
 // A wave's 64 consecutive 32-byte elements (lane l holds element l) stored through the wave's
 // 2 KiB of LDS so that each store instruction writes 1 KiB contiguous (lane l the 16-byte chunk
 // l): a lane storing its own element writes 16 bytes every 32 per instruction, half of every
@@ -473,8 +476,8 @@ __device__ __forceinline__ void wave_store_rows(uint64_t* dst, uint4* st, uint32
   wave_unstage_done();
   uint4* d = reinterpret_cast<uint4*>(dst);
 #if B2F_LK_NT & 1
-  if ((lane >> 1) < n) __builtin_nontemporal_store(x, d + lane);
-  if (32u + (lane >> 1) < n) __builtin_nontemporal_store(y, d + 64 + lane);
+  if ((lane >> 1) < n) nt_store(d + lane, x);
+  if (32u + (lane >> 1) < n) nt_store(d + 64 + lane, y);
 #else
   if ((lane >> 1) < n) d[lane] = x;
   if (32u + (lane >> 1) < n) d[64 + lane] = y;
@@ -489,8 +492,8 @@ __device__ __forceinline__ void wave_store_slots(Fe* slots_base, uint4* st, uint
   wave_unstage_done();
   uint4* d = reinterpret_cast<uint4*>(slots_base);  // element (j * 16 + e), half h
 #if B2F_LK_NT & 2
-  __builtin_nontemporal_store(x, d + 2 * (r * 16 + e) + h);
-  __builtin_nontemporal_store(y, d + 2 * ((r + 8) * 16 + e) + h);
+  nt_store(d + 2 * (r * 16 + e) + h, x);
+  nt_store(d + 2 * ((r + 8) * 16 + e) + h, y);
 #else
   d[2 * (r * 16 + e) + h] = x;
   d[2 * ((r + 8) * 16 + e) + h] = y;
