@@ -449,7 +449,11 @@ __global__ __launch_bounds__(256) void lk_rows_kernel(uint64_t usable, const uin
 }
 
 #ifndef B2F_LK_NT
-#define B2F_LK_NT 0  // non-temporal stores: 1 the columns, 2 the factors
+#define B2F_LK_NT 2  // non-temporal stores: 1 the columns, 2 the factors (3 both). The factors
+                     // non-temporal: permute pass 552 -> 358 us, the columns too: 546 (alone)
+#endif
+#ifndef B2F_LK_SEARCH
+#define B2F_LK_SEARCH 0
 #endif
 __device__ __forceinline__ void nt_store(uint4* p, const uint4& v) {
   __builtin_nontemporal_store(field::u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<field::u32x4*>(p));
@@ -508,9 +512,24 @@ __global__ __launch_bounds__(256) void lk_permute_kernel(
     const uint32_t* __restrict__ adv, uint64_t total_rows, const uint64_t* __restrict__ row_begin,
     uint32_t c0, uint64_t usable, const Fe* __restrict__ Tx, const Fe* __restrict__ Ts,
     const uint2* __restrict__ rr, bool mont, uint64_t* __restrict__ out, uint64_t out_rows, Chal ch,
-    Fe* __restrict__ num, Fe* __restrict__ den) {
+    Fe* __restrict__ num, Fe* __restrict__ den, const uint32_t* __restrict__ sr_pos,
+    const uint32_t* __restrict__ sr_dcnt, const uint32_t* __restrict__ sr_lp,
+    const uint32_t* __restrict__ samp) {
   __shared__ uint4 stage[4][128];
   const uint32_t c = blockIdx.y, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+#if B2F_LK_SEARCH
+  __shared__ uint32_t sP[SAMPLE], sL[SAMPLE];
+  {
+    const uint4* sa = reinterpret_cast<const uint4*>(samp + (uint64_t)c * 2 * SAMPLE);
+    uint4* sp4 = reinterpret_cast<uint4*>(sP);
+    uint4* sl4 = reinterpret_cast<uint4*>(sL);
+    for (uint32_t i = threadIdx.x; i < (uint32_t)SAMPLE / 4; i += 256) {
+      sp4[i] = sa[i];
+      sl4[i] = sa[SAMPLE / 4 + i];
+    }
+  }
+  __syncthreads();
+#endif
   uint4* st = stage[wv];
   const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
   const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
@@ -525,7 +544,19 @@ __global__ __launch_bounds__(256) void lk_permute_kernel(
     const bool in = p < usable;
     const uint32_t nv = (uint32_t)(usable - base < 64 ? usable - base : 64);
     const uint32_t x = p < k.n_in ? (adv[total_rows + k.first + p] & 0xffffu) : 0u;
+#if B2F_LK_SEARCH  // diagnostics: per-row searches instead of lk_rows_kernel
+    uint2 r = make_uint2(0u, 0u);
+    if (in) {
+      const uint32_t* P = sr_pos + (uint64_t)c * TROWS;
+      const uint32_t* D = sr_dcnt + (uint64_t)c * TROWS;
+      const uint32_t* L = sr_lp + (uint64_t)c * TROWS;
+      const uint32_t n_left = (uint32_t)usable - D[TROWS - 1];
+      r.x = last_le(P, sP, (uint32_t)p);
+      r.y = P[r.x] == (uint32_t)p ? r.x : last_le(L, sL, n_left - 1u - ((uint32_t)p - D[r.x]));
+    }
+#else
     const uint2 r = in ? RR[p] : make_uint2(0u, 0u);
+#endif
 #ifndef B2F_LK_ABL
 #define B2F_LK_ABL 0  // diagnostics (variant builds only): 1 no gathers, 2 no products, 4 no column stores
 #endif
@@ -651,13 +682,14 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
     hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
     hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
                        k.part, k.pos, k.dcnt, k.lp, k.samp, k.srk, k.lrk);
-    hipLaunchKernelGGL(lk_rows_kernel, dim3((uint32_t)((usable_rows + 4 * PW_ROWS - 1) / (4 * PW_ROWS)), g),
+    if (!B2F_LK_SEARCH)
+      hipLaunchKernelGGL(lk_rows_kernel, dim3((uint32_t)((usable_rows + 4 * PW_ROWS - 1) / (4 * PW_ROWS)), g),
                        dim3(256), 0, s, usable_rows, k.pos, k.dcnt, k.lp, k.samp, k.srk, k.lrk, k.rr);
     // permute: ~4096 rows per workgroup
     const uint32_t px = (uint32_t)((usable_rows + 4095) / 4096);
     hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
                        d_row_begin, c0, usable_rows, k.Tx, k.Ts, k.rr, mont, d_out, out_rows, ch,
-                       k.num, k.den);
+                       k.num, k.den, k.pos, k.dcnt, k.lp, k.samp);
     e = gp::run<F>(g, usable_rows, mont, d_out + ((uint64_t)c0 * 5 + 4) * out_rows * 4,
                    5 * out_rows * 4, k.num, k.den, k.zs, nullptr, nullptr, s, nullptr, sticky, side);
     if (e != hipSuccess) return e;
