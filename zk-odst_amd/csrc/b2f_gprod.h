@@ -53,6 +53,56 @@ __host__ __device__ inline uint64_t elems(uint64_t usable) {
   return (usable + ZC * ZC - 1) / (ZC * ZC) * (ZC * ZC);
 }
 
+// A wave's 64 consecutive 32-byte elements (lane l holds element l) stored through the wave's
+// 2 KiB of LDS (st: 128 x 16 B) so that each store instruction writes 1 KiB contiguous (lane l
+// the 16-byte chunk l); a lane storing its own element writes 16 bytes every 32 per instruction.
+// NT: non-temporal stores (data no later kernel of the call re-reads soon).
+__device__ __forceinline__ void nt_store(uint4* p, const uint4& v) {
+  __builtin_nontemporal_store(field::u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<field::u32x4*>(p));
+}
+template <bool NT>
+__device__ __forceinline__ void put16(uint4* p, const uint4& v) {
+  if (NT) nt_store(p, v); else *p = v;
+}
+__device__ __forceinline__ void wave_stage(uint4* st, uint32_t lane, const Fe& v) {
+  st[2 * lane] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+  st[2 * lane + 1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void wave_unstage_done() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+// elements 0 .. n - 1 of the staged 64 to dst (contiguous)
+template <bool NT>
+__device__ __forceinline__ void wave_store_rows(uint64_t* dst, uint4* st, uint32_t lane, const Fe& v,
+                                                uint32_t n) {
+  wave_stage(st, lane, v);
+  const uint4 x = st[lane], y = st[64 + lane];
+  wave_unstage_done();
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  if ((lane >> 1) < n) put16<NT>(d + lane, x);
+  if (32u + (lane >> 1) < n) put16<NT>(d + 64 + lane, y);
+}
+// The staged 64 rows base .. base + 63 (base a multiple of 64) to their slot_of slots: 16 runs of
+// 4 elements (128 bytes) 512 bytes apart, 8 lanes per run. slots_base = the array + the slot of
+// row base. Non-temporal by default: the lookup's permute pass wrote its factors 1.55x faster so
+// (552 -> 358 us, the write-back stores' partial lines evicting the gathered tables).
+template <bool NT>
+__device__ __forceinline__ void wave_store_slots(Fe* slots_base, uint4* st, uint32_t lane, const Fe& v) {
+  wave_stage(st, lane, v);
+  const uint32_t c = lane & 7u, e = c >> 1, h = c & 1u, r = lane >> 3;
+  const uint4 x = st[2 * (16 * e + r) + h], y = st[2 * (16 * e + r + 8) + h];
+  wave_unstage_done();
+  uint4* d = reinterpret_cast<uint4*>(slots_base);  // element (j * 16 + e), half h
+  put16<NT>(d + 2 * (r * 16 + e) + h, x);
+  put16<NT>(d + 2 * ((r + 8) * 16 + e) + h, y);
+}
+__host__ __device__ inline uint64_t slot_base64(uint64_t base) {  // slot of row base (64 | base)
+  return (base / (ZC * ZC)) * (ZC * ZC) + (base / ZC) % ZC;
+}
+
 template <class F>
 __device__ __forceinline__ Fe out_form(const Fe& a, bool mont) {
   return mont ? a : field::to_canonical<F>(a);

@@ -455,55 +455,6 @@ __global__ __launch_bounds__(256) void lk_rows_kernel(uint64_t usable, const uin
 #ifndef B2F_LK_SEARCH
 #define B2F_LK_SEARCH 0
 #endif
-__device__ __forceinline__ void nt_store(uint4* p, const uint4& v) {
-  __builtin_nontemporal_store(field::u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<field::u32x4*>(p));
-}
-// A wave's 64 consecutive 32-byte elements (lane l holds element l) stored through the wave's
-// 2 KiB of LDS so that each store instruction writes 1 KiB contiguous (lane l the 16-byte chunk
-// l): a lane storing its own element writes 16 bytes every 32 per instruction, half of every
-// line it touches, and the permute pass stored at 2.8 TB/s that way.
-__device__ __forceinline__ void wave_stage(uint4* st, uint32_t lane, const Fe& v) {
-  st[2 * lane] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
-  st[2 * lane + 1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-__device__ __forceinline__ void wave_unstage_done() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-// elements 0 .. n - 1 of the staged 64 to dst (contiguous)
-__device__ __forceinline__ void wave_store_rows(uint64_t* dst, uint4* st, uint32_t lane, const Fe& v,
-                                                uint32_t n) {
-  wave_stage(st, lane, v);
-  const uint4 x = st[lane], y = st[64 + lane];
-  wave_unstage_done();
-  uint4* d = reinterpret_cast<uint4*>(dst);
-#if B2F_LK_NT & 1
-  if ((lane >> 1) < n) nt_store(d + lane, x);
-  if (32u + (lane >> 1) < n) nt_store(d + 64 + lane, y);
-#else
-  if ((lane >> 1) < n) d[lane] = x;
-  if (32u + (lane >> 1) < n) d[64 + lane] = y;
-#endif
-}
-// the staged 64 rows (a 64-row aligned group) to their gp::slot_of slots: 16 runs of 4
-// elements (128 bytes) 512 bytes apart, 8 lanes per run
-__device__ __forceinline__ void wave_store_slots(Fe* slots_base, uint4* st, uint32_t lane, const Fe& v) {
-  wave_stage(st, lane, v);
-  const uint32_t c = lane & 7u, e = c >> 1, h = c & 1u, r = lane >> 3;
-  const uint4 x = st[2 * (16 * e + r) + h], y = st[2 * (16 * e + r + 8) + h];
-  wave_unstage_done();
-  uint4* d = reinterpret_cast<uint4*>(slots_base);  // element (j * 16 + e), half h
-#if B2F_LK_NT & 2
-  nt_store(d + 2 * (r * 16 + e) + h, x);
-  nt_store(d + 2 * ((r + 8) * 16 + e) + h, y);
-#else
-  d[2 * (r * 16 + e) + h] = x;
-  d[2 * ((r + 8) * 16 + e) + h] = y;
-#endif
-}
-
 // The four columns and the grand product's factors, a lane per row (grid-stride over 64-row
 // groups): A = Tx[x], S = Tx[p] (row 0's value past the table), A' = Ts[r], S' = Ts[r'] from
 // lk_rows_kernel.
@@ -570,20 +521,20 @@ __global__ __launch_bounds__(256) void lk_permute_kernel(
     const Fe sp = Ts[r.y];
 #endif
     if (!(B2F_LK_ABL & 4)) {
-      wave_store_rows(o + 4 * base, st, lane, out_form<F>(a, mont), nv);
-      wave_store_rows(o + (out_rows + base) * 4, st, lane, out_form<F>(sv, mont), nv);
-      wave_store_rows(o + (2 * out_rows + base) * 4, st, lane, out_form<F>(ap, mont), nv);
-      wave_store_rows(o + (3 * out_rows + base) * 4, st, lane, out_form<F>(sp, mont), nv);
+      gp::wave_store_rows<B2F_LK_NT & 1>(o + 4 * base, st, lane, out_form<F>(a, mont), nv);
+      gp::wave_store_rows<B2F_LK_NT & 1>(o + (out_rows + base) * 4, st, lane, out_form<F>(sv, mont), nv);
+      gp::wave_store_rows<B2F_LK_NT & 1>(o + (2 * out_rows + base) * 4, st, lane, out_form<F>(ap, mont), nv);
+      gp::wave_store_rows<B2F_LK_NT & 1>(o + (3 * out_rows + base) * 4, st, lane, out_form<F>(sp, mont), nv);
     }
     // the grand product's factors (A + beta)(S + gamma) / ((A' + beta)(S' + gamma)); rows past
     // `usable` land in slots of the last tile that the grand product never reads
     const uint64_t sb = (base / (gp::ZC * gp::ZC)) * (gp::ZC * gp::ZC) + (base / gp::ZC) % gp::ZC;
     if (B2F_LK_ABL & 2) {
-      wave_store_slots(nm + sb, st, lane, field::add<F>(field::add<F>(a, beta), field::add<F>(sv, gamma)));
-      wave_store_slots(dn + sb, st, lane, field::add<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma)));
+      gp::wave_store_slots<(B2F_LK_NT >> 1) & 1>(nm + sb, st, lane, field::add<F>(field::add<F>(a, beta), field::add<F>(sv, gamma)));
+      gp::wave_store_slots<(B2F_LK_NT >> 1) & 1>(dn + sb, st, lane, field::add<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma)));
     } else {
-      wave_store_slots(nm + sb, st, lane, field::mul<F>(field::add<F>(a, beta), field::add<F>(sv, gamma)));
-      wave_store_slots(dn + sb, st, lane, field::mul<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma)));
+      gp::wave_store_slots<(B2F_LK_NT >> 1) & 1>(nm + sb, st, lane, field::mul<F>(field::add<F>(a, beta), field::add<F>(sv, gamma)));
+      gp::wave_store_slots<(B2F_LK_NT >> 1) & 1>(dn + sb, st, lane, field::mul<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma)));
     }
   }
 }

@@ -94,6 +94,15 @@ struct Inst {
   uint32_t n;
 };
 
+// the instance holding row r of a wave whose first row is `base` (wave-uniform: one search per
+// wave, scalar loads), then a lane's forward steps past the instance starts up to its row (an
+// instance has at least 228 rows, so a 64-row wave crosses at most one start)
+__device__ __forceinline__ uint32_t inst_of_wave(const Inst& I, uint64_t base, uint64_t r) {
+  uint32_t ii = __builtin_amdgcn_readfirstlane(inst_of(I.start, I.n, base));
+  while (ii < I.n && I.start[ii + 1] <= r) ii++;
+  return ii;
+}
+
 // mapping of cell (j, r) -> circuit (c', r')
 __device__ __forceinline__ void mapped(const Inst& I, const uint32_t* __restrict__ pool, uint32_t ii,
                                        uint32_t j, uint64_t r, uint32_t& c2, uint64_t& r2) {
@@ -114,25 +123,34 @@ __device__ __forceinline__ Fe dw(const Fe* __restrict__ T, const Fe* __restrict_
   return field::mul<F>(T[c * LO + (uint32_t)(r & (LO - 1))], OH[r >> 10]);
 }
 
-// sigma_j(w^r) for every row r < 2^k (keygen: the permutation polynomials' values)
+// sigma_j(w^r) for every row r < 2^k (keygen: the permutation polynomials' values); a wave per
+// 64 rows, each column's 64 values stored through LDS as 1 KiB runs (gp::wave_store_rows)
 template <class F>
 __global__ __launch_bounds__(256) void pm_sigma_kernel(Inst I, const uint32_t* __restrict__ pool,
                                                        uint64_t n_rows, const Fe* __restrict__ OL,
                                                        const Fe* __restrict__ OH, bool mont,
                                                        uint64_t* __restrict__ out, uint64_t out_rows) {
-  const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= n_rows) return;
-  const uint32_t ii = inst_of(I.start, I.n, r);
+  __shared__ uint4 stage[4][128];
+  const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t base = (uint64_t)blockIdx.x * 256 + 64 * wv;
+  if (base >= n_rows) return;
+  const uint64_t r = base + lane;
+  const uint32_t nv = (uint32_t)(n_rows - base < 64 ? n_rows - base : 64);
+  const uint64_t rr = r < n_rows ? r : base;
+  const uint32_t ii = inst_of_wave(I, base, rr);
 #pragma unroll 1
   for (uint32_t j = 0; j < NCOL; j++) {
     uint32_t c2;
     uint64_t r2;
-    mapped(I, pool, ii, j, r, c2, r2);
-    field::store(out + ((uint64_t)j * out_rows + r) * 4, gp::out_form<F>(dw<F>(OL, OH, c2, r2), mont));
+    mapped(I, pool, ii, j, rr, c2, r2);
+    gp::wave_store_rows<true>(out + ((uint64_t)j * out_rows + base) * 4, stage[wv], lane,
+                              gp::out_form<F>(dw<F>(OL, OH, c2, r2), mont), nv);
   }
 }
 
-// num/den of the columns [j0, j1) for rows r < usable
+// num/den of every column set for rows r < usable: a wave per 64 rows (the instance lookup and
+// the cell loads shared by the sets), the factors stored through LDS to their slots
+// (gp::wave_store_slots, non-temporal)
 template <class F>
 __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* __restrict__ pool,
                                                         const uint32_t* __restrict__ adv,
@@ -141,14 +159,18 @@ __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* 
                                                         const Fe* __restrict__ BL,
                                                         const Fe* __restrict__ OH, const Fe* __restrict__ G,
                                                         Fe* __restrict__ num, Fe* __restrict__ den) {
-  const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= usable) return;
+  __shared__ uint4 stage[4][128];
+  const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t base = (uint64_t)blockIdx.x * 256 + 64 * wv;
+  if (base >= usable) return;
+  const uint64_t r0 = base + lane;
+  const uint64_t r = r0 < usable ? r0 : base;  // lanes past the end repeat row base (slots unused)
   const uint32_t set = blockIdx.y;  // column set: columns [j0, j1)
   const uint32_t j0 = set * chunk_len, j1 = j0 + chunk_len < (uint32_t)NCOL ? j0 + chunk_len : NCOL;
   num += (uint64_t)set * gp::elems(usable);
   den += (uint64_t)set * gp::elems(usable);
   const Fe gamma = G[0];
-  const uint32_t ii = inst_of(I.start, I.n, r);
+  const uint32_t ii = inst_of_wave(I, base, r);
   const uint64_t used = I.start[I.n];
   Fe n, d;  // the first column's factors, then one product per further column
 #pragma unroll 1
@@ -165,9 +187,9 @@ __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* 
     n = j == j0 ? fn : field::mul<F>(n, fn);
     d = j == j0 ? fd : field::mul<F>(d, fd);
   }
-  const uint64_t sl = gp::slot_of(r, gp::n_chunks(usable));  // chunk-interleaved (b2f_gprod.h)
-  num[sl] = n;
-  den[sl] = d;
+  const uint64_t sb = gp::slot_base64(base);
+  gp::wave_store_slots<true>(num + sb, stage[wv], lane, n);
+  gp::wave_store_slots<true>(den + sb, stage[wv], lane, d);
 }
 
 struct Carve {
