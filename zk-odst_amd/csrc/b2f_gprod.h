@@ -313,6 +313,10 @@ __global__ __launch_bounds__(DOWN_T) void gp_block_down(uint64_t nq, Fe* __restr
 // 64 chunks so that every 8 lanes write one 128-byte run of rows (a lane storing its own rows
 // straight away wrote 64 lines 512 bytes apart per store instruction).
 constexpr int GW_ROWS = 4;
+#ifndef B2F_GW_NT
+#define B2F_GW_NT 1  // z stores non-temporal (the call's output, not re-read)
+#endif
+constexpr bool GW_NT = B2F_GW_NT != 0;
 static_assert(ZC % GW_ROWS == 0, "whole row groups per chunk");
 template <class F>
 __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint64_t* __restrict__ z_base,
@@ -322,7 +326,9 @@ __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint
                                                 const Fe* __restrict__ seed,
                                                 const Fe* __restrict__ post,
                                                 const Fe* __restrict__ dinv) {
-  __shared__ uint4 stage[4][64][GW_ROWS][2];
+  // a lane's GW_ROWS x 2 chunks padded to 9 (144 bytes): lanes 128 bytes apart hit the same
+  // banks in pairs (4-way conflicts on the staging writes, 83 % of the LDS cycles)
+  __shared__ uint4 stage[4][64][GW_ROWS * 2 + 1];
   const uint32_t c = blockIdx.y, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint64_t nq = n_chunks(usable);
   const uint64_t q0w = (uint64_t)blockIdx.x * 256 + 64 * wv;  // the wave's first chunk
@@ -347,8 +353,8 @@ __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint
     if (p < e) {
       const uint64_t sl = slot_of(p, nq);
       const Fe z = out_form<F>(field::mul<F>(nm[sl], k), mont);
-      stage[wv][lane][j % GW_ROWS][0] = make_uint4(z.w[0], z.w[1], z.w[2], z.w[3]);
-      stage[wv][lane][j % GW_ROWS][1] = make_uint4(z.w[4], z.w[5], z.w[6], z.w[7]);
+      stage[wv][lane][2 * (j % GW_ROWS)] = make_uint4(z.w[0], z.w[1], z.w[2], z.w[3]);
+      stage[wv][lane][2 * (j % GW_ROWS) + 1] = make_uint4(z.w[4], z.w[5], z.w[6], z.w[7]);
       if (j > 0) k = field::mul<F>(k, dn[sl]);
     }
     if (j % GW_ROWS == 0) {  // rows b + j + 1 .. b + j + GW_ROWS of the wave's 64 chunks
@@ -359,8 +365,8 @@ __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint
         const uint32_t u = 64u * i + lane, ch = u / (2 * GW_ROWS), rr = (u >> 1) % GW_ROWS, h = u & 1u;
         const uint64_t cq = q0w + ch, pr = cq * ZC + (uint64_t)j + rr;  // the row p whose z[p + 1] this is
         if (cq < nq && pr < usable && pr < cq * ZC + ZC) {
-          const uint4 v = stage[wv][ch][rr][h];
-          *reinterpret_cast<uint4*>(zcol + 4 * (pr + 1) + 2 * h) = v;
+          const uint4 v = stage[wv][ch][2 * rr + h];
+          put16<GW_NT>(reinterpret_cast<uint4*>(zcol + 4 * (pr + 1) + 2 * h), v);
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

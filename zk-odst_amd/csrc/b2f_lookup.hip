@@ -17,17 +17,10 @@
 //   scan:    in rank order, run starts pos[r] (exclusive prefix of counts), D[r] (runs up to
 //            and including r) and LP[r] (exclusive prefix of leftover table multiplicities), 16
 //            workgroups per circuit (part totals, then each part's scan);
-//            The scan also scatters two mark arrays (cleared by the count pass): srk[pos[r]] =
-//            r + 1 at every run start, and lrk[L - LP[r] - m_r] = 2^16 - r at the first repeated
-//            row index j that takes a leftover of rank r (m_r leftovers); both mark sequences
-//            increase along their index, so a running maximum recovers the rank at any index;
-//   permute: row p of A' is Ts[r] for the run r holding p; a run start gets S'[p] = Ts[r];
-//            the j-th repeated row gets leftover item L - 1 - j (halo2 hands leftovers out in
-//            ascending order, each to the last open repeated row). A wave walks 1,024
-//            consecutive rows 64 at a time: r is the running maximum of srk (a wave max-scan
-//            carried from the previous 64 rows), j counts the repeated rows (ballot), and the
-//            leftover rank of j is the running maximum of lrk; two binary searches of pos / LP
-//            per wave give the carries at its first row;
+//   permute: row p of A' is Ts[r] for the run r holding p (binary search of pos); a run
+//            start gets S'[p] = Ts[r]; the j-th repeated row gets leftover item L - 1 - j
+//            (halo2 hands leftovers out in ascending order, each to the last open repeated
+//            row), found by binary search of LP;
 //   z:       the permute pass also writes each row's factors num = (A + beta)(S + gamma) and
 //            den = (A' + beta)(S' + gamma); the grand product over them (b2f_gprod.h: one
 //            inversion per circuit, 4 products per row) writes the z column.
@@ -150,27 +143,12 @@ __device__ __forceinline__ Circ circ(const uint64_t* row_begin, uint64_t total_r
 // binned by their low 16 bits regardless.
 constexpr int CNT_SPLIT = 4, CNT_BINS = TROWS / CNT_SPLIT, CNT_THREADS = 1024, CNT_UNROLL = 8;
 static_assert(CNT_UNROLL % CNT_SPLIT == 0, "every workgroup checks one block per CNT_SPLIT blocks");
-// Mark arrays (srk, lrk) hold mark_stride(usable) words per circuit, a multiple of 64 so every
-// circuit's slice is 256-byte aligned; the count pass clears them (a quarter per workgroup).
-__host__ __device__ inline uint64_t mark_stride(uint64_t usable) { return (usable + 63) & ~63ull; }
-
 __global__ __launch_bounds__(CNT_THREADS) void lk_count_kernel(
     const uint32_t* __restrict__ adv, uint64_t total_rows, const uint64_t* __restrict__ row_begin,
-    uint32_t c0, uint64_t usable, uint32_t* __restrict__ count, uint64_t* __restrict__ first_bad,
-    uint32_t* __restrict__ srk, uint32_t* __restrict__ lrk) {
+    uint32_t c0, uint64_t usable, uint32_t* __restrict__ count, uint64_t* __restrict__ first_bad) {
   __shared__ uint32_t bins[CNT_BINS];
   const uint32_t b = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
   const Circ k = circ(row_begin, total_rows, usable, c0 + c);
-  {
-    const uint64_t ms = mark_stride(usable), q = ms / 4 / CNT_SPLIT;  // uint4 per workgroup
-    uint4* s4 = reinterpret_cast<uint4*>(srk + (uint64_t)c * ms) + (uint64_t)b * q;
-    uint4* l4 = reinterpret_cast<uint4*>(lrk + (uint64_t)c * ms) + (uint64_t)b * q;
-    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-    for (uint64_t i = t; i < q; i += CNT_THREADS) {
-      s4[i] = z;
-      l4[i] = z;
-    }
-  }
   for (uint32_t i = t; i < (uint32_t)CNT_BINS; i += CNT_THREADS) bins[i] = 0;
   __syncthreads();
   if (b == 0 && t == 0 && usable > k.n_in) atomicAdd(&bins[0], (uint32_t)(usable - k.n_in));  // zero rows
@@ -271,25 +249,18 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
                                                             const uint32_t* __restrict__ count,
                                                             uint64_t usable, const uint32_t* __restrict__ part,
                                                             uint32_t* __restrict__ pos, uint32_t* __restrict__ dcnt,
-                                                            uint32_t* __restrict__ lp, uint32_t* __restrict__ samp,
-                                                            uint32_t* __restrict__ srk, uint32_t* __restrict__ lrk) {
+                                                            uint32_t* __restrict__ lp, uint32_t* __restrict__ samp) {
   const uint32_t pt = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
   const uint32_t mult0 = (uint32_t)(usable - TROWS + 1);
   const uint32_t r0 = (pt * SC_THREADS + t) * SC_PER;
   const RankRun R = rank_run(perm, count + (uint64_t)c * TROWS, r0, mult0);
-  uint32_t bc = 0, bd = 0, bl = 0, runs = 0;  // totals of the parts before this one; all runs
-  for (uint32_t q = 0; q < (uint32_t)SC_PARTS; q++) {
+  uint32_t bc = 0, bd = 0, bl = 0;  // totals of the parts before this one
+  for (uint32_t q = 0; q < pt; q++) {
     const uint32_t* pq = part + ((uint64_t)c * SC_PARTS + q) * 3;
-    if (q < pt) {
-      bc += pq[0];
-      bd += pq[1];
-      bl += pq[2];
-    }
-    runs += pq[1];
+    bc += pq[0];
+    bd += pq[1];
+    bl += pq[2];
   }
-  const uint32_t n_left = (uint32_t)usable - runs;  // repeated rows = leftover table items
-  uint32_t* SR = srk + (uint64_t)c * mark_stride(usable);
-  uint32_t* LR = lrk + (uint64_t)c * mark_stride(usable);
   __shared__ uint32_t s[3][SC_THREADS];
   s[0][t] = R.sc;
   s[1][t] = R.sd;
@@ -323,10 +294,8 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
     uint32_t pq[4], dq[4], lq[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const uint32_t n = R.nv[4 * i + j], r = r0 + 4 * i + j;
-      const uint32_t m = (4 * i + j == R.iz ? mult0 : 1u) - (n ? 1u : 0u);  // leftovers of r
-      if (n) SR[ec] = r + 1u;                  // run start
-      if (m) LR[n_left - el - m] = TROWS - r;  // first repeated row taking a leftover of r
+      const uint32_t n = R.nv[4 * i + j];
+      const uint32_t m = (4 * i + j == R.iz ? mult0 : 1u) - (n ? 1u : 0u);  // leftovers
       pq[j] = ec;
       ed += n ? 1u : 0u;
       dq[j] = ed;
@@ -360,115 +329,29 @@ __device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, cons
   return 16 * lo + n;
 }
 
-// inclusive running maximum over the wave's 64 lanes
-__device__ __forceinline__ uint32_t wave_max_scan(uint32_t v) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(v, d, 64);  // a lane below d gets its own value: harmless
-    v = o > v ? o : v;
-  }
-  return v;
-}
-
-// Rows of a circuit -> (rank of A'[p], rank of S'[p]) into rr[p], a wave per PW_ROWS consecutive
-// rows, 64 at a time: r is the running maximum of srk (a wave max-scan carried from the previous
-// 64 rows), repeated rows are counted by ballot, and the leftover rank of repeated row j is the
-// running maximum of lrk. Two binary searches of pos / LP per wave give the carries at its first
-// row; the wave's srk values and its window of lrk (at most PW_ROWS repeated rows) are loaded up
-// front, so the 64-row steps depend on each other only through LDS and the scans. Integer work
-// only: it runs at full occupancy and leaves the field work to lk_permute_kernel.
-constexpr uint32_t PW_ROWS = 1024, PW_IT = PW_ROWS / 64;
-__global__ __launch_bounds__(256) void lk_rows_kernel(uint64_t usable, const uint32_t* __restrict__ pos,
-                                                      const uint32_t* __restrict__ dcnt,
-                                                      const uint32_t* __restrict__ lp,
-                                                      const uint32_t* __restrict__ samp,
-                                                      const uint32_t* __restrict__ srk,
-                                                      const uint32_t* __restrict__ lrk,
-                                                      uint2* __restrict__ rr) {
-  const uint32_t c = blockIdx.y, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t* P = pos + (uint64_t)c * TROWS;
-  const uint32_t* D = dcnt + (uint64_t)c * TROWS;
-  const uint32_t* L = lp + (uint64_t)c * TROWS;
-  const uint64_t ms = mark_stride(usable);
-  const uint32_t* SR = srk + (uint64_t)c * ms;
-  const uint32_t* LR = lrk + (uint64_t)c * ms;
-  uint2* RR = rr + (uint64_t)c * ms;
-  const uint32_t n_left = (uint32_t)usable - D[TROWS - 1];
-  __shared__ uint32_t sP[SAMPLE], sL[SAMPLE];
-  __shared__ uint32_t win[4][PW_ROWS];  // each wave's window of lrk
-  {
-    const uint4* sa = reinterpret_cast<const uint4*>(samp + (uint64_t)c * 2 * SAMPLE);
-    uint4* sp4 = reinterpret_cast<uint4*>(sP);
-    uint4* sl4 = reinterpret_cast<uint4*>(sL);
-    for (uint32_t i = threadIdx.x; i < (uint32_t)SAMPLE / 4; i += 256) {
-      sp4[i] = sa[i];
-      sl4[i] = sa[SAMPLE / 4 + i];
-    }
-  }
-  __syncthreads();
-  const uint64_t b0 = ((uint64_t)blockIdx.x * 4 + wv) * PW_ROWS;
-  if (b0 >= usable) return;
-  const uint32_t nrows = (uint32_t)(b0 + PW_ROWS < usable ? PW_ROWS : usable - b0);
-  // carries at the wave's first row: the run holding b0 (as its mark r + 1), the repeated rows
-  // before b0 (jb) and the mark of the leftover rank that repeated row jb takes
-  const uint32_t r0 = last_le(P, sP, (uint32_t)b0);
-  uint32_t rcar = r0 + 1u;
-  const uint32_t j0 = (uint32_t)b0 - D[r0] + (P[r0] == (uint32_t)b0 ? 1u : 0u);
-  uint32_t lcar = j0 < n_left ? (uint32_t)TROWS - last_le(L, sL, n_left - 1u - j0) : 0u;
-  uint32_t sm[PW_IT];
-#pragma unroll
-  for (uint32_t i = 0; i < PW_IT; i++) {
-    const uint32_t q = 64u * i + lane;
-    sm[i] = q < nrows ? SR[b0 + q] : 0u;
-    win[wv][q] = j0 + q < n_left ? LR[j0 + q] : 0u;
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  uint32_t jo = 0;  // repeated rows of this wave so far (window offset)
-#pragma unroll
-  for (uint32_t i = 0; i < PW_IT; i++) {
-    const uint32_t q = 64u * i + lane;
-    const uint32_t m = sm[i];
-    uint32_t rv = wave_max_scan(m);
-    rv = rv > rcar ? rv : rcar;  // the run holding row b0 + q, as r + 1
-    rcar = __builtin_amdgcn_readlane(rv, 63);
-    const bool rep = q < nrows && m == 0;
-    const uint64_t bal = __ballot(rep);
-    const uint32_t kr = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-    const uint32_t nrep = (uint32_t)__popcll(bal);
-    uint32_t lv = wave_max_scan(jo + lane < PW_ROWS ? win[wv][jo + lane] : 0u);
-    lv = lv > lcar ? lv : lcar;  // lane i: the leftover mark of repeated row j0 + jo + i
-    const uint32_t lm = __shfl(lv, (int)kr, 64);
-    if (nrep) {
-      lcar = __builtin_amdgcn_readlane(lv, nrep - 1u);
-      jo += nrep;
-    }
-    if (q < nrows) RR[b0 + q] = make_uint2(rv - 1u, rep ? (uint32_t)TROWS - lm : rv - 1u);
-  }
-}
-
 #ifndef B2F_LK_NT
-#define B2F_LK_NT 2  // non-temporal stores: 1 the columns, 2 the factors (3 both). The factors
-                     // non-temporal: permute pass 552 -> 358 us, the columns too: 546 (alone)
-#endif
-#ifndef B2F_LK_SEARCH
-#define B2F_LK_SEARCH 0
+#define B2F_LK_NT 3  // non-temporal stores: 1 the columns, 2 the factors, 3 both (permute pass
+                     // 552 us write-back, 546 columns only, 358 both: the write-back lines
+                     // evicted the gathered tables)
 #endif
 // The four columns and the grand product's factors, a lane per row (grid-stride over 64-row
-// groups): A = Tx[x], S = Tx[p] (row 0's value past the table), A' = Ts[r], S' = Ts[r'] from
-// lk_rows_kernel.
+// groups): A = Tx[x], S = Tx[p] (row 0's value past the table), A' = Ts[r] for the run r holding
+// p (binary search of pos: the top 12 levels in the workgroup's LDS sample), S' = A' at a run
+// start, else leftover item L - 1 - j for the j-th repeated row (halo2 hands leftovers out in
+// ascending order, each to the last open repeated row), found by binary search of LP. Each
+// column's 64 values of a wave go out as 1 KiB non-temporal stores (gp::wave_store_rows), the
+// factors to their chunk-interleaved slots (gp::wave_store_slots). Measured the searches cost
+// about what a separate rank-expansion pass (run-start / leftover marks and wave max-scans)
+// did, so they stay: r04e, 1.319 vs 1.321-1.332 ms per call.
 template <class F>
 __global__ __launch_bounds__(256) void lk_permute_kernel(
     const uint32_t* __restrict__ adv, uint64_t total_rows, const uint64_t* __restrict__ row_begin,
     uint32_t c0, uint64_t usable, const Fe* __restrict__ Tx, const Fe* __restrict__ Ts,
-    const uint2* __restrict__ rr, bool mont, uint64_t* __restrict__ out, uint64_t out_rows, Chal ch,
-    Fe* __restrict__ num, Fe* __restrict__ den, const uint32_t* __restrict__ sr_pos,
-    const uint32_t* __restrict__ sr_dcnt, const uint32_t* __restrict__ sr_lp,
-    const uint32_t* __restrict__ samp) {
+    bool mont, uint64_t* __restrict__ out, uint64_t out_rows, Chal ch, Fe* __restrict__ num,
+    Fe* __restrict__ den, const uint32_t* __restrict__ pos, const uint32_t* __restrict__ dcnt,
+    const uint32_t* __restrict__ lp, const uint32_t* __restrict__ samp) {
   __shared__ uint4 stage[4][128];
   const uint32_t c = blockIdx.y, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-#if B2F_LK_SEARCH
   __shared__ uint32_t sP[SAMPLE], sL[SAMPLE];
   {
     const uint4* sa = reinterpret_cast<const uint4*>(samp + (uint64_t)c * 2 * SAMPLE);
@@ -480,14 +363,16 @@ __global__ __launch_bounds__(256) void lk_permute_kernel(
     }
   }
   __syncthreads();
-#endif
   uint4* st = stage[wv];
   const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
   const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
   Fe* nm = num + (uint64_t)c * gp::elems(usable);
   Fe* dn = den + (uint64_t)c * gp::elems(usable);
   const Circ k = circ(row_begin, total_rows, usable, c0 + c);
-  const uint2* RR = rr + (uint64_t)c * mark_stride(usable);
+  const uint32_t* P = pos + (uint64_t)c * TROWS;
+  const uint32_t* D = dcnt + (uint64_t)c * TROWS;
+  const uint32_t* L = lp + (uint64_t)c * TROWS;
+  const uint32_t n_left = (uint32_t)usable - D[TROWS - 1];  // repeated rows = leftover items
   uint64_t* o = out + (uint64_t)(c0 + c) * 5 * out_rows * 4;
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t base = (uint64_t)blockIdx.x * 256 + 64 * wv; base < usable; base += stride) {
@@ -495,19 +380,11 @@ __global__ __launch_bounds__(256) void lk_permute_kernel(
     const bool in = p < usable;
     const uint32_t nv = (uint32_t)(usable - base < 64 ? usable - base : 64);
     const uint32_t x = p < k.n_in ? (adv[total_rows + k.first + p] & 0xffffu) : 0u;
-#if B2F_LK_SEARCH  // diagnostics: per-row searches instead of lk_rows_kernel
-    uint2 r = make_uint2(0u, 0u);
+    uint2 r = make_uint2(0u, 0u);  // ranks of A'[p] and S'[p]
     if (in) {
-      const uint32_t* P = sr_pos + (uint64_t)c * TROWS;
-      const uint32_t* D = sr_dcnt + (uint64_t)c * TROWS;
-      const uint32_t* L = sr_lp + (uint64_t)c * TROWS;
-      const uint32_t n_left = (uint32_t)usable - D[TROWS - 1];
       r.x = last_le(P, sP, (uint32_t)p);
       r.y = P[r.x] == (uint32_t)p ? r.x : last_le(L, sL, n_left - 1u - ((uint32_t)p - D[r.x]));
     }
-#else
-    const uint2 r = in ? RR[p] : make_uint2(0u, 0u);
-#endif
 #ifndef B2F_LK_ABL
 #define B2F_LK_ABL 0  // diagnostics (variant builds only): 1 no gathers, 2 no products, 4 no column stores
 #endif
@@ -553,9 +430,6 @@ struct Carve {
   uint32_t* dcnt;
   uint32_t* lp;
   uint32_t* samp;  // group x 2 x SAMPLE
-  uint32_t* srk;   // group x mark_stride(usable): run-start marks
-  uint32_t* lrk;   // group x mark_stride(usable): leftover marks
-  uint2* rr;       // group x mark_stride(usable): (rank of A', rank of S') per row
   uint32_t* part;  // group x SC_PARTS x 3 (rank-scan part totals)
   Fe* num;  // group x usable
   Fe* den;
@@ -592,9 +466,6 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.dcnt = (uint32_t*)take(4ull * TROWS * group);
   k.lp = (uint32_t*)take(4ull * TROWS * group);
   k.samp = (uint32_t*)take(8ull * SAMPLE * group);
-  k.srk = (uint32_t*)take(4ull * mark_stride(usable) * group);
-  k.lrk = (uint32_t*)take(4ull * mark_stride(usable) * group);
-  k.rr = (uint2*)take(8ull * mark_stride(usable) * group);
   k.part = (uint32_t*)take(12ull * SC_PARTS * group);
   k.num = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);  // chunk-interleaved (b2f_gprod.h)
   k.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);
@@ -629,18 +500,15 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   for (uint32_t c0 = 0; c0 < n_circuits; c0 += group) {
     const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
     hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
-                       total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad, k.srk, k.lrk);
+                       total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
     hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
     hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
-                       k.part, k.pos, k.dcnt, k.lp, k.samp, k.srk, k.lrk);
-    if (!B2F_LK_SEARCH)
-      hipLaunchKernelGGL(lk_rows_kernel, dim3((uint32_t)((usable_rows + 4 * PW_ROWS - 1) / (4 * PW_ROWS)), g),
-                       dim3(256), 0, s, usable_rows, k.pos, k.dcnt, k.lp, k.samp, k.srk, k.lrk, k.rr);
+                       k.part, k.pos, k.dcnt, k.lp, k.samp);
     // permute: ~4096 rows per workgroup
     const uint32_t px = (uint32_t)((usable_rows + 4095) / 4096);
     hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
-                       d_row_begin, c0, usable_rows, k.Tx, k.Ts, k.rr, mont, d_out, out_rows, ch,
-                       k.num, k.den, k.pos, k.dcnt, k.lp, k.samp);
+                       d_row_begin, c0, usable_rows, k.Tx, k.Ts, mont, d_out, out_rows, ch, k.num,
+                       k.den, k.pos, k.dcnt, k.lp, k.samp);
     e = gp::run<F>(g, usable_rows, mont, d_out + ((uint64_t)c0 * 5 + 4) * out_rows * 4,
                    5 * out_rows * 4, k.num, k.den, k.zs, nullptr, nullptr, s, nullptr, sticky, side);
     if (e != hipSuccess) return e;
