@@ -173,18 +173,26 @@ def gather_trace(adv_local, fixed_local, rows_per_rank, dist, torch, group=None,
     if not (coalesce and _gather_coalesced(out, cols, dist, group, dev)):
         for c in range(11):
             dist.all_gather_into_tensor(out[c], cols[c], group=group)
-    # compaction of the padded windows (no-op when every shard fills its window)
-    stage = None
+    compact_windows(out, rows_per_rank, w, torch)
+    return out[:10], out[10]
+
+
+def compact_windows(out, rows_per_rank, w, torch, stage=None):
+    """In place: the padded windows of `out` [cols, world * w] (rank k's rows at k * w) moved
+    back to back from row 0 in rank order through a staging buffer of at most STAGE_ROWS rows
+    (allocated here unless given), zeros after. Rank k's rows move down, chunk by chunk in
+    increasing row order, so a staged chunk never overwrites rows still to move. No-op (no
+    staging) when every shard fills its window."""
     dst = 0
     for k, r in enumerate(rows_per_rank):
         src = k * w
         if src != dst and r:
             if stage is None:
-                stage = torch.empty((11, min(STAGE_ROWS, w)), dtype=out.dtype, device=dev)
+                stage = torch.empty((out.shape[0], min(STAGE_ROWS, w)), dtype=out.dtype,
+                                    device=out.device)
             for o in range(0, r, stage.shape[1]):
                 t = min(stage.shape[1], r - o)
                 stage[:, :t].copy_(out[:, src + o: src + o + t])
                 out[:, dst + o: dst + o + t].copy_(stage[:, :t])
         dst += r
     out[:, dst:].zero_()
-    return out[:10], out[10]

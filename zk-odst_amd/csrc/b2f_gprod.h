@@ -314,7 +314,7 @@ __global__ __launch_bounds__(DOWN_T) void gp_block_down(uint64_t nq, Fe* __restr
 // straight away wrote 64 lines 512 bytes apart per store instruction).
 constexpr int GW_ROWS = 4;
 #ifndef B2F_GW_NT
-#define B2F_GW_NT 1  // z stores non-temporal (the call's output, not re-read)
+#define B2F_GW_NT 0  // z stores non-temporal: measured slower (gp_write 263 -> 363 us Pallas, 389 -> 527 BN254)
 #endif
 constexpr bool GW_NT = B2F_GW_NT != 0;
 static_assert(ZC % GW_ROWS == 0, "whole row groups per chunk");
