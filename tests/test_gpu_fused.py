@@ -362,3 +362,80 @@ def test_2p18x12_fused_equals_split_past_2p30(engine, orc):
         assert got == want, (i, c, r, b, got, want)
     del adv, fx, h
     torch.cuda.empty_cache()
+
+
+def test_fused_long_instance_is_segmented(engine, orc):
+    """an instance far longer than the rest (10^4 rounds, 20,000 half-round tiles) in
+    a batch of 12-round ones. The half-round launch walks it in segments of SEG_HR half-rounds,
+    the later ones from recorded states on whichever waves are free, so it no longer runs at one
+    wave's speed: fused trace == split trace column by column, h' and verdict equal, oracle
+    samples at segment starts, and the pass takes a few ms (one wave alone took ~100 ms)."""
+    import time
+
+    import torch
+
+    import b2f
+
+    x = random_inputs(4096, (12,), 91)
+    x["rounds"][1777] = 10000
+    fused = _fused(engine, x)
+    split = b2f.DeviceBatch(x)
+    split.fill(engine)
+    split.evaluate(engine)
+    engine.sync(_stream())
+    for c in range(10):
+        assert torch.equal(fused.advice[c], split.advice[c]), "a_%d" % c
+    assert torch.equal(fused.fixed, split.fixed)
+    assert torch.equal(fused.h_out, split.h_out)
+    rep = fused.report_dict()
+    assert rep == split.report_dict() and rep["first_failure"] == NONE
+    # oracle on the long instance alone, compared at its segment starts (rows of half-rounds
+    # 24 m - 1 .. 24 m)
+    one = x[1777:1778].copy()
+    oadv, ofixed, oh, _ = orc.fill(_as_oracle(one, orc))
+    base = int(fused.offsets_host[1777])
+    adv = fused.advice[:, base: base + oadv.shape[1]].cpu().numpy().view(np.uint32)
+    for m in (1, 2, 417, 833):
+        lo = 164 + 208 * (24 * m - 1)
+        assert np.array_equal(adv[:, lo: lo + 416], oadv[:, lo: lo + 416]), m
+    assert np.array_equal(fused.host_h_out()[1777], oh[0])
+    # time: the pass with the long instance vs without it
+    s = _stream()
+    engine.set_timing(True)
+    for _ in range(3):
+        fused.fill_evaluate(engine, s)
+    t_long = engine.kernel_times()["fill_eval"][0] / 3
+    x2 = x.copy()
+    x2["rounds"][1777] = 12
+    b2 = b2f.DeviceBatch(x2)
+    b2.fill_evaluate(engine, s)
+    engine.sync(s)
+    engine.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        b2.fill_evaluate(engine, s)
+    t_base = engine.kernel_times()["fill_eval"][0] / 3
+    print("fused fill+eval: %.3f ms with the 10^4-round instance, %.3f ms without (%.1f s wall)"
+          % (t_long, t_base, time.perf_counter() - t0))
+    assert t_long < 30.0
+
+
+def test_fused_injection_at_segment_starts(engine, orc):
+    """Faults on both sides of the segment boundaries of 25-round instances (half-round 24 starts
+    a listed segment on another wave): fused verdict == b2f_eval_dev verdict == oracle."""
+    x = random_inputs(6, (25,), 92)
+    clean = _fused(engine, x)
+    off = clean.offsets_host
+    cases = 0
+    for i in (0, 3, 5):
+        b = int(off[i]) + 164 + 208 * 24  # first row of half-round 24
+        for r in (b - 29, b - 4, b - 1, b, b + 3, b + 51):
+            for col in (1, 3, 10):
+                batch = _fused(engine, x, inject=(r, col, 1 << (cases % 13)))
+                got = batch.report_dict()
+                batch.evaluate(engine)
+                engine.sync(_stream())
+                assert got == batch.report_dict(), (i, r, col)
+                adv, fixed = batch.host_trace()
+                assert got == orc.evaluate(adv, fixed, off), (i, r, col)
+                cases += 1

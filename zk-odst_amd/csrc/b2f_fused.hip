@@ -1068,7 +1068,8 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
                 uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
                 uint32_t* __restrict__ fixed, const TileDesc* __restrict__ desc,
                 b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
-                uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk) {
+                uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk,
+                const uint64_t* __restrict__ seg) {
   using namespace hr2;
   __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS];
   uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
@@ -1114,27 +1115,29 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       while (j < n && in[j].rounds == 0) j += W;
       return j < n ? (uint32_t)j : n;
     };
-    uint32_t inst;
-    {
-      const uint64_t f = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
-      inst = f < n ? (in[f].rounds ? (uint32_t)f : next_inst((uint32_t)f)) : n;
-    }
+    const uint64_t w0 = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
+    uint32_t inst = w0 < n ? (in[w0].rounds ? (uint32_t)w0 : next_inst((uint32_t)w0)) : n;
     uint64_t Pi = rec_word(inst);  // the current instance's record word
     // settled before the loop: otherwise the compiler cannot prove at the loop header that Pi is
     // never pending and waits for vmcnt(0) -- every store in flight -- at its first use
     asm volatile("" ::"v"(Pi));
     HCtx c;
-    uint32_t ninst = 0;
+    uint32_t ninst = 0, hr_end = 0;
+    uint64_t qs = w0;  // this wave's next entry of the segment list (after its instances)
+    bool fresh = true;
     c.hr = 0;
-    for (; inst < n;) {
+    for (;;) {
       tick(-1);
-      if (c.hr == 0) {  // an instance's first tile: its context, its record into IN, the initial
-                        // work vector (h, IV, IV ^ (t0, t1, fmask)) into OUT slot 0 in column-G order
+      if (fresh && inst < n) {  // an instance's first tile: its context, its record into IN, the
+                                // initial work vector (h, IV, IV ^ (t0, t1, fmask)) into OUT slot 0
+                                // in column-G order; its first SEG_HR half-rounds
         const uint64_t o = off[inst];
         c.inst = inst;
         c.rounds = in[inst].rounds;
         c.st = (uint32_t)((o - 20ull * inst) / 208);
         c.off = o;
+        c.hr = 0;
+        hr_end = 2 * c.rounds < SEG_HR ? 2 * c.rounds : SEG_HR;
         ninst = next_inst(inst);
         if (lane < 27) st64(aIN + 8 * lane, Pi);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1148,6 +1151,55 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
+        fresh = false;
+      } else if (fresh) {  // a later segment m of a long instance (the list, after the instances):
+                           // half-rounds h0 = m SEG_HR .. from the recorded states h0 - 1 and h0
+        if (qs >= seg[0]) break;
+        const uint64_t e = seg[1 + qs];
+        qs += W;
+        const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)(e >> 32));
+        const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)e);
+        const uint64_t o = off[i];
+        c.inst = i;
+        c.rounds = in[i].rounds;
+        c.st = (uint32_t)((o - 20ull * i) / 208);
+        c.off = o;
+        c.hr = m * SEG_HR;
+        hr_end = 2 * c.rounds < (m + 1) * SEG_HR ? 2 * c.rounds : (m + 1) * SEG_HR;
+        ninst = n;
+        const uint64_t* sp = rec + 16ull * ((uint64_t)c.st + c.hr);  // state at h0, natural order
+        const uint32_t ob0 = 128u * (c.hr & 1u);
+        const uint64_t rw = rec_word(i);
+        // OUT: the state at h0 in the previous half-round's G order (its G outputs as the walk
+        // would have left them); the lanes' words settle before the LDS writes
+        const uint32_t gs = (lane >> 2) & 3u, kk = lane & 3u;
+        const uint32_t gw = gidx_word(gs + 4 * ((c.hr - 1) & 1u));
+        const uint64_t vs = sp[(gw >> (8 * kk)) & 15u];
+        if (lane < 27) st64(aIN + 8 * lane, rw);
+        if (lane < 16) st64(Sb + 4 * H_OUT + ob0 + 8 * lane, vs);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {  // GP: the chain of half-round h0 - 1's G 3 (the tail lanes' quads)
+          const uint32_t hp = c.hr - 1, g3 = 3 + 4 * (hp & 1u);
+          const uint64_t* pp = rec + 16ull * ((uint64_t)c.st + hp);
+          const uint32_t gi = gidx_word(g3);
+          const uint64_t a = pp[gi & 15u], b = pp[(gi >> 8) & 15u], cc = pp[(gi >> 16) & 15u], d = pp[gi >> 24];
+          const uint8_t* sg = Sg + 16 * ((hp >> 1) % 10) + 2 * g3;
+          const uint64_t mx = INW[8 + sg[0]], my = INW[8 + sg[1]];
+          const uint64_t a1 = a + b + mx, d1 = rotr64(d ^ a1, 32), c1 = cc + d1, b1 = rotr64(b ^ c1, 24);
+          const uint64_t a2 = a1 + b1 + my, d2 = rotr64(d1 ^ a2, 16), c2 = c1 + d2;
+          const uint32_t gp = Sb + 4 * H_GP + ob0;
+          st128(gp, make_uint4(lo32(a), hi32(a), lo32(d), hi32(d)));
+          st128(gp + 16, make_uint4(lo32(cc), hi32(cc), lo32(b), hi32(b)));
+          st128(gp + 32, make_uint4(lo32(a1), hi32(a1), lo32(d1), hi32(d1)));
+          st128(gp + 48, make_uint4(lo32(c1), hi32(c1), lo32(b1), hi32(b1)));
+          st128(gp + 64, make_uint4(lo32(a2), hi32(a2), lo32(d2), hi32(d2)));
+          st128(gp + 80, make_uint4(lo32(c2), hi32(c2), lo32(mx), hi32(mx)));
+          st128(gp + 96, make_uint4(lo32(my), hi32(my), 0u, 0u));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        fresh = false;
       }
       c.row0 = c.off + INIT_ROWS + 208ull * c.hr;
       const uint32_t ob = 128u * (c.hr & 1u), nb = 128u - ob;  // this tile's OUT / GP slot, the next's
@@ -1382,10 +1434,10 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       asm volatile("" ::: "memory");
       __builtin_amdgcn_wave_barrier();
       tick(6);
-      if (c.hr + 1 < 2 * c.rounds) {
+      if (c.hr + 1 < hr_end) {
         c.hr++;
-      } else {
-        c.hr = 0;
+      } else {  // the unit (an instance's first segment, or a listed segment) is done
+        fresh = true;
         inst = ninst;
         Pi = Pn;
       }
@@ -2223,7 +2275,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                             uint32_t* d_fixed, void* scratch, uint64_t tiles,
                             b2f_eval_report* d_rep, const int* d_status, uint64_t inj_row,
                             uint32_t inj_col, uint32_t inj_mask, int mode, int cu_count,
-                            unsigned long long* clk, hipStream_t s) {
+                            unsigned long long* clk, const uint64_t* seg, hipStream_t s) {
   TileDesc* desc = reinterpret_cast<TileDesc*>(scratch);
   uint64_t* defer = reinterpret_cast<uint64_t*>(desc + tiles);
   uint32_t* redo = reinterpret_cast<uint32_t*>(defer + 1 + DEFER_CAP);
@@ -2280,7 +2332,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   case M:                                                                                          \
     hipLaunchKernelGGL(fused_hr_kernel<M>, dim3(grid), dim3(FW * WAVES), 0, s, d_in, n, d_off,     \
                        total_rows, rec, d_adv, d_fixed, desc, d_rep, d_status, inj, defer, DEFER_CAP, \
-                       clk);                                                                       \
+                       clk, seg);                                                                  \
     hipLaunchKernelGGL(fused_edge_kernel<M>, dim3(grid_e), dim3(FW * WAVES), 0, s, d_in, n, d_off, \
                        total_rows, rec, d_adv, d_fixed, redo, d_rep, d_status, inj, defer,         \
                        DEFER_CAP, clk);                                                            \

@@ -63,7 +63,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                             uint32_t* d_fixed, void* scratch, uint64_t tiles,
                             b2f_eval_report* d_rep, const int* d_status, uint64_t inj_row,
                             uint32_t inj_col, uint32_t inj_mask, int mode, int cu_count,
-                            unsigned long long* clk, hipStream_t s);  // b2f_fused.hip
+                            unsigned long long* clk, const uint64_t* seg, hipStream_t s);  // b2f_fused.hip
 }
 
 namespace {
@@ -106,7 +106,8 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
                                                       int* __restrict__ status,
                                                       int* __restrict__ sticky,
                                                       b2f_eval_report* __restrict__ rep,
-                                                      bool lite) {
+                                                      bool lite, uint64_t* __restrict__ seg,
+                                                      uint64_t seg_cap) {
   const uint32_t gt = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t i = gt >> 2, c = gt & 3u;  // the quad's four lanes share instance i
   if (i >= n) return;
@@ -154,8 +155,22 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
   // 2 rounds + 1
   uint32_t k = 0;
   const uint32_t keep = lite ? (rounds ? 2 * rounds - 1 : 0) : 0;
+  const uint32_t hr_all = 2 * rounds;
+  // lite: also the states before and at every later segment start m SEG_HR < 2 rounds (a
+  // segment's first tile starts from the one and recomputes the previous tile's tail from the
+  // other); the segments themselves go to the fused launch's list
+  auto keep_state = [&](uint32_t q) {
+    return q >= keep || (q % SEG_HR == 0 && q != 0 && q < hr_all) ||
+           ((q + 1) % SEG_HR == 0 && q + 1 < hr_all);
+  };
+  if (lite && seg && c == 0 && hr_all > SEG_HR) {
+    const uint64_t nseg = (hr_all - 1) / SEG_HR;  // segments m = 1 .. nseg
+    const uint64_t at = atomicAdd(reinterpret_cast<unsigned long long*>(seg), (unsigned long long)nseg);
+    for (uint64_t m = 1; m <= nseg; m++)
+      if (at + m - 1 < seg_cap) seg[1 + at + m - 1] = ((uint64_t)i << 32) | m;
+  }
   auto dump = [&](void) {
-    if (k++ < keep) {
+    if (!keep_state(k++)) {
       s += 16;
       return;
     }
@@ -777,6 +792,8 @@ struct b2f_ctx {
   int* d_status;       // [0] fill call, [1] eval call, [2] sticky (cleared by b2f_sync only)
   uint64_t* d_rec;     // half-round states
   uint64_t rec_cap;    // in states (16 x u64 each)
+  uint64_t* d_seg;     // the fused launch's segment list (count, entries: instance << 32 | m)
+  uint64_t seg_cap;    // in u64 words
   TileInfo* d_tiles;   // per-tile instance context
   uint64_t tiles_cap;
   int timing;
@@ -1073,6 +1090,7 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipFree(ctx->d_status);
   (void)hipFree(ctx->d_rec);
+  (void)hipFree(ctx->d_seg);
   (void)hipFree(ctx->d_tiles);
   (void)hipFree(ctx->d_clock);
   (void)hipFree(ctx->d_lk);
@@ -1151,9 +1169,23 @@ int fill_prologue(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const uint64_t*
   }
   uint32_t nn = (uint32_t)n;
   int tk = timed_begin(ctx, B2F_KERNEL_RECORD, s);
+  uint64_t* seg = nullptr;
+  if (lite) {  // the fused launch's segment list: count, then at most states / SEG_HR entries
+    const uint64_t cap = states / SEG_HR + 1;
+    if (cap + 1 > ctx->seg_cap) {
+      HIPCHK(ctx, hipStreamSynchronize(s));
+      if (ctx->d_seg) HIPCHK(ctx, hipFree(ctx->d_seg));
+      ctx->d_seg = nullptr;
+      ctx->seg_cap = 0;
+      HIPCHK(ctx, hipMalloc(&ctx->d_seg, (cap + 1) * sizeof(uint64_t)));
+      ctx->seg_cap = cap + 1;
+    }
+    seg = ctx->d_seg;
+    HIPCHK(ctx, hipMemsetAsync(seg, 0, sizeof(uint64_t), s));
+  }
   hipLaunchKernelGGL(record_kernel, dim3((uint32_t)((4ull * nn + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, d_in, nn,
                      d_offsets, total_rows, ctx->rec_cap, ctx->d_rec, d_h_out, ctx->d_status,
-                     ctx->d_status + 2, d_report, lite);
+                     ctx->d_status + 2, d_report, lite, seg, lite ? ctx->seg_cap - 1 : 0);
   HIPCHK(ctx, hipGetLastError());
   timed_end(ctx, tk, s);
   return B2F_OK;
@@ -1230,7 +1262,7 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
   HIPCHK(ctx, launch_fill_eval(d_in, (uint32_t)n, d_offsets, total_rows, ctx->d_rec, d_advice,
                                d_fixed, ctx->d_fz, tiles, d_report, ctx->d_status,
                                ctx->inj_row, ctx->inj_col, ctx->inj_mask, fmode,
-                               ctx->cu_count, ctx->d_clock, s));
+                               ctx->cu_count, ctx->d_clock, ctx->d_seg, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }

@@ -11,6 +11,11 @@ constexpr uint32_t INIT_ROWS = 164, ROUND_ROWS = 416, FINAL_ROWS = 64, G_ROWS = 
 constexpr uint32_t INIT_QUADS = INIT_ROWS / 4, ROUND_QUADS = ROUND_ROWS / 4;
 constexpr uint32_t G_QUADS = G_ROWS / 4, FINAL_QUADS = FINAL_ROWS / 4;
 constexpr uint32_t FIXED_ROWS = INIT_ROWS + FINAL_ROWS;  // R(0)
+// The fused half-round launch walks an instance's half-rounds on one wave in segments of at most
+// SEG_HR (12 rounds): an instance's first segment is dealt with the instance, the later ones of a
+// longer instance go to a list that every wave drains after its instances, each starting from
+// recorded states (the record kernel keeps the state before and at every segment start).
+constexpr uint32_t SEG_HR = 24;
 
 // columns
 enum : int { A0 = 0, A1, A2, A3, A4, A5, A6, A7, A8, A9 };
