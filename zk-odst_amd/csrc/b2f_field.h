@@ -87,12 +87,72 @@ __device__ __forceinline__ Fe reduce_once(const Fe& t) {
   return borrow ? t : d;
 }
 
-// Montgomery product a b / 2^256 mod p (a, b < p). The 32-bit sums that feed each
+// Montgomery product a b / 2^256 mod p (a, b < p), product scanning (Comba): column k of the
+// 512-bit sum of a_i b_j and m_i p_j (i + j = k; m_k chosen so column k < 8 ends in a zero word)
+// accumulates in a 64-bit VGPR pair by v_mad_u64_u32, whose carry out of the 64-bit add goes
+// straight into a third word by v_addc (acc_madd): two instructions per word product. The
+// constant words of p are SGPR operands and fold (pallas has three zero words). The compiler's
+// form of the operand-scanning CIOS (add-with-carry fed addends, kept below as mul_cios) took
+// about three instructions and a wait state per word product: tools/mulbench.hip, gfx950,
+// profiles/r04h_mulbench.txt: pallas 141-144 vs 111-113 G products/s, BN254 121-124 vs 104-105,
+// identical results on 4.2 M random products of each field.
+__device__ __forceinline__ void acc_madd(uint64_t& acc, uint32_t& ov, uint32_t x, uint32_t y) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(ov)
+      : "v"(x), "v"(y)
+      : "vcc");
+}
+__device__ __forceinline__ void acc_maddc(uint64_t& acc, uint32_t& ov, uint32_t x, uint32_t y) {  // y uniform
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(ov)
+      : "v"(x), "s"(y)
+      : "vcc");
+}
+template <class F>
+__device__ __forceinline__ Fe mul(const Fe& a, const Fe& b) {
+  uint32_t m[8], r[8];
+  uint64_t acc = 0;
+  uint32_t ov = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#pragma unroll
+    for (int i = 0; i < k; i++) {
+      acc_madd(acc, ov, a.w[i], b.w[k - i]);
+      if (F::P[k - i]) acc_maddc(acc, ov, m[i], F::P[k - i]);
+    }
+    acc_madd(acc, ov, a.w[k], b.w[0]);
+    m[k] = (uint32_t)acc * F::NP;
+    acc_maddc(acc, ov, m[k], F::P[0]);  // the low word is now zero
+    acc = (acc >> 32) | ((uint64_t)ov << 32);
+    ov = 0;
+  }
+#pragma unroll
+  for (int k = 8; k < 15; k++) {
+#pragma unroll
+    for (int i = k - 7; i < 8; i++) {
+      acc_madd(acc, ov, a.w[i], b.w[k - i]);
+      if (F::P[k - i]) acc_maddc(acc, ov, m[i], F::P[k - i]);
+    }
+    r[k - 8] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)ov << 32);
+    ov = 0;
+  }
+  r[7] = (uint32_t)acc;  // the result is < 2p < 2^256: nothing above this word
+  Fe o;
+#pragma unroll
+  for (int j = 0; j < 8; j++) o.w[j] = r[j];
+  return reduce_once<F>(o);
+}
+
+// The operand-scanning CIOS form the product had before (kept as the cross-check of mul in
+// tools/mulbench.hip). The 32-bit sums that feed each
 // v_mad_u64_u32 addend are formed with add-with-carry (the carry becomes the addend's high
 // word) instead of 64-bit adds of zero-extended words: 20 % fewer instructions, ~1.25x the
 // throughput on gfx950 (tools/mulbench.hip: 114 vs 90 G products/s chip-wide).
 template <class F>
-__device__ __forceinline__ Fe mul(const Fe& a, const Fe& b) {
+__device__ __forceinline__ Fe mul_cios(const Fe& a, const Fe& b) {
   uint32_t t[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) t[j] = 0;
