@@ -1062,6 +1062,18 @@ __device__ __forceinline__ uint32_t hr_fast_checks(const hr2::Lane& K, uint32_t 
   return acc;
 }
 
+#ifndef B2F_EDGE_SEPARATE
+#define B2F_EDGE_SEPARATE 0  // 1 (diagnostics): the edge tiles in their own launch after this one
+#endif
+template <int MODE>
+__device__ __forceinline__ void edge_walk(uint32_t* S, uint32_t lane, uint64_t t_first, uint64_t W,
+                                          const uint64_t* IV, const uint8_t* Sg, EvalAcc& A,
+                                          const b2f_input* __restrict__ in, uint32_t n,
+                                          const uint64_t* __restrict__ off, uint64_t total_rows,
+                                          const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
+                                          uint32_t* __restrict__ fixed, uint32_t* __restrict__ redo,
+                                          const Inject& inj, uint64_t* __restrict__ defer,
+                                          uint32_t defer_cap);
 template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES, B2F_FUSED_WAVES)
 fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
@@ -1069,7 +1081,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
                 uint32_t* __restrict__ fixed, const TileDesc* __restrict__ desc,
                 b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
                 uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk,
-                const uint64_t* __restrict__ seg) {
+                const uint64_t* __restrict__ seg, uint32_t* __restrict__ redo) {
   using namespace hr2;
   __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS];
   uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
@@ -1442,6 +1454,9 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
         Pi = Pn;
       }
     }
+    if (!B2F_EDGE_SEPARATE)  // then the edge tiles, in the wave's whole region
+      edge_walk<MODE>(L + H_WAVE + wv * HW_WORDS, lane, w0, W, IV, Sg, A, in, n, off, total_rows, rec,
+                      adv, fixed, redo, inj, defer, defer_cap);
   }
   if ((MODE & FZ_CLOCK) && lane == 0) {
 #pragma unroll
@@ -1547,6 +1562,7 @@ constexpr int E_LT = NSTAGE * STR_E;
 constexpr int E_PROD = E_LT + 64;
 constexpr int EW_WORDS = E_PROD + 32;
 static_assert(EW_WORDS >= WAVE_WORDS, "the exact edge path's carve fits");
+static_assert(EW_WORDS <= hr2::HW_WORDS, "the half-round launch's wave region holds an edge tile");
 constexpr int E_ACC = 0, E_IV = 24, E_SG = E_IV + 16, E_WAVE = E_SG + 40;
 constexpr int E_WORDS = E_WAVE + WAVES * EW_WORDS;
 static_assert(E_WAVE % 4 == 0 && EW_WORDS % 4 == 0 && E_PROD % 2 == 0, "aligned carve");
@@ -1679,34 +1695,24 @@ __device__ __forceinline__ uint32_t edge_fast_checks(const ELane& E) {
   return acc;
 }
 
-#ifndef B2F_EDGE_WAVES
-#define B2F_EDGE_WAVES 3  // waves per SIMD the edge kernel is compiled for (VGPR budget)
-#endif
+// The edge tiles t_first, t_first + W, ... of a batch (one per instance, then the zero rows past
+// the last instance) on this wave, staged in the wave region S (EW_WORDS words): the body of the
+// edge launch, and the last phase of the half-round launch (each wave walks edge tiles once its
+// instances and listed segments are done, so the edge work fills the half-round launch's tail
+// instead of waiting for it).
 template <int MODE>
-__global__ void __launch_bounds__(FW * WAVES, B2F_EDGE_WAVES)
-fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
-                  uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
-                  uint32_t* __restrict__ fixed, uint32_t* __restrict__ redo,
-                  b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
-                  uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk) {
+__device__ __forceinline__ void edge_walk(uint32_t* S, uint32_t lane, uint64_t t_first, uint64_t W,
+                                          const uint64_t* IV, const uint8_t* Sg, EvalAcc& A,
+                                          const b2f_input* __restrict__ in, uint32_t n,
+                                          const uint64_t* __restrict__ off, uint64_t total_rows,
+                                          const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
+                                          uint32_t* __restrict__ fixed, uint32_t* __restrict__ redo,
+                                          const Inject& inj, uint64_t* __restrict__ defer,
+                                          uint32_t defer_cap) {
   using namespace hr2;
   using namespace edge2;
-  (void)clk;
-  __shared__ __attribute__((aligned(16))) uint32_t L[E_WORDS];
-  const int tid = threadIdx.x;
-  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
-  if (tid < 22) L[E_ACC + tid] = 0;
-  if (tid == 22) *reinterpret_cast<uint64_t*>(L + E_ACC + 20) = ~0ull;
-  if (tid < 16) L[E_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
-  if (tid < 40) L[E_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
-  __syncthreads();
-  EvalAcc A{L + E_ACC};
-  const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + E_IV);
-  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + E_SG);
-  uint32_t* S = L + E_WAVE + wv * EW_WORDS;
   const uint32_t Sb = lds_byte(S);
   uint64_t* prod = reinterpret_cast<uint64_t*>(S + E_PROD);
-
   // per-lane constants
   const ELane E = make_elane(lane, Sb, IV);
   const uint32_t kind = E.kind, qq = E.qq, wa = E.a;
@@ -1715,12 +1721,11 @@ fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* 
   const bool plane = lane >= NQ && lane < NQ + 4;
   const uint32_t pg = lane - NQ;
 
-  if (*status == 0) {
+  {
     const uint64_t used_rows = off[n];
     const uint64_t n_pad = ((total_rows - used_rows) / 4 + PAD_Q - 1) / PAD_Q;
     const uint64_t t_all = (uint64_t)n + n_pad;
-    const uint64_t W = (uint64_t)gridDim.x * WAVES;
-    uint64_t t = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
+    uint64_t t = t_first;
     auto ectx = [&](uint64_t tt) {
       ECtx c;
       const uint32_t i = tt < n ? (uint32_t)tt : 0u;
@@ -1903,7 +1908,39 @@ fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* 
       cn = cnn;
       P = Pn;
     }
-  }
+    }
+}
+
+#ifndef B2F_EDGE_WAVES
+#define B2F_EDGE_WAVES 3  // waves per SIMD the edge kernel is compiled for (VGPR budget)
+#endif
+template <int MODE>
+__global__ void __launch_bounds__(FW * WAVES, B2F_EDGE_WAVES)
+fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
+                  uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
+                  uint32_t* __restrict__ fixed, uint32_t* __restrict__ redo,
+                  b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
+                  uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk) {
+  using namespace hr2;
+  using namespace edge2;
+  (void)clk;
+  __shared__ __attribute__((aligned(16))) uint32_t L[E_WORDS];
+  const int tid = threadIdx.x;
+  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
+  if (tid < 22) L[E_ACC + tid] = 0;
+  if (tid == 22) *reinterpret_cast<uint64_t*>(L + E_ACC + 20) = ~0ull;
+  if (tid < 16) L[E_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
+  if (tid < 40) L[E_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
+  __syncthreads();
+  EvalAcc A{L + E_ACC};
+  const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + E_IV);
+  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + E_SG);
+  uint32_t* S = L + E_WAVE + wv * EW_WORDS;
+
+  if (*status == 0)
+    edge_walk<MODE>(S, lane, first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x),
+                    (uint64_t)gridDim.x * WAVES, IV, Sg, A, in, n, off, total_rows, rec, adv, fixed,
+                    redo, inj, defer, defer_cap);
   __syncthreads();
   flush_report(A, rep, tid);
 }
@@ -2332,10 +2369,11 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   case M:                                                                                          \
     hipLaunchKernelGGL(fused_hr_kernel<M>, dim3(grid), dim3(FW * WAVES), 0, s, d_in, n, d_off,     \
                        total_rows, rec, d_adv, d_fixed, desc, d_rep, d_status, inj, defer, DEFER_CAP, \
-                       clk, seg);                                                                  \
-    hipLaunchKernelGGL(fused_edge_kernel<M>, dim3(grid_e), dim3(FW * WAVES), 0, s, d_in, n, d_off, \
-                       total_rows, rec, d_adv, d_fixed, redo, d_rep, d_status, inj, defer,         \
-                       DEFER_CAP, clk);                                                            \
+                       clk, seg, redo);                                                            \
+    if (B2F_EDGE_SEPARATE)                                                                         \
+      hipLaunchKernelGGL(fused_edge_kernel<M>, dim3(grid_e), dim3(FW * WAVES), 0, s, d_in, n, d_off, \
+                         total_rows, rec, d_adv, d_fixed, redo, d_rep, d_status, inj, defer,       \
+                         DEFER_CAP, clk);                                                          \
     hipLaunchKernelGGL(edge_redo_kernel<M>, dim3(cu_count), dim3(FW * WAVES), 0, s, d_in, d_off,   \
                        total_rows, rec, d_adv, d_fixed, redo, d_rep, d_status, inj, defer,         \
                        DEFER_CAP);                                                                 \
