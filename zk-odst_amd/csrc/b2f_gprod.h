@@ -5,22 +5,22 @@
 //
 // z[p + 1] = seed N_p / D_p with N_p, D_p the prefix products through row p, and
 // D_p^-1 = D^-1 prod_{i > p} den_i: ONE inversion per product (of the whole den product D),
-// the rest prefix and suffix products. Three passes over ZC-row chunks (one lane walks one
-// chunk):
-//   gp_chunk:  the chunk's num prefix Nloc_p (written over num in place), the chunk totals of
-//              num and den (2 products per row);
-//   gp_total:  the den total D (from the chunk totals, or from gp_block_reduce's block totals);
-//   gp_scan:   K'_q = seed N_before(q) prod_{q' > q} D_q' per chunk (K_q = K'_q D^-1) and seed N
-//              (the closing value seed N / D = z[usable] before its D^-1).
-//              Up to SCAN_THREADS x 4 chunks one workgroup per product scans them directly;
-//              beyond, three levels over blocks of SCAN_THREADS chunks (gp_block_reduce: block
-//              totals; gp_scan over the block totals; gp_block_down: in-block exclusive prefix /
-//              suffix combined with the block's K'), so the serial run per lane stays short;
+// the rest prefix and suffix products. Chunks of ZC rows (one lane walks one chunk), blocks of
+// BLK chunks (one workgroup):
+//   gp_chunk:  the chunk's num prefix Nloc_p (written over num in place) and its num / den
+//              totals (2 products per row); then, across the workgroup's BLK chunks, the
+//              exclusive prefix of the num totals and exclusive suffix of the den totals (zn /
+//              zd per chunk) and the block's totals (tn / td) -- Hillis-Steele in LDS;
+//   gp_total:  the den total D from the block totals;
 //   gp_inv:    D^-1 (one lane's Kaliski inversion, ~100 us of latency) and the closing values.
-//              It depends only on gp_total, so it runs on a second stream beside the scans;
-//   gp_write:  backward over the chunk: z[p + 1] = K'_q D^-1 Nloc_p prod_{p < i < e} den_i
-//              (2 products per row), converted to the output form and staged through LDS so a
-//              wave's stores cover whole 128-byte row groups.
+//              It depends only on gp_total, so it runs on a second stream beside the scan;
+//   gp_scan:   K'_b = seed N_before(b) prod_{b' > b} D_b' per block (K = K' D^-1) and seed N
+//              (the closing value seed N / D = z[usable] before its D^-1);
+//   gp_write:  backward over the chunk: z[p + 1] = K'_b zn_q zd_q D^-1 Nloc_p prod_{p < i < e}
+//              den_i (2 products per row), converted to the output form and staged through LDS
+//              so a wave's stores cover whole 128-byte row groups.
+// (Round 3 reduced and down-swept 1,024-chunk blocks in two more passes, 124-151 us per lookup
+// call of 64 circuits; the in-block scans now ride in gp_chunk, one product per row more.)
 // Products are independent along blockIdx.y: product y reads num/den + y * elems(usable) and
 // writes z column z_base + y * z_stride (u64 units, 4 per element).
 #pragma once
@@ -108,35 +108,61 @@ __device__ __forceinline__ Fe out_form(const Fe& a, bool mont) {
   return mont ? a : field::to_canonical<F>(a);
 }
 
+constexpr int BLK = 256;  // chunks per block = gp_chunk's workgroup
+__host__ __device__ inline uint64_t n_blocks(uint64_t usable) { return (n_chunks(usable) + BLK - 1) / BLK; }
+
 template <class F>
-__global__ __launch_bounds__(256) void gp_chunk(uint64_t usable, Fe* __restrict__ num,
+__global__ __launch_bounds__(BLK) void gp_chunk(uint64_t usable, Fe* __restrict__ num,
                                                 const Fe* __restrict__ den, Fe* __restrict__ zn,
-                                                Fe* __restrict__ zd) {
-  const uint32_t c = blockIdx.y;
-  const uint64_t nq = n_chunks(usable);
-  const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (q >= nq) return;
-  Fe* nm = num + (uint64_t)c * elems(usable);
-  const Fe* dn = den + (uint64_t)c * elems(usable);
-  const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
-  Fe pn = nm[slot_of(b, nq)], pd = dn[slot_of(b, nq)];  // row b
-  for (uint64_t p = b + 1; p < e; p++) {
-    const uint64_t k = slot_of(p, nq);
-    pn = field::mul<F>(pn, nm[k]);
-    pd = field::mul<F>(pd, dn[k]);
-    nm[k] = pn;
+                                                Fe* __restrict__ zd, Fe* __restrict__ tn,
+                                                Fe* __restrict__ td) {
+  __shared__ Fe sn[BLK], sd[BLK];
+  const uint32_t c = blockIdx.y, t = threadIdx.x;
+  const uint64_t nq = n_chunks(usable), nb = n_blocks(usable);
+  const uint64_t q = (uint64_t)blockIdx.x * BLK + t;
+  Fe pn = field::one<F>(), pd = field::one<F>();  // chunks past the end: the identity
+  if (q < nq) {
+    Fe* nm = num + (uint64_t)c * elems(usable);
+    const Fe* dn = den + (uint64_t)c * elems(usable);
+    const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
+    pn = nm[slot_of(b, nq)];  // row b
+    pd = dn[slot_of(b, nq)];
+    for (uint64_t p = b + 1; p < e; p++) {
+      const uint64_t k = slot_of(p, nq);
+      pn = field::mul<F>(pn, nm[k]);
+      pd = field::mul<F>(pd, dn[k]);
+      nm[k] = pn;
+    }
   }
-  zn[(uint64_t)c * nq + q] = pn;
-  zd[(uint64_t)c * nq + q] = pd;
+  // inclusive scans over the block: prefix of the num totals, suffix of the den totals
+  sn[t] = pn;
+  sd[t] = pd;
+  __syncthreads();
+  for (int off = 1; off < BLK; off <<= 1) {
+    Fe xn = pn, xd = pd;
+    if (t >= (uint32_t)off) xn = field::mul<F>(sn[t - off], pn);
+    if (t + off < (uint32_t)BLK) xd = field::mul<F>(pd, sd[t + off]);
+    __syncthreads();
+    sn[t] = pn = xn;
+    sd[t] = pd = xd;
+    __syncthreads();
+  }
+  if (q < nq) {
+    zn[(uint64_t)c * nq + q] = t ? sn[t - 1] : field::one<F>();
+    zd[(uint64_t)c * nq + q] = t + 1 < (uint32_t)BLK ? sd[t + 1] : field::one<F>();
+  }
+  if (t == 0) {
+    tn[(uint64_t)c * nb + blockIdx.x] = sn[BLK - 1];
+    td[(uint64_t)c * nb + blockIdx.x] = sd[0];
+  }
 }
 
-// zn[q] <- K'_q = seed N_before(q) prod_{q' > q} zd[q'] with N_before(q) = prod_{q' < q} zn[q']
-// (K_q = K'_q D^-1: gp_write applies D^-1). Per-thread runs of chunks, Hillis-Steele scans of the
-// run products in LDS (a prefix for num, a suffix for den). seed: Montgomery elements per product
-// (nullptr: 1); sn[c] <- seed N.
-// T threads: SCAN_THREADS, or one wave when there are at most 64 chunk totals (the block totals
-// of the three-level path) -- a 1,024-thread scan of 8 values spent ten levels of products on
-// every thread.
+// Over the block totals (zn = tn, zd = td, nq = the block count): zn[b] <- K'_b = seed
+// N_before(b) prod_{b' > b} zd[b'] with N_before(b) = prod_{b' < b} zn[b'] (K_b = K'_b D^-1:
+// gp_write applies D^-1). Per-thread runs of blocks, Hillis-Steele scans of the run products in
+// LDS (a prefix for num, a suffix for den). seed: Montgomery elements per product (nullptr: 1);
+// sn[c] <- seed N. T threads: SCAN_THREADS, or one wave for at most 64 blocks (a 1,024-thread
+// scan of 8 values spent ten levels of products on every thread).
 template <class F, int T = SCAN_THREADS>
 __global__ __launch_bounds__(T) void gp_scan(uint64_t nq, Fe* __restrict__ zn,
                                              const Fe* __restrict__ zd,
@@ -180,9 +206,8 @@ __global__ __launch_bounds__(T) void gp_scan(uint64_t nq, Fe* __restrict__ zn,
   }
 }
 
-// D = the product of a product's den totals: the chunk totals (up to 4 x SCAN_THREADS chunks) or,
-// on the three-level path, gp_block_reduce's block totals -- a few hundred values, so D is ready
-// right after the reduction and the inversion starts before the scans. (Over all chunk totals a
+// D = the product of a product's den block totals (a few to a few thousand values), so D is ready
+// right after gp_chunk and the inversion starts before the scan. (Over all chunk totals a
 // workgroup's serial strides took 750 us at 2^22 rows.) One workgroup per product.
 constexpr int TOT_T = 256;
 template <class F>
@@ -227,87 +252,6 @@ __global__ void gp_close(const Fe* __restrict__ sn, const Fe* __restrict__ dinv,
   if (c < g) closing[c] = field::mul<F>(sn[c], dinv[c]);
 }
 
-// block b of product c: the products of its SCAN_THREADS chunks' zn and zd -> tn/td[c][b]
-template <class F>
-__global__ __launch_bounds__(SCAN_THREADS) void gp_block_reduce(uint64_t nq, const Fe* __restrict__ zn,
-                                                                const Fe* __restrict__ zd,
-                                                                Fe* __restrict__ tn, Fe* __restrict__ td) {
-  const uint32_t b = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
-  const uint64_t nb = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
-  const uint64_t q = (uint64_t)b * SCAN_THREADS + t;
-  __shared__ Fe sn[SCAN_THREADS], sd[SCAN_THREADS];
-  Fe pn = q < nq ? zn[(uint64_t)c * nq + q] : field::one<F>();
-  Fe pd = q < nq ? zd[(uint64_t)c * nq + q] : field::one<F>();
-  for (uint32_t w = SCAN_THREADS / 2; w > 0; w >>= 1) {
-    if (t >= w && t < 2 * w) {
-      sn[t] = pn;
-      sd[t] = pd;
-    }
-    __syncthreads();
-    if (t < w) {
-      pn = field::mul<F>(pn, sn[t + w]);
-      pd = field::mul<F>(pd, sd[t + w]);
-    }
-    __syncthreads();
-  }
-  if (t == 0) {
-    tn[(uint64_t)c * nb + b] = pn;
-    td[(uint64_t)c * nb + b] = pd;
-  }
-}
-
-// K_q = KB[b] * (exclusive in-block prefix of zn) * (exclusive in-block suffix of zd), KB[b] the
-// block's K from gp_scan over the block totals. DOWN_T threads, each owning DOWN_PER consecutive
-// chunks of the block -- thread totals, a DOWN_T-wide scan of them, then a backward pass that
-// leaves each chunk's exclusive zd suffix in zd (not read after this pass) and a forward pass that
-// writes K -- about 36 products per thread. (64 threads x 16 chunks: ~90 products per thread on
-// one wave per block, 123 us for 64 lookup circuits; a 1,024-wide Hillis-Steele scan: 22 per chunk.)
-constexpr int DOWN_T = 256, DOWN_PER = SCAN_THREADS / DOWN_T;
-template <class F>
-__global__ __launch_bounds__(DOWN_T) void gp_block_down(uint64_t nq, Fe* __restrict__ zn,
-                                                        Fe* __restrict__ zd,
-                                                        const Fe* __restrict__ kb) {
-  const uint32_t b = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
-  const uint64_t nb = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
-  const uint64_t q0 = (uint64_t)b * SCAN_THREADS + (uint64_t)t * DOWN_PER;
-  Fe* an = zn + (uint64_t)c * nq;
-  Fe* ad = zd + (uint64_t)c * nq;
-  const uint32_t cnt = q0 >= nq ? 0u : (uint32_t)(nq - q0 < DOWN_PER ? nq - q0 : DOWN_PER);
-  Fe tn = field::one<F>(), td = field::one<F>();
-  for (uint32_t i = 0; i < cnt; i++) {
-    tn = field::mul<F>(tn, an[q0 + i]);
-    td = field::mul<F>(td, ad[q0 + i]);
-  }
-  __shared__ Fe sn[DOWN_T], sd[DOWN_T];
-  sn[t] = tn;
-  sd[t] = td;
-  __syncthreads();
-  Fe pn = tn, pd = td;
-  for (int off = 1; off < DOWN_T; off <<= 1) {  // inclusive prefix of sn, suffix of sd
-    Fe xn = pn, xd = pd;
-    if (t >= (uint32_t)off) xn = field::mul<F>(sn[t - off], pn);
-    if (t + off < (uint32_t)DOWN_T) xd = field::mul<F>(pd, sd[t + off]);
-    __syncthreads();
-    sn[t] = pn = xn;
-    sd[t] = pd = xd;
-    __syncthreads();
-  }
-  if (!cnt) return;
-  const Fe k = kb[(uint64_t)c * nb + b];
-  Fe e = t ? field::mul<F>(k, sn[t - 1]) : k;                               // KB x thread prefix
-  Fe sf = t + 1 < (uint32_t)DOWN_T ? sd[t + 1] : field::one<F>();           // thread suffix
-  for (uint32_t i = cnt; i-- > 0;) {  // backward: zd[q] <- exclusive in-block suffix of zd
-    const Fe v = ad[q0 + i];
-    ad[q0 + i] = sf;
-    sf = field::mul<F>(sf, v);
-  }
-  for (uint32_t i = 0; i < cnt; i++) {  // forward: K_q
-    const Fe v = an[q0 + i];
-    an[q0 + i] = field::mul<F>(e, ad[q0 + i]);
-    e = field::mul<F>(e, v);
-  }
-}
-
 // z rows go out through LDS in groups of GW_ROWS rows: each lane walks its chunk backward as
 // before, stages the z values of GW_ROWS rows, and the wave then stores the group's rows of its
 // 64 chunks so that every 8 lanes write one 128-byte run of rows (a lane storing its own rows
@@ -323,6 +267,8 @@ __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint
                                                 uint64_t z_stride, const Fe* __restrict__ num,
                                                 const Fe* __restrict__ den,
                                                 const Fe* __restrict__ zn,
+                                                const Fe* __restrict__ zd,
+                                                const Fe* __restrict__ kb,
                                                 const Fe* __restrict__ seed,
                                                 const Fe* __restrict__ post,
                                                 const Fe* __restrict__ dinv) {
@@ -343,8 +289,10 @@ __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint
   const Fe s0 = post ? post[c] : (seed ? seed[c] : field::one<F>());
   if (q == 0) field::store(zcol, out_form<F>(s0, mont));
   Fe k = field::one<F>();
-  if (act) {
-    k = field::mul<F>(zn[(uint64_t)c * nq + q], dinv[c]);  // K'_q D^-1
+  if (act) {  // K'_q D^-1 = K'_b (exclusive in-block num prefix) (exclusive in-block den suffix) D^-1
+    const uint64_t nb = n_blocks(usable);
+    k = field::mul<F>(field::mul<F>(kb[(uint64_t)c * nb + q / BLK], zn[(uint64_t)c * nq + q]),
+                      field::mul<F>(zd[(uint64_t)c * nq + q], dinv[c]));
     if (post) k = field::mul<F>(k, post[c]);
   }
 #pragma unroll 1
@@ -390,8 +338,8 @@ __global__ void gp_chain_seeds(const Fe* __restrict__ T, Fe* __restrict__ S, uin
 
 // Scratch (Fe elements) gp::run needs per product: chunk products, and block totals + K.
 __host__ __device__ inline uint64_t scratch_elems(uint64_t usable) {
-  const uint64_t nq = n_chunks(usable), nb = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
-  return 2 * nq + 2 * nb + 2;  // chunk totals, block totals, (seed N, D / D^-1)
+  const uint64_t nq = n_chunks(usable), nb = n_blocks(usable);
+  return 2 * nq + 2 * nb + 2;  // in-block chunk prefixes / suffixes, block totals, (seed N, D / D^-1)
 }
 
 // The passes for `g` products on `s`. zs: scratch of g * scratch_elems(usable). With `chain`
@@ -414,47 +362,32 @@ hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_
     closing = chain;  // T
     post = chain + g;  // S
   }
-  const uint64_t nq = n_chunks(usable), nb = (nq + SCAN_THREADS - 1) / SCAN_THREADS;
+  const uint64_t nq = n_chunks(usable), nb = n_blocks(usable);
   Fe* zn = zs;
   Fe* zd = zs + (uint64_t)g * nq;
   Fe* tn = zd + (uint64_t)g * nq;
   Fe* td = tn + (uint64_t)g * nb;
   Fe* sn = td + (uint64_t)g * nb;  // g: seed N per product (gp_scan)
   Fe* dt = sn + g;                  // g: D, then D^-1 (gp_total, gp_inv)
-  const uint32_t zq = (uint32_t)((nq + 255) / 256);
   hipError_t e;
-  hipLaunchKernelGGL(gp_chunk<F>, dim3(zq, g), dim3(256), 0, s, usable, num, den, zn, zd);
-  const bool three = nq > 4ull * SCAN_THREADS;
-  if (three)
-    hipLaunchKernelGGL(gp_block_reduce<F>, dim3((uint32_t)nb, g), dim3(SCAN_THREADS), 0, s, nq, zn, zd,
-                       tn, td);
-  if (three)
-    hipLaunchKernelGGL(gp_total<F>, dim3(g), dim3(TOT_T), 0, s, nb, td, dt);
-  else
-    hipLaunchKernelGGL(gp_total<F>, dim3(g), dim3(TOT_T), 0, s, nq, zd, dt);
-  const bool fork = side.s2 && three;  // the scans are long enough to hide it
+  hipLaunchKernelGGL(gp_chunk<F>, dim3((uint32_t)nb, g), dim3(BLK), 0, s, usable, num, den, zn, zd, tn, td);
+  hipLaunchKernelGGL(gp_total<F>, dim3(g), dim3(TOT_T), 0, s, nb, td, dt);
+  const bool fork = side.s2 && nb > 64;  // the scan is long enough to hide the inversion
   if (fork) {
     if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
   }
   hipLaunchKernelGGL(gp_inv<F>, dim3(g), dim3(64), 0, fork ? side.s2 : s, dt, sticky);
   if (fork && (e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;
-  if (nq <= 64) {
-    hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nq, zn, zd, seed, sn);
-  } else if (!three) {
-    hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nq, zn, zd, seed, sn);
-  } else {
-    if (nb <= 64)
-      hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nb, tn, td, seed, sn);
-    else
-      hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, tn, td, seed, sn);
-    hipLaunchKernelGGL(gp_block_down<F>, dim3((uint32_t)nb, g), dim3(DOWN_T), 0, s, nq, zn, zd, tn);
-  }
+  if (nb <= 64)
+    hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nb, tn, td, seed, sn);
+  else
+    hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, tn, td, seed, sn);
   if (fork && (e = hipStreamWaitEvent(s, side.join, 0)) != hipSuccess) return e;
   if (closing) hipLaunchKernelGGL(gp_close<F>, dim3(1), dim3(256), 0, s, sn, dt, closing, g);
   if (chain) hipLaunchKernelGGL(gp_chain_seeds<F>, dim3(1), dim3(64), 0, s, chain, post, g);
-  hipLaunchKernelGGL(gp_write<F>, dim3(zq, g), dim3(256), 0, s, usable, mont, z_base, z_stride, num,
-                     den, zn, seed, post, dt);
+  hipLaunchKernelGGL(gp_write<F>, dim3((uint32_t)((nq + 255) / 256), g), dim3(256), 0, s, usable, mont,
+                     z_base, z_stride, num, den, zn, zd, tn, seed, post, dt);
   return hipGetLastError();
 }
 
