@@ -342,20 +342,53 @@ __host__ __device__ inline uint64_t scratch_elems(uint64_t usable) {
   return 2 * nq + 2 * nb + 2;  // in-block chunk prefixes / suffixes, block totals, (seed N, D / D^-1)
 }
 
-// The passes for `g` products on `s`. zs: scratch of g * scratch_elems(usable). With `chain`
-// (2 g elements of scratch) the products are chained -- product c starts from product c - 1's
-// closing value, product 0 from 1 -- and still scanned side by side: their single inversions
-// run in parallel, the seeds are applied in gp_write. With a second stream `s2` and two events
-// the inversions run there, beside gp_block_down (they need only gp_scan's totals); s2 = null
-// runs them on `s`.
 struct Side {
   hipStream_t s2;
   hipEvent_t fork, join;
 };
+struct Scratch {  // the carve of zs for g products
+  Fe *zn, *zd, *tn, *td, *sn, *dt;
+};
+inline Scratch scratch_of(Fe* zs, uint32_t g, uint64_t usable) {
+  const uint64_t nq = n_chunks(usable), nb = n_blocks(usable);
+  Scratch k;
+  k.zn = zs;
+  k.zd = zs + (uint64_t)g * nq;
+  k.tn = k.zd + (uint64_t)g * nq;
+  k.td = k.tn + (uint64_t)g * nb;
+  k.sn = k.td + (uint64_t)g * nb;  // g: seed N per product (gp_scan)
+  k.dt = k.sn + g;                  // g: D, then D^-1 (gp_total, gp_inv)
+  return k;
+}
+// First half of the passes: chunk products and block scans, the den total D, and D^-1 -- on the
+// side stream when `side` has one (forked after gp_total, joined by run_end), so whatever the
+// caller launches on `s` between run_begin and run_end overlaps the inversion's ~100 us of
+// latency (the lookup's other half of its circuits, the permutation's sigma columns).
 template <class F>
-hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_t z_stride,
-               Fe* num, const Fe* den, Fe* zs, const Fe* seed, Fe* closing, hipStream_t s,
-               Fe* chain = nullptr, int* sticky = nullptr, Side side = Side{nullptr, nullptr, nullptr}) {
+hipError_t run_begin(uint32_t g, uint64_t usable, Fe* num, const Fe* den, Fe* zs, int* sticky,
+                     Side side, hipStream_t s) {
+  const uint64_t nb = n_blocks(usable);
+  const Scratch k = scratch_of(zs, g, usable);
+  hipError_t e;
+  hipLaunchKernelGGL(gp_chunk<F>, dim3((uint32_t)nb, g), dim3(BLK), 0, s, usable, num, den, k.zn, k.zd,
+                     k.tn, k.td);
+  hipLaunchKernelGGL(gp_total<F>, dim3(g), dim3(TOT_T), 0, s, nb, k.td, k.dt);
+  if (side.s2) {
+    if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(gp_inv<F>, dim3(g), dim3(64), 0, side.s2 ? side.s2 : s, k.dt, sticky);
+  if (side.s2 && (e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;
+  return hipGetLastError();
+}
+// Second half: the block scan, the join with the inversion, closing values / chained seeds, and
+// z. With `chain` (2 g elements of scratch) the products are chained -- product c starts from
+// product c - 1's closing value, product 0 from 1 -- and still scanned side by side: their single
+// inversions run in parallel, the seeds are applied in gp_write.
+template <class F>
+hipError_t run_end(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_t z_stride,
+                   Fe* num, const Fe* den, Fe* zs, const Fe* seed, Fe* closing, hipStream_t s,
+                   Fe* chain, Side side) {
   Fe* post = nullptr;
   if (chain) {
     seed = nullptr;
@@ -363,32 +396,27 @@ hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_
     post = chain + g;  // S
   }
   const uint64_t nq = n_chunks(usable), nb = n_blocks(usable);
-  Fe* zn = zs;
-  Fe* zd = zs + (uint64_t)g * nq;
-  Fe* tn = zd + (uint64_t)g * nq;
-  Fe* td = tn + (uint64_t)g * nb;
-  Fe* sn = td + (uint64_t)g * nb;  // g: seed N per product (gp_scan)
-  Fe* dt = sn + g;                  // g: D, then D^-1 (gp_total, gp_inv)
+  const Scratch k = scratch_of(zs, g, usable);
   hipError_t e;
-  hipLaunchKernelGGL(gp_chunk<F>, dim3((uint32_t)nb, g), dim3(BLK), 0, s, usable, num, den, zn, zd, tn, td);
-  hipLaunchKernelGGL(gp_total<F>, dim3(g), dim3(TOT_T), 0, s, nb, td, dt);
-  const bool fork = side.s2 && nb > 64;  // the scan is long enough to hide the inversion
-  if (fork) {
-    if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(gp_inv<F>, dim3(g), dim3(64), 0, fork ? side.s2 : s, dt, sticky);
-  if (fork && (e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;
   if (nb <= 64)
-    hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nb, tn, td, seed, sn);
+    hipLaunchKernelGGL((gp_scan<F, 64>), dim3(g), dim3(64), 0, s, nb, k.tn, k.td, seed, k.sn);
   else
-    hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, tn, td, seed, sn);
-  if (fork && (e = hipStreamWaitEvent(s, side.join, 0)) != hipSuccess) return e;
-  if (closing) hipLaunchKernelGGL(gp_close<F>, dim3(1), dim3(256), 0, s, sn, dt, closing, g);
+    hipLaunchKernelGGL(gp_scan<F>, dim3(g), dim3(SCAN_THREADS), 0, s, nb, k.tn, k.td, seed, k.sn);
+  if (side.s2 && (e = hipStreamWaitEvent(s, side.join, 0)) != hipSuccess) return e;
+  if (closing) hipLaunchKernelGGL(gp_close<F>, dim3(1), dim3(256), 0, s, k.sn, k.dt, closing, g);
   if (chain) hipLaunchKernelGGL(gp_chain_seeds<F>, dim3(1), dim3(64), 0, s, chain, post, g);
   hipLaunchKernelGGL(gp_write<F>, dim3((uint32_t)((nq + 255) / 256), g), dim3(256), 0, s, usable, mont,
-                     z_base, z_stride, num, den, zn, zd, tn, seed, post, dt);
+                     z_base, z_stride, num, den, k.zn, k.zd, k.tn, seed, post, k.dt);
   return hipGetLastError();
+}
+// The passes for `g` products on `s` (zs: g * scratch_elems(usable) elements).
+template <class F>
+hipError_t run(uint32_t g, uint64_t usable, bool mont, uint64_t* z_base, uint64_t z_stride,
+               Fe* num, const Fe* den, Fe* zs, const Fe* seed, Fe* closing, hipStream_t s,
+               Fe* chain = nullptr, int* sticky = nullptr, Side side = Side{nullptr, nullptr, nullptr}) {
+  hipError_t e = run_begin<F>(g, usable, num, den, zs, sticky, side, s);
+  if (e != hipSuccess) return e;
+  return run_end<F>(g, usable, mont, z_base, z_stride, num, den, zs, seed, closing, s, chain, side);
 }
 
 }  // namespace

@@ -41,7 +41,8 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
                          void* scratch, uint32_t group, int* sticky, hipStream_t s2,
-                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s);
+                         hipEvent_t ev_fork, hipEvent_t ev_join, hipEvent_t ev_fork2,
+                         hipEvent_t ev_join2, hipStream_t s);
 
 namespace {
 
@@ -480,7 +481,7 @@ template <class F>
 hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint64_t* d_row_begin,
                       uint32_t n_circuits, uint64_t usable_rows, const Chal& ch, bool mont,
                       uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad, void* scratch,
-                      uint32_t group, int* sticky, gp::Side side, hipStream_t s) {
+                      uint32_t group, int* sticky, const gp::Side* sides, hipStream_t s) {
   Carve k = carve(scratch, group, usable_rows);
   const dim3 tb(TROWS / 256);
   hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm);
@@ -497,22 +498,57 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   hipLaunchKernelGGL(lk_rank_kernel, tb, dim3(256), 0, s, k.Tx, pa, k.Ts);
   hipError_t e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s);
   if (e != hipSuccess) return e;
-  for (uint32_t c0 = 0; c0 < n_circuits; c0 += group) {
-    const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
+  // Circuits in sub-groups of half the scratch (slots 0 / 1 alternating), pipelined: sub-group
+  // i's grand product is started (gp::run_begin: chunk passes, D, and D^-1 forked to the side
+  // stream), then sub-group i - 1's is finished (gp::run_end), so every inversion's ~100 us of
+  // latency runs beside the other sub-group's passes instead of in front of its own gp_write.
+  const bool pipe = group > 1;  // two slots of `sub` circuits fit the scratch
+  const uint32_t sub = pipe ? group / 2 : 1;
+  const uint64_t zse = gp::scratch_elems(usable_rows);
+  struct Pending {
+    uint32_t c0, g, slot;
+  };
+  Pending prev{0, 0, 0};
+  auto finish = [&](const Pending& p) -> hipError_t {
+    const uint64_t h0 = (uint64_t)p.slot * sub;
+    return gp::run_end<F>(p.g, usable_rows, mont, d_out + ((uint64_t)p.c0 * 5 + 4) * out_rows * 4,
+                          5 * out_rows * 4, k.num + h0 * gp::elems(usable_rows),
+                          k.den + h0 * gp::elems(usable_rows), k.zs + h0 * zse, nullptr, nullptr, s,
+                          nullptr, sides[p.slot]);
+  };
+  uint32_t i = 0;
+  for (uint32_t c0 = 0; c0 < n_circuits; c0 += sub, i++) {
+    const uint32_t g = n_circuits - c0 < sub ? n_circuits - c0 : sub;
+    const uint32_t slot = pipe ? (i & 1u) : 0u;
+    const uint64_t h0 = (uint64_t)slot * sub;  // the slot's first circuit in the scratch
+    uint32_t* count = k.count + h0 * TROWS;
+    uint32_t* pos = k.pos + h0 * TROWS;
+    uint32_t* dcnt = k.dcnt + h0 * TROWS;
+    uint32_t* lp = k.lp + h0 * TROWS;
+    uint32_t* samp = k.samp + h0 * 2 * SAMPLE;
+    uint32_t* part = k.part + h0 * SC_PARTS * 3;
+    Fe* num = k.num + h0 * gp::elems(usable_rows);
+    Fe* den = k.den + h0 * gp::elems(usable_rows);
     hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
-                       total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
-    hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
-    hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
-                       k.part, k.pos, k.dcnt, k.lp, k.samp);
+                       total_rows, d_row_begin, c0, usable_rows, count, d_first_bad);
+    hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, count, usable_rows, part);
+    hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, count, usable_rows,
+                       part, pos, dcnt, lp, samp);
     // permute: ~4096 rows per workgroup
     const uint32_t px = (uint32_t)((usable_rows + 4095) / 4096);
     hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
-                       d_row_begin, c0, usable_rows, k.Tx, k.Ts, mont, d_out, out_rows, ch, k.num,
-                       k.den, k.pos, k.dcnt, k.lp, k.samp);
-    e = gp::run<F>(g, usable_rows, mont, d_out + ((uint64_t)c0 * 5 + 4) * out_rows * 4,
-                   5 * out_rows * 4, k.num, k.den, k.zs, nullptr, nullptr, s, nullptr, sticky, side);
+                       d_row_begin, c0, usable_rows, k.Tx, k.Ts, mont, d_out, out_rows, ch, num,
+                       den, pos, dcnt, lp, samp);
+    e = gp::run_begin<F>(g, usable_rows, num, den, k.zs + h0 * zse, sticky, sides[slot], s);
     if (e != hipSuccess) return e;
+    if (!pipe) {  // one slot: finish before the next sub-group reuses it
+      if ((e = finish(Pending{c0, g, slot})) != hipSuccess) return e;
+      continue;
+    }
+    if (i > 0 && (e = finish(prev)) != hipSuccess) return e;
+    prev = Pending{c0, g, slot};
   }
+  if (pipe && i > 0 && (e = finish(prev)) != hipSuccess) return e;
   return hipSuccess;
 }
 
@@ -527,8 +563,9 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
                          void* scratch, uint32_t group, int* sticky, hipStream_t s2,
-                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s) {
-  const gp::Side side{s2, ev_fork, ev_join};
+                         hipEvent_t ev_fork, hipEvent_t ev_join, hipEvent_t ev_fork2,
+                         hipEvent_t ev_join2, hipStream_t s) {
+  const gp::Side sides[2] = {{s2, ev_fork, ev_join}, {s2, ev_fork2, ev_join2}};
   Chal ch;
   for (int i = 0; i < 4; i++) {
     ch.theta[i] = theta[i];
@@ -538,9 +575,9 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
   const bool mont = (form & 1u) != 0;
   if (form >> 1)
     return run_lookup<field::Bn254>(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, ch,
-                                    mont, d_out, out_rows, d_first_bad, scratch, group, sticky, side, s);
+                                    mont, d_out, out_rows, d_first_bad, scratch, group, sticky, sides, s);
   return run_lookup<field::Pallas>(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, ch,
-                                   mont, d_out, out_rows, d_first_bad, scratch, group, sticky, side, s);
+                                   mont, d_out, out_rows, d_first_bad, scratch, group, sticky, sides, s);
 }
 
 }  // namespace b2f

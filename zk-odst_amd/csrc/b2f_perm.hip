@@ -240,16 +240,19 @@ hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0
   const uint64_t tab = n_hi > (uint64_t)NCOL * LO ? n_hi : (uint64_t)NCOL * LO;
   hipLaunchKernelGGL(pm_table_kernel<F>, dim3((uint32_t)((tab + 255) / 256)), dim3(256), 0, s, prm,
                      n_hi, m.OL, m.BL, m.OH, m.gm);
-  if (d_sigma)
-    hipLaunchKernelGGL(pm_sigma_kernel<F>, dim3((uint32_t)((n_rows + 255) / 256)), dim3(256), 0, s, I,
-                       d_pool, n_rows, m.OL, m.OH, mont, d_sigma, out_rows);
-  // every column set's factors in one launch, then their grand products side by side,
-  // chained (set c starts where set c - 1 closed)
+  // every column set's factors in one launch, then their grand products side by side, chained
+  // (set c starts where set c - 1 closed); the sigma columns go between the two halves of the
+  // grand product, beside its inversions on the side stream
   hipLaunchKernelGGL(pm_factor_kernel<F>, dim3((uint32_t)((usable + 255) / 256), sets), dim3(256), 0, s,
                      I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, m.gm, m.num,
                      m.den);
-  hipError_t e = gp::run<F>(sets, usable, mont, d_z, out_rows * 4, m.num, m.den, m.zs, nullptr,
-                            nullptr, s, m.seed, sticky, side);
+  hipError_t e = gp::run_begin<F>(sets, usable, m.num, m.den, m.zs, sticky, side, s);
+  if (e != hipSuccess) return e;
+  if (d_sigma)
+    hipLaunchKernelGGL(pm_sigma_kernel<F>, dim3((uint32_t)((n_rows + 255) / 256)), dim3(256), 0, s, I,
+                       d_pool, n_rows, m.OL, m.OH, mont, d_sigma, out_rows);
+  e = gp::run_end<F>(sets, usable, mont, d_z, out_rows * 4, m.num, m.den, m.zs, nullptr, nullptr, s,
+                     m.seed, side);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }
