@@ -65,3 +65,21 @@ def test_param_state_errors():
     with pytest.raises(B2FError):
         hasher.Plan([b"x"], 32, bytes(65))
     assert hasher.Plan([], 64).steps == 0
+
+
+def test_workspace_reuse_rules():
+    """hasher.Workspace (no allocation inside the timed hasher call): a plan's
+    workspace is sized from the plan and reused by every plan that fits it (device, messages,
+    compressions, steps, kept inputs). Built on the CPU device here: sizes only."""
+    from b2f import hasher
+
+    big = hasher.Plan([bytes(300), bytes(1000), b"x"])
+    small = hasher.Plan([bytes(200), b"y"])
+    ws = hasher.Workspace.for_plan(big, device="cpu")
+    assert (ws.n, ws.compressions, ws.steps) == (3, int(big.start[-1]), big.steps)
+    assert ws.advice.numel() == 10 * hasher.rows(12) * 3 and ws.inputs.numel() == 3 * 216
+    assert ws.fits(big, "cpu") and ws.fits(small, "cpu")
+    assert not ws.fits(big, "cpu", keep_inputs=True)  # kept inputs need a step-major buffer
+    assert not hasher.Workspace.for_plan(small, device="cpu").fits(big, "cpu")
+    kept = hasher.Workspace.for_plan(big, device="cpu", keep_inputs=True)
+    assert kept.inputs.numel() == int(big.start[-1]) * 216 and kept.fits(small, "cpu", keep_inputs=True)
