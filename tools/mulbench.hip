@@ -8,6 +8,54 @@
 #include "../zk-odst_amd/csrc/b2f_field.h"
 using namespace b2f::field;
 
+// product scanning with two word products per asm block (one compiler wait state per block
+// instead of one per product): a probe of the wait states' cost
+__device__ __forceinline__ void madd_vv_vs(uint64_t& acc, uint32_t& ov, uint32_t x0, uint32_t y0, uint32_t x1,
+                                           uint32_t y1) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
+      "v_mad_u64_u32 %0, vcc, %4, %5, %0\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(ov)
+      : "v"(x0), "v"(y0), "v"(x1), "s"(y1)
+      : "vcc");
+}
+template <class F>
+__device__ __forceinline__ Fe mul2(const Fe& a, const Fe& b) {
+  uint32_t m[8], r[8];
+  uint64_t acc = 0;
+  uint32_t ov = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#pragma unroll
+    for (int i = 0; i < k; i++) {
+      if (F::P[k - i]) madd_vv_vs(acc, ov, a.w[i], b.w[k - i], m[i], F::P[k - i]);
+      else acc_madd(acc, ov, a.w[i], b.w[k - i]);
+    }
+    acc_madd(acc, ov, a.w[k], b.w[0]);
+    m[k] = (uint32_t)acc * F::NP;
+    acc_maddc(acc, ov, m[k], F::P[0]);
+    acc = (acc >> 32) | ((uint64_t)ov << 32);
+    ov = 0;
+  }
+#pragma unroll
+  for (int k = 8; k < 15; k++) {
+#pragma unroll
+    for (int i = k - 7; i < 8; i++) {
+      if (F::P[k - i]) madd_vv_vs(acc, ov, a.w[i], b.w[k - i], m[i], F::P[k - i]);
+      else acc_madd(acc, ov, a.w[i], b.w[k - i]);
+    }
+    r[k - 8] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)ov << 32);
+    ov = 0;
+  }
+  r[7] = (uint32_t)acc;
+  Fe o;
+#pragma unroll
+  for (int j = 0; j < 8; j++) o.w[j] = r[j];
+  return reduce_once<F>(o);
+}
+
 // mul (b2f_field.h, product scanning) vs mul_cios (the operand-scanning form it replaced) on
 // pseudo-random operands below p (top word reduced mod p's top word) and on 0, 1, p - 1: count of
 // differing products
@@ -27,9 +75,9 @@ __global__ void check(uint32_t* bad, int n) {
       b.w[0] = threadIdx.x & 1u;
       if (threadIdx.x & 2u) b = a;
     }
-    const Fe x = mul<F>(a, b), y = mul_cios<F>(a, b);
+    const Fe x = mul<F>(a, b), y = mul_cios<F>(a, b), z = mul2<F>(a, b);
     uint32_t d = 0;
-    for (int i = 0; i < 8; i++) d |= x.w[i] ^ y.w[i];
+    for (int i = 0; i < 8; i++) d |= (x.w[i] ^ y.w[i]) | (z.w[i] ^ y.w[i]);
     if (d) atomicAdd(bad, 1u);
   }
 }
@@ -42,7 +90,7 @@ __global__ __launch_bounds__(256) void k(const Fe* in, Fe* out, int n) {
   const Fe b = in[256 + (blockIdx.x & 15)];
   for (int i = 0; i < n; i++)
 #pragma unroll
-    for (int c = 0; c < CH; c++) acc[c] = V == 0 ? mul<F>(acc[c], b) : mul_cios<F>(acc[c], b);
+    for (int c = 0; c < CH; c++) acc[c] = V == 0 ? mul<F>(acc[c], b) : V == 1 ? mul_cios<F>(acc[c], b) : mul2<F>(acc[c], b);
   Fe s = acc[0];
 #pragma unroll
   for (int c = 1; c < CH; c++) s = add<F>(s, acc[c]);
@@ -89,8 +137,8 @@ int main() {
     float ms = timeit([&] { hipLaunchKernelGGL((k<F, V, CH>), dim3(blocks), dim3(256), 0, 0, in, out, n); }); \
     printf("%-7s variant %d chains %d: %.3f ms, %.2f G products/s\n", #F, V, CH, ms, prods * CH / ms / 1e6); \
   }
-  RUN(Pallas, 0, 1) RUN(Pallas, 0, 2) RUN(Pallas, 1, 1) RUN(Pallas, 1, 2)
-  RUN(Bn254, 0, 1) RUN(Bn254, 0, 2) RUN(Bn254, 1, 1) RUN(Bn254, 1, 2)
+  RUN(Pallas, 0, 1) RUN(Pallas, 0, 2) RUN(Pallas, 1, 1) RUN(Pallas, 1, 2) RUN(Pallas, 2, 1) RUN(Pallas, 2, 2)
+  RUN(Bn254, 0, 1) RUN(Bn254, 0, 2) RUN(Bn254, 1, 1) RUN(Bn254, 1, 2) RUN(Bn254, 2, 1) RUN(Bn254, 2, 2)
   {
     uint32_t* bad;
     hipMalloc(&bad, 8);
@@ -99,7 +147,7 @@ int main() {
     hipLaunchKernelGGL(check<Bn254>, dim3(1024), dim3(256), 0, 0, bad + 1, 16);
     uint32_t h[2];
     hipMemcpy(h, bad, 8, hipMemcpyDeviceToHost);
-    printf("mul (product scanning) vs mul_cios mismatches over 4.2M products: pallas %u bn254 %u\n", h[0], h[1]);
+    printf("mul / mul2 (product scanning) vs mul_cios mismatches over 4.2M products: pallas %u bn254 %u\n", h[0], h[1]);
   }
   {
     float ms = timeit([&] { hipLaunchKernelGGL(madk, dim3(blocks), dim3(256), 0, 0, (uint64_t*)out, 1024); });
