@@ -187,3 +187,30 @@ def test_lookup_zero_factor_reported_then_clean(engine, trace, form):
     z = _col_ints(out[0, 4, usable:usable + 1])[0]
     one = 1 if form in (0, 2) else R256 % p
     assert z == one  # a valid lookup closes to 1
+
+
+def test_lookup_pipelined_subgroups_equal_oracle(engine, trace):
+    """Five circuits in one call: the grand products run in pipelined sub-groups of two
+    (scratch slots 0, 1, 0; each sub-group's inversion beside the next one's passes). Every
+    circuit's five columns equal the restatement, BN254 Montgomery form."""
+    import lookup as lk
+    import torch
+
+    form = 3
+    usable = (1 << 16) + 100
+    total = trace.total_rows
+    begins = [0, 70001, 2 * usable, total - 40000, total - 3]
+    p = _mod(form)
+    theta, beta, gamma = _chal(23, form)
+    out, bad = trace.lookup_columns(engine, begins, usable, theta, beta, gamma, form=form)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    assert (bad.cpu().numpy().view(np.uint64) == np.uint64(2**64 - 1)).all()
+    adv, _ = trace.host_trace()
+    for c, b in enumerate(begins):
+        a = _circuit_rows(adv, total, b, usable)
+        ref = lk.columns(a[0], a[1], a[2], usable, theta, beta, gamma, p)
+        for j in (2, 3, 4):  # A', S' and z (A and S are per-row maps, covered above)
+            n = usable + 1 if j == 4 else usable
+            got = _col_ints(out[c, j, :n])
+            want = [v * R256 % p for v in ref[j]]
+            assert got == want, (c, j)
