@@ -111,6 +111,36 @@ __device__ __forceinline__ Fe out_form(const Fe& a, bool mont) {
 constexpr int BLK = 256;  // chunks per block = gp_chunk's workgroup
 __host__ __device__ inline uint64_t n_blocks(uint64_t usable) { return (n_chunks(usable) + BLK - 1) / BLK; }
 
+// The block scan of gp_chunk: chunk totals pn / pd of the workgroup's BLK chunks -> exclusive
+// in-block num prefix (zn) / den suffix (zd) per chunk and the block totals (tn / td). Every
+// thread of the workgroup calls it (chunks past the end with the identity).
+template <class F>
+__device__ __forceinline__ void block_scan(Fe* sn, Fe* sd, uint32_t t, uint64_t q, uint64_t nq, uint64_t nb,
+                                           uint32_t c, Fe pn, Fe pd, Fe* __restrict__ zn,
+                                           Fe* __restrict__ zd, Fe* __restrict__ tn, Fe* __restrict__ td) {
+  // inclusive scans over the block: prefix of the num totals, suffix of the den totals
+  sn[t] = pn;
+  sd[t] = pd;
+  __syncthreads();
+  for (int off = 1; off < BLK; off <<= 1) {
+    Fe xn = pn, xd = pd;
+    if (t >= (uint32_t)off) xn = field::mul<F>(sn[t - off], pn);
+    if (t + off < (uint32_t)BLK) xd = field::mul<F>(pd, sd[t + off]);
+    __syncthreads();
+    sn[t] = pn = xn;
+    sd[t] = pd = xd;
+    __syncthreads();
+  }
+  if (q < nq) {
+    zn[(uint64_t)c * nq + q] = t ? sn[t - 1] : field::one<F>();
+    zd[(uint64_t)c * nq + q] = t + 1 < (uint32_t)BLK ? sd[t + 1] : field::one<F>();
+  }
+  if (t == 0) {
+    tn[(uint64_t)c * nb + blockIdx.x] = sn[BLK - 1];
+    td[(uint64_t)c * nb + blockIdx.x] = sd[0];
+  }
+}
+
 template <class F>
 __global__ __launch_bounds__(BLK) void gp_chunk(uint64_t usable, Fe* __restrict__ num,
                                                 const Fe* __restrict__ den, Fe* __restrict__ zn,
@@ -134,27 +164,7 @@ __global__ __launch_bounds__(BLK) void gp_chunk(uint64_t usable, Fe* __restrict_
       nm[k] = pn;
     }
   }
-  // inclusive scans over the block: prefix of the num totals, suffix of the den totals
-  sn[t] = pn;
-  sd[t] = pd;
-  __syncthreads();
-  for (int off = 1; off < BLK; off <<= 1) {
-    Fe xn = pn, xd = pd;
-    if (t >= (uint32_t)off) xn = field::mul<F>(sn[t - off], pn);
-    if (t + off < (uint32_t)BLK) xd = field::mul<F>(pd, sd[t + off]);
-    __syncthreads();
-    sn[t] = pn = xn;
-    sd[t] = pd = xd;
-    __syncthreads();
-  }
-  if (q < nq) {
-    zn[(uint64_t)c * nq + q] = t ? sn[t - 1] : field::one<F>();
-    zd[(uint64_t)c * nq + q] = t + 1 < (uint32_t)BLK ? sd[t + 1] : field::one<F>();
-  }
-  if (t == 0) {
-    tn[(uint64_t)c * nb + blockIdx.x] = sn[BLK - 1];
-    td[(uint64_t)c * nb + blockIdx.x] = sd[0];
-  }
+  block_scan<F>(sn, sd, t, q, nq, nb, c, pn, pd, zn, zd, tn, td);
 }
 
 // Over the block totals (zn = tn, zd = td, nq = the block count): zn[b] <- K'_b = seed
@@ -349,7 +359,7 @@ struct Side {
 struct Scratch {  // the carve of zs for g products
   Fe *zn, *zd, *tn, *td, *sn, *dt;
 };
-inline Scratch scratch_of(Fe* zs, uint32_t g, uint64_t usable) {
+__host__ __device__ inline Scratch scratch_of(Fe* zs, uint32_t g, uint64_t usable) {
   const uint64_t nq = n_chunks(usable), nb = n_blocks(usable);
   Scratch k;
   k.zn = zs;
@@ -364,14 +374,17 @@ inline Scratch scratch_of(Fe* zs, uint32_t g, uint64_t usable) {
 // side stream when `side` has one (forked after gp_total, joined by run_end), so whatever the
 // caller launches on `s` between run_begin and run_end overlaps the inversion's ~100 us of
 // latency (the lookup's other half of its circuits, the permutation's sigma columns).
+// chunked: the caller's factor pass already wrote what gp_chunk writes (Nloc over num, zn / zd,
+// tn / td: the permutation's pm_chunk_kernel)
 template <class F>
 hipError_t run_begin(uint32_t g, uint64_t usable, Fe* num, const Fe* den, Fe* zs, int* sticky,
-                     Side side, hipStream_t s) {
+                     Side side, hipStream_t s, bool chunked = false) {
   const uint64_t nb = n_blocks(usable);
   const Scratch k = scratch_of(zs, g, usable);
   hipError_t e;
-  hipLaunchKernelGGL(gp_chunk<F>, dim3((uint32_t)nb, g), dim3(BLK), 0, s, usable, num, den, k.zn, k.zd,
-                     k.tn, k.td);
+  if (!chunked)
+    hipLaunchKernelGGL(gp_chunk<F>, dim3((uint32_t)nb, g), dim3(BLK), 0, s, usable, num, den, k.zn, k.zd,
+                       k.tn, k.td);
   hipLaunchKernelGGL(gp_total<F>, dim3(g), dim3(TOT_T), 0, s, nb, k.td, k.dt);
   if (side.s2) {
     if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;

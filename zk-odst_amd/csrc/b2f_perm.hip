@@ -192,6 +192,68 @@ __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* 
   gp::wave_store_slots<true>(den + sb, stage[wv], lane, d);
 }
 
+// The factors fused with the grand product's chunk pass (replaces pm_factor_kernel + gp_chunk):
+// a lane per 16-row chunk walks its rows -- per row the set's num / den factors as
+// pm_factor_kernel forms them, the running num prefix Nloc written over num and the den factor
+// to den (gp::slot_of, non-temporal) -- then the workgroup's block scan (gp::block_scan). The
+// factors never make the round trip through HBM that pm_factor_kernel -> gp_chunk took (64
+// bytes written, 64 read and 32 rewritten per row and set).
+template <class F>
+__global__ __launch_bounds__(gp::BLK) void pm_chunk_kernel(Inst I, const uint32_t* __restrict__ pool,
+                                                           const uint32_t* __restrict__ adv,
+                                                           uint64_t total_rows, uint64_t row0,
+                                                           uint64_t usable, uint32_t chunk_len,
+                                                           const Fe* __restrict__ BL,
+                                                           const Fe* __restrict__ OH,
+                                                           const Fe* __restrict__ G,
+                                                           Fe* __restrict__ num, Fe* __restrict__ den,
+                                                           Fe* __restrict__ zs) {
+  __shared__ Fe sn[gp::BLK], sd[gp::BLK];
+  const uint32_t t = threadIdx.x, set = blockIdx.y, sets = gridDim.y;
+  const uint32_t j0 = set * chunk_len, j1 = j0 + chunk_len < (uint32_t)NCOL ? j0 + chunk_len : NCOL;
+  const uint64_t nq = gp::n_chunks(usable), nb = gp::n_blocks(usable);
+  const gp::Scratch k = gp::scratch_of(zs, sets, usable);
+  Fe* nm = num + (uint64_t)set * gp::elems(usable);
+  Fe* dn = den + (uint64_t)set * gp::elems(usable);
+  const uint64_t q = (uint64_t)blockIdx.x * gp::BLK + t;
+  const Fe gamma = G[0];
+  const uint64_t used = I.start[I.n];
+  Fe pn = field::one<F>(), pd = field::one<F>();
+  {
+    // the wave's first row -> its instance (one search per wave), then this lane's first row
+    const uint64_t wq = __builtin_amdgcn_readfirstlane((uint32_t)(blockIdx.x * gp::BLK + (t & ~63u)));
+    const uint64_t rb = q * gp::ZC, re = rb + gp::ZC < usable ? rb + gp::ZC : usable;
+    uint32_t ii = inst_of_wave(I, wq * gp::ZC < usable ? wq * gp::ZC : 0, rb < usable ? rb : 0);
+#pragma unroll 1
+    for (uint64_t r = rb; r < re; r++) {
+      while (ii < I.n && I.start[ii + 1] <= r) ii++;  // an instance has >= 228 rows: <= 1 step
+      Fe n, d;
+#pragma unroll 1
+      for (uint32_t j = j0; j < j1; j++) {
+        const uint32_t x = r < used ? adv[(uint64_t)(j + 1) * total_rows + row0 + r] : 0u;
+        const Fe vg = field::add<F>(field::from_u32<F>(x), gamma);
+        uint32_t c2;
+        uint64_t r2;
+        mapped(I, pool, ii, j, r, c2, r2);
+        const Fe fn = field::add<F>(vg, dw<F>(BL, OH, j, r));
+        const Fe fd = (c2 == j && r2 == r) ? fn : field::add<F>(vg, dw<F>(BL, OH, c2, r2));
+        n = j == j0 ? fn : field::mul<F>(n, fn);
+        d = j == j0 ? fd : field::mul<F>(d, fd);
+      }
+      pn = r == rb ? n : field::mul<F>(pn, n);
+      pd = r == rb ? d : field::mul<F>(pd, d);
+      const uint64_t sl = gp::slot_of(r, nq);
+      uint4* pnp = reinterpret_cast<uint4*>(nm + sl);
+      uint4* dnp = reinterpret_cast<uint4*>(dn + sl);
+      gp::nt_store(pnp, make_uint4(pn.w[0], pn.w[1], pn.w[2], pn.w[3]));
+      gp::nt_store(pnp + 1, make_uint4(pn.w[4], pn.w[5], pn.w[6], pn.w[7]));
+      gp::nt_store(dnp, make_uint4(d.w[0], d.w[1], d.w[2], d.w[3]));
+      gp::nt_store(dnp + 1, make_uint4(d.w[4], d.w[5], d.w[6], d.w[7]));
+    }
+  }
+  gp::block_scan<F>(sn, sd, t, q, nq, nb, set, pn, pd, k.zn, k.zd, k.tn, k.td);
+}
+
 struct Carve {
   Fe* OL;
   Fe* BL;
@@ -243,10 +305,17 @@ hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0
   // every column set's factors in one launch, then their grand products side by side, chained
   // (set c starts where set c - 1 closed); the sigma columns go between the two halves of the
   // grand product, beside its inversions on the side stream
+#ifdef B2F_PM_SEPARATE  // diagnostics: the factor pass and gp_chunk as two launches
   hipLaunchKernelGGL(pm_factor_kernel<F>, dim3((uint32_t)((usable + 255) / 256), sets), dim3(256), 0, s,
                      I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, m.gm, m.num,
                      m.den);
   hipError_t e = gp::run_begin<F>(sets, usable, m.num, m.den, m.zs, sticky, side, s);
+#else
+  hipLaunchKernelGGL(pm_chunk_kernel<F>, dim3((uint32_t)gp::n_blocks(usable), sets), dim3(gp::BLK), 0, s,
+                     I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, m.gm, m.num,
+                     m.den, m.zs);
+  hipError_t e = gp::run_begin<F>(sets, usable, m.num, m.den, m.zs, sticky, side, s, true);
+#endif
   if (e != hipSuccess) return e;
   if (d_sigma)
     hipLaunchKernelGGL(pm_sigma_kernel<F>, dim3((uint32_t)((n_rows + 255) / 256)), dim3(256), 0, s, I,
