@@ -717,10 +717,11 @@ def main():
             first = {}
             hasher.run_plan(eng, plan, phases=first)  # allocates the plan's workspace
             torch.cuda.synchronize()
-            phases = {}
             t2 = time.perf_counter()
-            res = hasher.run_plan(eng, plan, phases=phases)  # reuses it: no allocation
+            res = hasher.run_plan(eng, plan)  # reuses it: no allocation
             el2 = time.perf_counter() - t2
+            phases = {}
+            hasher.run_plan(eng, plan, phases=phases)  # again, phases timed apart (synchronizes)
             ok = res.verified and all(res.digests[i] == hashlib.blake2b(msgs[i]).digest()
                                       for i in range(0, hm, max(1, hm // 64)))
             hasher_aux = {"messages": hm, "bytes_each": 1024, "block_steps": plan.steps,

@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <tuple>
+
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "../../include/b2f.h"
@@ -498,57 +500,43 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   hipLaunchKernelGGL(lk_rank_kernel, tb, dim3(256), 0, s, k.Tx, pa, k.Ts);
   hipError_t e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s);
   if (e != hipSuccess) return e;
-  // Circuits in sub-groups of half the scratch (slots 0 / 1 alternating), pipelined: sub-group
-  // i's grand product is started (gp::run_begin: chunk passes, D, and D^-1 forked to the side
-  // stream), then sub-group i - 1's is finished (gp::run_end), so every inversion's ~100 us of
-  // latency runs beside the other sub-group's passes instead of in front of its own gp_write.
-  const bool pipe = group > 1;  // two slots of `sub` circuits fit the scratch
-  const uint32_t sub = pipe ? group / 2 : 1;
+  // Per group: the count / scan / permute passes over all its circuits at once (a workgroup
+  // count per circuit that fills the chip), then the grand products in two halves, pipelined:
+  // half A's run_begin (chunk passes, D, D^-1 forked to the side stream), half B's run_begin,
+  // half A's run_end, half B's run_end -- each inversion's ~100 us of latency runs beside the
+  // other half's passes instead of in front of its own gp_write. (Pipelining whole sub-groups,
+  // count and permute included, ran the count pass at half the chip: same total, r04l.)
   const uint64_t zse = gp::scratch_elems(usable_rows);
-  struct Pending {
-    uint32_t c0, g, slot;
-  };
-  Pending prev{0, 0, 0};
-  auto finish = [&](const Pending& p) -> hipError_t {
-    const uint64_t h0 = (uint64_t)p.slot * sub;
-    return gp::run_end<F>(p.g, usable_rows, mont, d_out + ((uint64_t)p.c0 * 5 + 4) * out_rows * 4,
-                          5 * out_rows * 4, k.num + h0 * gp::elems(usable_rows),
-                          k.den + h0 * gp::elems(usable_rows), k.zs + h0 * zse, nullptr, nullptr, s,
-                          nullptr, sides[p.slot]);
-  };
-  uint32_t i = 0;
-  for (uint32_t c0 = 0; c0 < n_circuits; c0 += sub, i++) {
-    const uint32_t g = n_circuits - c0 < sub ? n_circuits - c0 : sub;
-    const uint32_t slot = pipe ? (i & 1u) : 0u;
-    const uint64_t h0 = (uint64_t)slot * sub;  // the slot's first circuit in the scratch
-    uint32_t* count = k.count + h0 * TROWS;
-    uint32_t* pos = k.pos + h0 * TROWS;
-    uint32_t* dcnt = k.dcnt + h0 * TROWS;
-    uint32_t* lp = k.lp + h0 * TROWS;
-    uint32_t* samp = k.samp + h0 * 2 * SAMPLE;
-    uint32_t* part = k.part + h0 * SC_PARTS * 3;
-    Fe* num = k.num + h0 * gp::elems(usable_rows);
-    Fe* den = k.den + h0 * gp::elems(usable_rows);
+  for (uint32_t c0 = 0; c0 < n_circuits; c0 += group) {
+    const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
     hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
-                       total_rows, d_row_begin, c0, usable_rows, count, d_first_bad);
-    hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, count, usable_rows, part);
-    hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, count, usable_rows,
-                       part, pos, dcnt, lp, samp);
+                       total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
+    hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
+    hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
+                       k.part, k.pos, k.dcnt, k.lp, k.samp);
     // permute: ~4096 rows per workgroup
     const uint32_t px = (uint32_t)((usable_rows + 4095) / 4096);
     hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
-                       d_row_begin, c0, usable_rows, k.Tx, k.Ts, mont, d_out, out_rows, ch, num,
-                       den, pos, dcnt, lp, samp);
-    e = gp::run_begin<F>(g, usable_rows, num, den, k.zs + h0 * zse, sticky, sides[slot], s);
+                       d_row_begin, c0, usable_rows, k.Tx, k.Ts, mont, d_out, out_rows, ch, k.num,
+                       k.den, k.pos, k.dcnt, k.lp, k.samp);
+    const uint32_t ga = g > 1 ? g / 2 : g, gb = g - ga;  // halves: circuits [0, ga), [ga, g)
+    auto half = [&](uint32_t h0) {
+      return std::make_tuple(k.num + (uint64_t)h0 * gp::elems(usable_rows),
+                             k.den + (uint64_t)h0 * gp::elems(usable_rows), k.zs + (uint64_t)h0 * zse,
+                             d_out + ((uint64_t)(c0 + h0) * 5 + 4) * out_rows * 4);
+    };
+    auto [na, da, za, oa] = half(0);
+    auto [nb, db, zb, ob] = half(ga);
+    e = gp::run_begin<F>(ga, usable_rows, na, da, za, sticky, sides[0], s);
+    if (e == hipSuccess && gb) e = gp::run_begin<F>(gb, usable_rows, nb, db, zb, sticky, sides[1], s);
+    if (e == hipSuccess)
+      e = gp::run_end<F>(ga, usable_rows, mont, oa, 5 * out_rows * 4, na, da, za, nullptr, nullptr, s,
+                         nullptr, sides[0]);
+    if (e == hipSuccess && gb)
+      e = gp::run_end<F>(gb, usable_rows, mont, ob, 5 * out_rows * 4, nb, db, zb, nullptr, nullptr, s,
+                         nullptr, sides[1]);
     if (e != hipSuccess) return e;
-    if (!pipe) {  // one slot: finish before the next sub-group reuses it
-      if ((e = finish(Pending{c0, g, slot})) != hipSuccess) return e;
-      continue;
-    }
-    if (i > 0 && (e = finish(prev)) != hipSuccess) return e;
-    prev = Pending{c0, g, slot};
   }
-  if (pipe && i > 0 && (e = finish(prev)) != hipSuccess) return e;
   return hipSuccess;
 }
 
