@@ -192,6 +192,7 @@ __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* 
   gp::wave_store_slots<true>(den + sb, stage[wv], lane, d);
 }
 
+constexpr uint32_t PM_CL = 3;  // pm_chunk_kernel's column sets: chunk_len <= 3 (halo2's usual 3)
 // The factors fused with the grand product's chunk pass (replaces pm_factor_kernel + gp_chunk):
 // a lane per 16-row chunk walks its rows -- per row the set's num / den factors as
 // pm_factor_kernel forms them, the running num prefix Nloc written over num and the den factor
@@ -224,21 +225,62 @@ __global__ __launch_bounds__(gp::BLK) void pm_chunk_kernel(Inst I, const uint32_
     const uint64_t wq = __builtin_amdgcn_readfirstlane((uint32_t)(blockIdx.x * gp::BLK + (t & ~63u)));
     const uint64_t rb = q * gp::ZC, re = rb + gp::ZC < usable ? rb + gp::ZC : usable;
     uint32_t ii = inst_of_wave(I, wq * gp::ZC < usable ? wq * gp::ZC : 0, rb < usable ? rb : 0);
+    // the lane's instance context, refreshed when its rows cross an instance start (an instance
+    // has >= 228 rows, so at most once per chunk)
+    uint64_t s_lo = ~0ull, s_hi = ~0ull, pat = 0;
+    if (ii < I.n) {
+      s_lo = I.start[ii];
+      s_hi = I.start[ii + 1];
+      pat = I.pat[ii];
+    }
+    // one row's loads (the set's cells and mapping entries), issued a row ahead of their use:
+    // a lane walks its 16 rows in order, so without the prefetch every row waited for its loads
+    struct RowIn {
+      uint32_t x[PM_CL], m[PM_CL];
+    };
+#define PM_FETCH(v, rr)                                                                          \
+    do {                                                                                         \
+      const uint64_t r_ = (rr);                                                                  \
+      if (r_ >= s_hi && ii < I.n) {                                                              \
+        ii++;                                                                                    \
+        s_lo = s_hi;                                                                             \
+        if (ii < I.n) {                                                                          \
+          s_hi = I.start[ii + 1];                                                                \
+          pat = I.pat[ii];                                                                       \
+        } else {                                                                                 \
+          s_lo = s_hi = ~0ull;                                                                   \
+        }                                                                                        \
+      }                                                                                          \
+      _Pragma("unroll") for (uint32_t jj = 0; jj < PM_CL; jj++) {                                \
+        const uint32_t j_ = j0 + jj < j1 ? j0 + jj : j0;                                         \
+        v.x[jj] = r_ < used ? adv[(uint64_t)(j_ + 1) * total_rows + row0 + r_] : 0u;             \
+        v.m[jj] = ii < I.n ? pool[pat + j_ * (s_hi - s_lo) + (r_ - s_lo)]                        \
+                           : (j_ << ROW_BITS) | 0x1fffffffu;                                     \
+      }                                                                                          \
+    } while (0)
+    RowIn cur;
+    PM_FETCH(cur, rb < usable ? rb : 0);
+    uint64_t cur_lo = s_lo;
 #pragma unroll 1
     for (uint64_t r = rb; r < re; r++) {
-      while (ii < I.n && I.start[ii + 1] <= r) ii++;  // an instance has >= 228 rows: <= 1 step
-      Fe n, d;
-#pragma unroll 1
-      for (uint32_t j = j0; j < j1; j++) {
-        const uint32_t x = r < used ? adv[(uint64_t)(j + 1) * total_rows + row0 + r] : 0u;
-        const Fe vg = field::add<F>(field::from_u32<F>(x), gamma);
-        uint32_t c2;
-        uint64_t r2;
-        mapped(I, pool, ii, j, r, c2, r2);
+      RowIn nxt;
+      PM_FETCH(nxt, r + 1 < re ? r + 1 : r);
+      const uint64_t nxt_lo = s_lo;
+      Fe n = field::one<F>(), d = field::one<F>();
+#pragma unroll
+      for (uint32_t jj = 0; jj < PM_CL; jj++) {
+        const uint32_t j = j0 + jj;
+        if (j >= j1) continue;  // a shorter last set (uniform)
+        const Fe vg = field::add<F>(field::from_u32<F>(cur.x[jj]), gamma);
+        // the mapping entry (c' << 29 | instance-relative r'), or the identity past the instances
+        const uint32_t mm = cur.m[jj];
+        const bool ident_enc = (mm & 0x1fffffffu) == 0x1fffffffu;
+        const uint32_t c2 = ident_enc ? j : mm >> ROW_BITS;
+        const uint64_t r2 = ident_enc ? r : cur_lo + (mm & ((1u << ROW_BITS) - 1));
         const Fe fn = field::add<F>(vg, dw<F>(BL, OH, j, r));
         const Fe fd = (c2 == j && r2 == r) ? fn : field::add<F>(vg, dw<F>(BL, OH, c2, r2));
-        n = j == j0 ? fn : field::mul<F>(n, fn);
-        d = j == j0 ? fd : field::mul<F>(d, fd);
+        n = jj == 0 ? fn : field::mul<F>(n, fn);
+        d = jj == 0 ? fd : field::mul<F>(d, fd);
       }
       pn = r == rb ? n : field::mul<F>(pn, n);
       pd = r == rb ? d : field::mul<F>(pd, d);
@@ -249,7 +291,10 @@ __global__ __launch_bounds__(gp::BLK) void pm_chunk_kernel(Inst I, const uint32_
       gp::nt_store(pnp + 1, make_uint4(pn.w[4], pn.w[5], pn.w[6], pn.w[7]));
       gp::nt_store(dnp, make_uint4(d.w[0], d.w[1], d.w[2], d.w[3]));
       gp::nt_store(dnp + 1, make_uint4(d.w[4], d.w[5], d.w[6], d.w[7]));
+      cur = nxt;
+      cur_lo = nxt_lo;
     }
+#undef PM_FETCH
   }
   gp::block_scan<F>(sn, sd, t, q, nq, nb, set, pn, pd, k.zn, k.zd, k.tn, k.td);
 }
@@ -306,16 +351,19 @@ hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0
   // (set c starts where set c - 1 closed); the sigma columns go between the two halves of the
   // grand product, beside its inversions on the side stream
 #ifdef B2F_PM_SEPARATE  // diagnostics: the factor pass and gp_chunk as two launches
-  hipLaunchKernelGGL(pm_factor_kernel<F>, dim3((uint32_t)((usable + 255) / 256), sets), dim3(256), 0, s,
-                     I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, m.gm, m.num,
-                     m.den);
-  hipError_t e = gp::run_begin<F>(sets, usable, m.num, m.den, m.zs, sticky, side, s);
+  const bool fused = false;
 #else
-  hipLaunchKernelGGL(pm_chunk_kernel<F>, dim3((uint32_t)gp::n_blocks(usable), sets), dim3(gp::BLK), 0, s,
-                     I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, m.gm, m.num,
-                     m.den, m.zs);
-  hipError_t e = gp::run_begin<F>(sets, usable, m.num, m.den, m.zs, sticky, side, s, true);
+  const bool fused = chunk_len <= PM_CL;  // longer column sets: the two-launch form
 #endif
+  if (fused)
+    hipLaunchKernelGGL(pm_chunk_kernel<F>, dim3((uint32_t)gp::n_blocks(usable), sets), dim3(gp::BLK), 0, s,
+                       I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, m.gm, m.num,
+                       m.den, m.zs);
+  else
+    hipLaunchKernelGGL(pm_factor_kernel<F>, dim3((uint32_t)((usable + 255) / 256), sets), dim3(256), 0, s,
+                       I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, m.gm, m.num,
+                       m.den);
+  hipError_t e = gp::run_begin<F>(sets, usable, m.num, m.den, m.zs, sticky, side, s, fused);
   if (e != hipSuccess) return e;
   if (d_sigma)
     hipLaunchKernelGGL(pm_sigma_kernel<F>, dim3((uint32_t)((n_rows + 255) / 256)), dim3(256), 0, s, I,
