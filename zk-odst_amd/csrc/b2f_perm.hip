@@ -193,6 +193,10 @@ __global__ __launch_bounds__(256) void pm_factor_kernel(Inst I, const uint32_t* 
 }
 
 constexpr uint32_t PM_CL = 3;  // pm_chunk_kernel's column sets: chunk_len <= 3 (halo2's usual 3)
+// waves per SIMD pm_chunk_kernel is compiled for: BN254 fits 4 (119 VGPRs, no scratch; 147 at
+// the default budget, 3 waves); pasta's form spills at 128, so it keeps 3
+template <class F> struct PmWaves { static constexpr int v = 3; };
+template <> struct PmWaves<field::Bn254> { static constexpr int v = 4; };
 // The factors fused with the grand product's chunk pass (replaces pm_factor_kernel + gp_chunk):
 // a lane per 16-row chunk walks its rows -- per row the set's num / den factors as
 // pm_factor_kernel forms them, the running num prefix Nloc written over num and the den factor
@@ -200,7 +204,7 @@ constexpr uint32_t PM_CL = 3;  // pm_chunk_kernel's column sets: chunk_len <= 3 
 // factors never make the round trip through HBM that pm_factor_kernel -> gp_chunk took (64
 // bytes written, 64 read and 32 rewritten per row and set).
 template <class F>
-__global__ __launch_bounds__(gp::BLK) void pm_chunk_kernel(Inst I, const uint32_t* __restrict__ pool,
+__global__ __launch_bounds__(gp::BLK) __attribute__((amdgpu_waves_per_eu(PmWaves<F>::v))) void pm_chunk_kernel(Inst I, const uint32_t* __restrict__ pool,
                                                            const uint32_t* __restrict__ adv,
                                                            uint64_t total_rows, uint64_t row0,
                                                            uint64_t usable, uint32_t chunk_len,
