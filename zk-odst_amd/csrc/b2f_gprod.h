@@ -157,10 +157,22 @@ __global__ __launch_bounds__(BLK) void gp_chunk(uint64_t usable, Fe* __restrict_
     const uint64_t b = q * ZC, e = b + ZC < usable ? b + ZC : usable;
     pn = nm[slot_of(b, nq)];  // row b
     pd = dn[slot_of(b, nq)];
+    // the next row's factors are loaded a row ahead (the prefix store to num would otherwise keep
+    // the compiler from hoisting them: same array)
+    Fe an = pn, ad = pd;
+    if (b + 1 < e) {
+      an = nm[slot_of(b + 1, nq)];
+      ad = dn[slot_of(b + 1, nq)];
+    }
     for (uint64_t p = b + 1; p < e; p++) {
       const uint64_t k = slot_of(p, nq);
-      pn = field::mul<F>(pn, nm[k]);
-      pd = field::mul<F>(pd, dn[k]);
+      const Fe cn = an, cd = ad;
+      if (p + 1 < e) {
+        an = nm[slot_of(p + 1, nq)];
+        ad = dn[slot_of(p + 1, nq)];
+      }
+      pn = field::mul<F>(pn, cn);
+      pd = field::mul<F>(pd, cd);
       nm[k] = pn;
     }
   }
@@ -305,15 +317,27 @@ __global__ __launch_bounds__(256) void gp_write(uint64_t usable, bool mont, uint
                       field::mul<F>(zd[(uint64_t)c * nq + q], dinv[c]));
     if (post) k = field::mul<F>(k, post[c]);
   }
+  // row p's Nloc and den are loaded a row ahead of their use (the staging barriers every
+  // GW_ROWS rows would otherwise hold each row's loads until its products)
+  Fe an = field::one<F>(), ad = field::one<F>();
+  if (b + ZC - 1 < e) {
+    an = nm[slot_of(b + ZC - 1, nq)];
+    ad = dn[slot_of(b + ZC - 1, nq)];
+  }
 #pragma unroll 1
   for (int j = ZC - 1; j >= 0; j--) {
     const uint64_t p = b + (uint64_t)j;
+    const Fe cn = an, cd = ad;
+    if (j > 0 && p - 1 < e) {
+      const uint64_t sp = slot_of(p - 1, nq);
+      an = nm[sp];
+      ad = dn[sp];
+    }
     if (p < e) {
-      const uint64_t sl = slot_of(p, nq);
-      const Fe z = out_form<F>(field::mul<F>(nm[sl], k), mont);
+      const Fe z = out_form<F>(field::mul<F>(cn, k), mont);
       stage[wv][lane][2 * (j % GW_ROWS)] = make_uint4(z.w[0], z.w[1], z.w[2], z.w[3]);
       stage[wv][lane][2 * (j % GW_ROWS) + 1] = make_uint4(z.w[4], z.w[5], z.w[6], z.w[7]);
-      if (j > 0) k = field::mul<F>(k, dn[sl]);
+      if (j > 0) k = field::mul<F>(k, cd);
     }
     if (j % GW_ROWS == 0) {  // rows b + j + 1 .. b + j + GW_ROWS of the wave's 64 chunks
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
