@@ -399,16 +399,19 @@ __host__ __device__ inline Scratch scratch_of(Fe* zs, uint32_t g, uint64_t usabl
 // caller launches on `s` between run_begin and run_end overlaps the inversion's ~100 us of
 // latency (the lookup's other half of its circuits, the permutation's sigma columns).
 // chunked: the caller's factor pass already wrote what gp_chunk writes (Nloc over num, zn / zd,
-// tn / td: the permutation's pm_chunk_kernel)
+// tn / td: the permutation's pm_chunk_kernel). have_dinv: the caller computes D^-1 into
+// scratch_of(zs).dt itself, on side.s2, recording side.join when done (the lookup: D from the
+// histogram, before its factor pass) -- only gp_chunk runs here.
 template <class F>
 hipError_t run_begin(uint32_t g, uint64_t usable, Fe* num, const Fe* den, Fe* zs, int* sticky,
-                     Side side, hipStream_t s, bool chunked = false) {
+                     Side side, hipStream_t s, bool chunked = false, bool have_dinv = false) {
   const uint64_t nb = n_blocks(usable);
   const Scratch k = scratch_of(zs, g, usable);
   hipError_t e;
   if (!chunked)
     hipLaunchKernelGGL(gp_chunk<F>, dim3((uint32_t)nb, g), dim3(BLK), 0, s, usable, num, den, k.zn, k.zd,
                        k.tn, k.td);
+  if (have_dinv) return hipGetLastError();
   hipLaunchKernelGGL(gp_total<F>, dim3(g), dim3(TOT_T), 0, s, nb, k.td, k.dt);
   if (side.s2) {
     if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;

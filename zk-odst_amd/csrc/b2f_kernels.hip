@@ -39,8 +39,7 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
                          void* scratch, uint32_t group, int* sticky, hipStream_t s2,
-                         hipEvent_t ev_fork, hipEvent_t ev_join, hipEvent_t ev_fork2,
-                         hipEvent_t ev_join2, hipStream_t s);
+                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s);
 hipError_t launch_spread_table(uint64_t usable_rows, uint32_t form, uint64_t* d_out,
                                uint64_t out_rows, hipStream_t s);
 size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst, uint32_t chunk_len);
@@ -826,7 +825,6 @@ struct b2f_ctx {
   // down-sweep (b2f_gprod.h), forked from and joined back to the caller's stream
   hipStream_t s2;
   hipEvent_t ev_fork, ev_join;
-  hipEvent_t ev_fork2, ev_join2;  // the lookup's second pipelined sub-group
 };
 
 namespace {
@@ -893,8 +891,6 @@ int ensure_side(b2f_ctx* ctx) {
   if (!ctx->s2) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
   if (!ctx->ev_fork) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
   if (!ctx->ev_join) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-  if (!ctx->ev_fork2) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_fork2, hipEventDisableTiming));
-  if (!ctx->ev_join2) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming));
   return B2F_OK;
 }
 
@@ -1106,8 +1102,6 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
   if (ctx->pm_inst_ev) (void)hipEventDestroy(ctx->pm_inst_ev);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-  if (ctx->ev_fork2) (void)hipEventDestroy(ctx->ev_fork2);
-  if (ctx->ev_join2) (void)hipEventDestroy(ctx->ev_join2);
   if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
   (void)hipHostFree(ctx->h_pm_inst);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
@@ -1462,8 +1456,7 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
   int tk = timed_begin(ctx, B2F_KERNEL_LOOKUP, s);
   HIPCHK(ctx, launch_lookup(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, theta, beta,
                             gamma, form, d_out, out_rows, d_first_bad, ctx->d_lk, group,
-                            ctx->d_status + 2, ctx->s2, ctx->ev_fork, ctx->ev_join, ctx->ev_fork2,
-                            ctx->ev_join2, s));
+                            ctx->d_status + 2, ctx->s2, ctx->ev_fork, ctx->ev_join, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }

@@ -27,8 +27,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <tuple>
-
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "../../include/b2f.h"
@@ -43,8 +41,7 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
                          void* scratch, uint32_t group, int* sticky, hipStream_t s2,
-                         hipEvent_t ev_fork, hipEvent_t ev_join, hipEvent_t ev_fork2,
-                         hipEvent_t ev_join2, hipStream_t s);
+                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s);
 
 namespace {
 
@@ -312,6 +309,52 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
   }
 }
 
+// The grand product's den total D, straight from the histogram and before the permute pass: A'
+// is a permutation of A and S' one of S (the leftover items are exactly the table rows no run
+// start took, row 0 with its usable - 2^16 + 1 multiplicity), so prod_p den_p = prod_p num_p =
+// prod_x (Tx[x] + beta)^count[x] (Tx[x] + gamma)^m[x] with m[x] = 1, m[0] = usable - 2^16 + 1.
+// DP_PARTS workgroups per circuit write partial products (gp_total multiplies them, gp_inv
+// inverts D) -- all on the side stream, beside the scans and the permute pass, so no inversion
+// waits in front of gp_write. The product is the same field element whether or not every row is
+// in the table (rows bin by their low 16 bits in both passes), so D = 0 still flags a zero factor.
+constexpr int DP_PARTS = 16, DP_THREADS = 256, DP_PER = TROWS / (DP_PARTS * DP_THREADS);
+template <class F>
+__device__ __forceinline__ Fe pow_small(Fe b, uint32_t e) {  // e >= 1, left to right
+  Fe r = b;
+  for (int i = 30 - __builtin_clz(e); i >= 0; i--) {
+    r = field::mul<F>(r, r);
+    if ((e >> i) & 1u) r = field::mul<F>(r, b);
+  }
+  return r;
+}
+template <class F>
+__global__ __launch_bounds__(DP_THREADS) void lk_dpart_kernel(const Fe* __restrict__ Tx,
+                                                              const uint32_t* __restrict__ count,
+                                                              uint64_t usable, Chal ch, Fe* __restrict__ part) {
+  const uint32_t pt = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
+  const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
+  const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
+  const uint32_t* cnt = count + (uint64_t)c * TROWS;
+  Fe acc = field::one<F>();
+#pragma unroll 2
+  for (int i = 0; i < DP_PER; i++) {
+    const uint32_t x = (pt * DP_PER + i) * DP_THREADS + t;
+    const Fe tx = Tx[x];
+    const uint32_t n = cnt[x];
+    const Fe sg = field::add<F>(tx, gamma);
+    acc = field::mul<F>(acc, x ? sg : pow_small<F>(sg, (uint32_t)(usable - TROWS + 1)));
+    if (n) acc = field::mul<F>(acc, pow_small<F>(field::add<F>(tx, beta), n));
+  }
+  __shared__ Fe sp[DP_THREADS];
+  for (uint32_t w = DP_THREADS / 2; w > 0; w >>= 1) {
+    if (t >= w && t < 2 * w) sp[t] = acc;
+    __syncthreads();
+    if (t < w) acc = field::mul<F>(acc, sp[t + w]);
+    __syncthreads();
+  }
+  if (t == 0) part[(uint64_t)c * DP_PARTS + pt] = acc;
+}
+
 // last index r with a[r] <= v (a nondecreasing over TROWS entries, a[0] <= v): the top 12
 // levels of the search over the workgroup's LDS sample s[k] = a[16 k], then the 16 entries
 // of that block (one 64-byte line, four loads in flight at once) in registers.
@@ -437,6 +480,7 @@ struct Carve {
   Fe* num;  // group x usable
   Fe* den;
   Fe* zs;  // group x gp::scratch_elems
+  Fe* dpart;  // group x DP_PARTS (lk_dpart_kernel)
   void* sort_tmp;
   size_t sort_bytes;
   size_t total;
@@ -473,6 +517,7 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.num = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);  // chunk-interleaved (b2f_gprod.h)
   k.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);
   k.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * group);
+  k.dpart = (Fe*)take(sizeof(Fe) * DP_PARTS * group);
   k.sort_bytes = sort_temp_bytes();
   k.sort_tmp = take(k.sort_bytes);
   k.total = off;
@@ -483,7 +528,7 @@ template <class F>
 hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint64_t* d_row_begin,
                       uint32_t n_circuits, uint64_t usable_rows, const Chal& ch, bool mont,
                       uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad, void* scratch,
-                      uint32_t group, int* sticky, const gp::Side* sides, hipStream_t s) {
+                      uint32_t group, int* sticky, const gp::Side& side, hipStream_t s) {
   Carve k = carve(scratch, group, usable_rows);
   const dim3 tb(TROWS / 256);
   hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm);
@@ -501,16 +546,23 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   hipError_t e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s);
   if (e != hipSuccess) return e;
   // Per group: the count / scan / permute passes over all its circuits at once (a workgroup
-  // count per circuit that fills the chip), then the grand products in two halves, pipelined:
-  // half A's run_begin (chunk passes, D, D^-1 forked to the side stream), half B's run_begin,
-  // half A's run_end, half B's run_end -- each inversion's ~100 us of latency runs beside the
-  // other half's passes instead of in front of its own gp_write. (Pipelining whole sub-groups,
-  // count and permute included, ran the count pass at half the chip: same total, r04l.)
-  const uint64_t zse = gp::scratch_elems(usable_rows);
+  // count per circuit that fills the chip), then the grand products. The den totals' inverses
+  // D^-1 come from the histogram on the side stream (lk_dpart_kernel, gp_total, gp_inv), forked
+  // right after the count pass, so the inversions' latency hides behind the scans and the permute
+  // pass. (r04m: with D taken from the den chunk totals, each half of the group's inversion still
+  // held its gp_write 13-65 us after two-way pipelining, 1.24-1.27 ms per call.)
   for (uint32_t c0 = 0; c0 < n_circuits; c0 += group) {
     const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
+    const gp::Scratch zk = gp::scratch_of(k.zs, g, usable_rows);
     hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
                        total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
+    if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL(lk_dpart_kernel<F>, dim3(DP_PARTS, g), dim3(DP_THREADS), 0, side.s2, k.Tx, k.count,
+                       usable_rows, ch, k.dpart);
+    hipLaunchKernelGGL(gp::gp_total<F>, dim3(g), dim3(gp::TOT_T), 0, side.s2, (uint64_t)DP_PARTS, k.dpart, zk.dt);
+    hipLaunchKernelGGL(gp::gp_inv<F>, dim3(g), dim3(64), 0, side.s2, zk.dt, sticky);
+    if ((e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;
     hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
     hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
                        k.part, k.pos, k.dcnt, k.lp, k.samp);
@@ -519,22 +571,10 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
     hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
                        d_row_begin, c0, usable_rows, k.Tx, k.Ts, mont, d_out, out_rows, ch, k.num,
                        k.den, k.pos, k.dcnt, k.lp, k.samp);
-    const uint32_t ga = g > 1 ? g / 2 : g, gb = g - ga;  // halves: circuits [0, ga), [ga, g)
-    auto half = [&](uint32_t h0) {
-      return std::make_tuple(k.num + (uint64_t)h0 * gp::elems(usable_rows),
-                             k.den + (uint64_t)h0 * gp::elems(usable_rows), k.zs + (uint64_t)h0 * zse,
-                             d_out + ((uint64_t)(c0 + h0) * 5 + 4) * out_rows * 4);
-    };
-    auto [na, da, za, oa] = half(0);
-    auto [nb, db, zb, ob] = half(ga);
-    e = gp::run_begin<F>(ga, usable_rows, na, da, za, sticky, sides[0], s);
-    if (e == hipSuccess && gb) e = gp::run_begin<F>(gb, usable_rows, nb, db, zb, sticky, sides[1], s);
+    e = gp::run_begin<F>(g, usable_rows, k.num, k.den, k.zs, sticky, side, s, false, true);
     if (e == hipSuccess)
-      e = gp::run_end<F>(ga, usable_rows, mont, oa, 5 * out_rows * 4, na, da, za, nullptr, nullptr, s,
-                         nullptr, sides[0]);
-    if (e == hipSuccess && gb)
-      e = gp::run_end<F>(gb, usable_rows, mont, ob, 5 * out_rows * 4, nb, db, zb, nullptr, nullptr, s,
-                         nullptr, sides[1]);
+      e = gp::run_end<F>(g, usable_rows, mont, d_out + ((uint64_t)c0 * 5 + 4) * out_rows * 4, 5 * out_rows * 4,
+                         k.num, k.den, k.zs, nullptr, nullptr, s, nullptr, side);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -551,9 +591,8 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
                          void* scratch, uint32_t group, int* sticky, hipStream_t s2,
-                         hipEvent_t ev_fork, hipEvent_t ev_join, hipEvent_t ev_fork2,
-                         hipEvent_t ev_join2, hipStream_t s) {
-  const gp::Side sides[2] = {{s2, ev_fork, ev_join}, {s2, ev_fork2, ev_join2}};
+                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s) {
+  const gp::Side side{s2, ev_fork, ev_join};
   Chal ch;
   for (int i = 0; i < 4; i++) {
     ch.theta[i] = theta[i];
@@ -563,9 +602,9 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
   const bool mont = (form & 1u) != 0;
   if (form >> 1)
     return run_lookup<field::Bn254>(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, ch,
-                                    mont, d_out, out_rows, d_first_bad, scratch, group, sticky, sides, s);
+                                    mont, d_out, out_rows, d_first_bad, scratch, group, sticky, side, s);
   return run_lookup<field::Pallas>(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, ch,
-                                   mont, d_out, out_rows, d_first_bad, scratch, group, sticky, sides, s);
+                                   mont, d_out, out_rows, d_first_bad, scratch, group, sticky, side, s);
 }
 
 }  // namespace b2f
