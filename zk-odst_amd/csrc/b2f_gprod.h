@@ -257,6 +257,10 @@ template <class F>
 __global__ __launch_bounds__(64) void gp_inv(Fe* __restrict__ dt, int* __restrict__ sticky) {
   const uint32_t c = blockIdx.x;
   if (threadIdx.x != 0) return;
+  // the inversion is one lane's serial chain beside whole-chip passes on the other stream: top
+  // issue priority on its SIMD (r04m: BN254 469 us beside the sigma pass, pasta 190-208 beside
+  // the lookup's passes, ~110-125 alone)
+  __builtin_amdgcn_s_setprio(3);
   const Fe D = dt[c];
   if (sticky && field::is_zero(D)) atomicOr(sticky, 1 << B2F_ERR_FIELD);
 #ifdef B2F_INV_EUCLID  // diagnostics: the plain binary extended Euclid
