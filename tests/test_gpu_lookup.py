@@ -158,12 +158,12 @@ def test_spread_table_columns(engine, form):
         assert np.array_equal(got[c], want), c
 
 
-@pytest.mark.parametrize("form", [1, 3])
-def test_lookup_zero_factor_reported_then_clean(engine, trace, form):
-    """beta = -A[row] makes (A + beta) and (A' + beta) zero for that row's value, so
-    the den total is zero: the call reports B2F_ERR_FIELD at b2f_sync (three-level grand product,
-    inversion on the side stream), and the next call with sound challenges syncs clean and
-    matches the oracle's closing value."""
+@pytest.mark.parametrize("form,which", [(1, "beta"), (3, "beta"), (1, "gamma")])
+def test_lookup_zero_factor_reported_then_clean(engine, trace, form, which):
+    """beta = -A[row] makes (A + beta) and (A' + beta) zero for that row's value, and
+    gamma = -T[x] makes (S + gamma) and (S' + gamma) zero for table row x, so the den total is
+    zero: the call reports B2F_ERR_FIELD at b2f_sync (D from the histogram, inversion on the side
+    stream), and the next call with sound challenges syncs clean and closes to one."""
     import lookup as lk
     import torch
 
@@ -177,11 +177,18 @@ def test_lookup_zero_factor_reported_then_clean(engine, trace, form):
     row = 1234
     a = lk.compress(theta, int(adv[0, row]), int(adv[1, row]), int(adv[2, row]), p)
     beta = (p - a) % p
+    if which == "gamma":  # table row 40,000 (not necessarily among the inputs)
+        _, beta, _ = _chal(19, form)
+        x = 40000
+        gamma = (p - lk.compress(theta, lk.tag(x), x, lk.spread(x), p)) % p
     out, bad = trace.lookup_columns(engine, [0], usable, theta, beta, gamma, form=form)
     with pytest.raises(b2f.B2FError) as e:
         engine.sync(s)
     assert e.value.code == b2f._lib.ERR_FIELD
-    beta = (beta + 1) % p
+    if which == "gamma":
+        gamma = (gamma + 1) % p
+    else:
+        beta = (beta + 1) % p
     out, bad = trace.lookup_columns(engine, [0], usable, theta, beta, gamma, form=form)
     engine.sync(s)
     z = _col_ints(out[0, 4, usable:usable + 1])[0]
@@ -189,10 +196,10 @@ def test_lookup_zero_factor_reported_then_clean(engine, trace, form):
     assert z == one  # a valid lookup closes to 1
 
 
-def test_lookup_pipelined_subgroups_equal_oracle(engine, trace):
-    """Five circuits in one call: the grand products run in pipelined sub-groups of two
-    (scratch slots 0, 1, 0; each sub-group's inversion beside the next one's passes). Every
-    circuit's five columns equal the restatement, BN254 Montgomery form."""
+def test_lookup_group_of_circuits_equal_oracle(engine, trace):
+    """Five circuits in one call, one group: each circuit's D^-1 comes from its histogram on the
+    side stream (lk_dpart_kernel) while the permute pass runs, and one grand product covers the
+    group. Every circuit's five columns equal the restatement, BN254 Montgomery form."""
     import lookup as lk
     import torch
 
@@ -214,3 +221,25 @@ def test_lookup_pipelined_subgroups_equal_oracle(engine, trace):
             got = _col_ints(out[c, j, :n])
             want = [v * R256 % p for v in ref[j]]
             assert got == want, (c, j)
+
+
+def test_lookup_two_groups_equal_within_call(engine, trace):
+    """More circuits than one group holds (1 GiB of scratch per group: 15 circuits of 2^20 rows),
+    so the call loops over two groups, each forking its own D^-1 chain to the side stream after
+    its count pass and reusing the count / D scratch of the group before. Circuit 16 (group 2)
+    repeats circuit 5's rows (group 1): all five columns bit-identical, and every z closes to one
+    (Montgomery form). A group that read the previous group's counts or D^-1 would differ."""
+    import torch
+
+    form = 1
+    usable = 1 << 20
+    begins = [i * 8000 for i in range(16)] + [5 * 8000]  # inside the 135,720-row trace
+    theta, beta, gamma = _chal(31, form)
+    out, bad = trace.lookup_columns(engine, begins, usable, theta, beta, gamma, form=form)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    assert (bad.cpu().numpy().view(np.uint64) == np.uint64(2**64 - 1)).all()
+    one = R256 % _mod(form)
+    for c in range(len(begins)):
+        assert _col_ints(out[c, 4, usable:usable + 1])[0] == one, c
+    assert torch.equal(out[16], out[5])
+    assert not torch.equal(out[16, 2], out[4, 2])
