@@ -309,41 +309,44 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
   }
 }
 
-// The grand product's den total D, straight from the histogram and before the permute pass: A'
-// is a permutation of A and S' one of S (the leftover items are exactly the table rows no run
-// start took, row 0 with its usable - 2^16 + 1 multiplicity), so prod_p den_p = prod_p num_p =
-// prod_x (Tx[x] + beta)^count[x] (Tx[x] + gamma)^m[x] with m[x] = 1, m[0] = usable - 2^16 + 1.
-// DP_PARTS workgroups per circuit write partial products (gp_total multiplies them, gp_inv
-// inverts D) -- all on the side stream, beside the scans and the permute pass, so no inversion
-// waits in front of gp_write. The product is the same field element whether or not every row is
-// in the table (rows bin by their low 16 bits in both passes), so D = 0 still flags a zero factor.
-constexpr int DP_PARTS = 16, DP_THREADS = 256, DP_PER = TROWS / (DP_PARTS * DP_THREADS);
+// The grand product's den total D before the permute pass: A' is a permutation of A and S' one
+// of S (the leftover items are exactly the table rows no run start took, row 0 with its
+// usable - 2^16 + 1 multiplicity), so D = prod_p den_p = prod_p num_p = prod_p (A_p + beta) *
+// prod_p (S_p + gamma). lk_dtot_kernel forms both from the rows -- A_p = Tx[dense cell] and
+// S_p = Tx[p] (row 0's value past the table) -- one product per row: workgroups (pt, c < g) the
+// A part of circuit c, workgroups (pt, g) the S part (the same for every circuit); lk_dinv
+// multiplies the partial products and inverts D. All on the side stream, beside the count, scan
+// and permute passes, so no inversion waits in front of gp_write. (A power per histogram bin,
+// (Tx[x] + beta)^count[x], ran lanes of one wave through different exponents: 362 us beside
+// the permute pass, r04n.) Rows bin by their low 16 bits in every pass, so the identity holds
+// whether or not every row is in the table, and D = 0 still flags a zero factor.
+constexpr int DP_PARTS = 16, DP_THREADS = 256;
 template <class F>
-__device__ __forceinline__ Fe pow_small(Fe b, uint32_t e) {  // e >= 1, left to right
-  Fe r = b;
-  for (int i = 30 - __builtin_clz(e); i >= 0; i--) {
-    r = field::mul<F>(r, r);
-    if ((e >> i) & 1u) r = field::mul<F>(r, b);
-  }
-  return r;
-}
-template <class F>
-__global__ __launch_bounds__(DP_THREADS) void lk_dpart_kernel(const Fe* __restrict__ Tx,
-                                                              const uint32_t* __restrict__ count,
-                                                              uint64_t usable, Chal ch, Fe* __restrict__ part) {
+__global__ __launch_bounds__(DP_THREADS) void lk_dtot_kernel(const uint32_t* __restrict__ adv, uint64_t total_rows,
+                                                             const uint64_t* __restrict__ row_begin, uint32_t c0,
+                                                             uint32_t g, uint64_t usable, const Fe* __restrict__ Tx,
+                                                             Chal ch, Fe* __restrict__ part) {
   const uint32_t pt = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
-  const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
-  const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
-  const uint32_t* cnt = count + (uint64_t)c * TROWS;
+  const bool s_part = c == g;
+  const Fe add = field::to_mont<F>(field::load_words(s_part ? ch.gamma : ch.beta));
+  const Circ k = s_part ? Circ{0, 0} : circ(row_begin, total_rows, usable, c0 + c);
+  const uint64_t per = (usable + DP_PARTS - 1) / DP_PARTS;
+  const uint64_t b = (uint64_t)pt * per, e = b + per < usable ? b + per : usable;
   Fe acc = field::one<F>();
-#pragma unroll 2
-  for (int i = 0; i < DP_PER; i++) {
-    const uint32_t x = (pt * DP_PER + i) * DP_THREADS + t;
-    const Fe tx = Tx[x];
-    const uint32_t n = cnt[x];
-    const Fe sg = field::add<F>(tx, gamma);
-    acc = field::mul<F>(acc, x ? sg : pow_small<F>(sg, (uint32_t)(usable - TROWS + 1)));
-    if (n) acc = field::mul<F>(acc, pow_small<F>(field::add<F>(tx, beta), n));
+  // four rows per step: their cell and table loads issued together, then two independent products
+  for (uint64_t p = b + t; p < e; p += 4 * DP_THREADS) {
+    uint32_t x[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint64_t q = p + (uint64_t)u * DP_THREADS;
+      x[u] = s_part ? (q < (uint64_t)TROWS ? (uint32_t)q : 0u)
+                    : (q < k.n_in ? (adv[total_rows + k.first + q] & 0xffffu) : 0u);
+    }
+    Fe v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      v[u] = p + (uint64_t)u * DP_THREADS < e ? field::add<F>(Tx[x[u]], add) : field::one<F>();
+    acc = field::mul<F>(acc, field::mul<F>(field::mul<F>(v[0], v[1]), field::mul<F>(v[2], v[3])));
   }
   __shared__ Fe sp[DP_THREADS];
   for (uint32_t w = DP_THREADS / 2; w > 0; w >>= 1) {
@@ -353,6 +356,25 @@ __global__ __launch_bounds__(DP_THREADS) void lk_dpart_kernel(const Fe* __restri
     __syncthreads();
   }
   if (t == 0) part[(uint64_t)c * DP_PARTS + pt] = acc;
+}
+// D_c = prod_i (A part i of c) (S part i), a tree over the DP_PARTS pairs, then D^-1 in place (one
+// lane: gp::gp_inv's zero check and issue priority)
+template <class F>
+__global__ __launch_bounds__(DP_PARTS) void lk_dinv_kernel(const Fe* __restrict__ part, uint32_t g,
+                                                           Fe* __restrict__ dt, int* __restrict__ sticky) {
+  const uint32_t c = blockIdx.x, t = threadIdx.x;
+  __shared__ Fe sp[DP_PARTS];
+  Fe d = field::mul<F>(part[(uint64_t)c * DP_PARTS + t], part[(uint64_t)g * DP_PARTS + t]);
+  for (uint32_t w = DP_PARTS / 2; w > 0; w >>= 1) {
+    if (t >= w && t < 2 * w) sp[t] = d;
+    __syncthreads();
+    if (t < w) d = field::mul<F>(d, sp[t + w]);
+    __syncthreads();
+  }
+  if (t != 0) return;
+  __builtin_amdgcn_s_setprio(3);
+  if (sticky && field::is_zero(d)) atomicOr(sticky, 1 << B2F_ERR_FIELD);
+  dt[c] = field::inv_kaliski<F>(d);
 }
 
 // last index r with a[r] <= v (a nondecreasing over TROWS entries, a[0] <= v): the top 12
@@ -480,7 +502,7 @@ struct Carve {
   Fe* num;  // group x usable
   Fe* den;
   Fe* zs;  // group x gp::scratch_elems
-  Fe* dpart;  // group x DP_PARTS (lk_dpart_kernel)
+  Fe* dpart;  // (group + 1) x DP_PARTS (lk_dtot_kernel)
   void* sort_tmp;
   size_t sort_bytes;
   size_t total;
@@ -517,7 +539,7 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.num = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);  // chunk-interleaved (b2f_gprod.h)
   k.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);
   k.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * group);
-  k.dpart = (Fe*)take(sizeof(Fe) * DP_PARTS * group);
+  k.dpart = (Fe*)take(sizeof(Fe) * DP_PARTS * (group + 1));
   k.sort_bytes = sort_temp_bytes();
   k.sort_tmp = take(k.sort_bytes);
   k.total = off;
@@ -547,22 +569,22 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   if (e != hipSuccess) return e;
   // Per group: the count / scan / permute passes over all its circuits at once (a workgroup
   // count per circuit that fills the chip), then the grand products. The den totals' inverses
-  // D^-1 come from the histogram on the side stream (lk_dpart_kernel, gp_total, gp_inv), forked
-  // right after the count pass, so the inversions' latency hides behind the scans and the permute
-  // pass. (r04m: with D taken from the den chunk totals, each half of the group's inversion still
-  // held its gp_write 13-65 us after two-way pipelining, 1.24-1.27 ms per call.)
+  // D^-1 come from the rows on the side stream (lk_dtot_kernel, lk_dinv_kernel), forked at the
+  // group's start (after the previous group's gp_write, which read the same D^-1 slots), so the
+  // inversions' latency hides behind the count, scan and permute passes. (r04m: with D taken from
+  // the den chunk totals, each half of the group's inversion still held its gp_write 25-52 us
+  // after two-way pipelining, 1.24-1.27 ms per call.)
   for (uint32_t c0 = 0; c0 < n_circuits; c0 += group) {
     const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
     const gp::Scratch zk = gp::scratch_of(k.zs, g, usable_rows);
-    hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
-                       total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
     if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL(lk_dpart_kernel<F>, dim3(DP_PARTS, g), dim3(DP_THREADS), 0, side.s2, k.Tx, k.count,
-                       usable_rows, ch, k.dpart);
-    hipLaunchKernelGGL(gp::gp_total<F>, dim3(g), dim3(gp::TOT_T), 0, side.s2, (uint64_t)DP_PARTS, k.dpart, zk.dt);
-    hipLaunchKernelGGL(gp::gp_inv<F>, dim3(g), dim3(64), 0, side.s2, zk.dt, sticky);
+    hipLaunchKernelGGL(lk_dtot_kernel<F>, dim3(DP_PARTS, g + 1), dim3(DP_THREADS), 0, side.s2, d_advice,
+                       total_rows, d_row_begin, c0, g, usable_rows, k.Tx, ch, k.dpart);
+    hipLaunchKernelGGL(lk_dinv_kernel<F>, dim3(g), dim3(DP_PARTS), 0, side.s2, k.dpart, g, zk.dt, sticky);
     if ((e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;
+    hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
+                       total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
     hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
     hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
                        k.part, k.pos, k.dcnt, k.lp, k.samp);
