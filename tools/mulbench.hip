@@ -139,6 +139,16 @@ int main() {
   }
   RUN(Pallas, 0, 1) RUN(Pallas, 0, 2) RUN(Pallas, 1, 1) RUN(Pallas, 1, 2) RUN(Pallas, 2, 1) RUN(Pallas, 2, 2)
   RUN(Bn254, 0, 1) RUN(Bn254, 0, 2) RUN(Bn254, 1, 1) RUN(Bn254, 1, 2) RUN(Bn254, 2, 1) RUN(Bn254, 2, 2)
+  // the same kernels with their workgroups per CU capped by dynamic LDS (48 KiB: 3 per CU = 3 waves
+  // per SIMD, as pm_chunk_kernel runs; 64 KiB: 2): does a second independent chain per lane (ILP)
+  // recover what fewer waves lose?
+#define RUNL(F, V, CH, KB)                                                                        \
+  {                                                                                               \
+    float ms = timeit([&] { hipLaunchKernelGGL((k<F, V, CH>), dim3(blocks), dim3(256), KB * 1024, 0, in, out, n); }); \
+    printf("%-7s variant %d chains %d lds %2d KiB: %.3f ms, %.2f G products/s\n", #F, V, CH, KB, ms, prods * CH / ms / 1e6); \
+  }
+  RUNL(Pallas, 0, 1, 48) RUNL(Pallas, 0, 2, 48) RUNL(Pallas, 0, 1, 64) RUNL(Pallas, 0, 2, 64)
+  RUNL(Bn254, 0, 1, 48) RUNL(Bn254, 0, 2, 48) RUNL(Bn254, 0, 1, 64) RUNL(Bn254, 0, 2, 64)
   {
     uint32_t* bad;
     hipMalloc(&bad, 8);
