@@ -56,6 +56,91 @@ __device__ __forceinline__ Fe mul2(const Fe& a, const Fe& b) {
   return reduce_once<F>(o);
 }
 
+// Two independent products interleaved inside each asm block (ILP in one wave): product A carries
+// through vcc, product B through an SGPR pair the compiler picks
+__device__ __forceinline__ void x2_madd2(uint64_t& aa, uint32_t& oa, uint64_t& ab, uint32_t& ob, uint32_t xa0,
+                                         uint32_t ya0, uint32_t xa1, uint32_t xb0, uint32_t yb0, uint32_t xb1,
+                                         uint32_t y1) {
+  uint64_t cb;
+  asm("v_mad_u64_u32 %0, vcc, %5, %6, %0\n\t"
+      "v_mad_u64_u32 %1, %4, %8, %9, %1\n\t"
+      "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
+      "v_addc_co_u32_e64 %3, %4, 0, %3, %4\n\t"
+      "v_mad_u64_u32 %0, vcc, %7, %11, %0\n\t"
+      "v_mad_u64_u32 %1, %4, %10, %11, %1\n\t"
+      "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
+      "v_addc_co_u32_e64 %3, %4, 0, %3, %4"
+      : "+v"(aa), "+v"(ab), "+v"(oa), "+v"(ob), "=&s"(cb)
+      : "v"(xa0), "v"(ya0), "v"(xa1), "v"(xb0), "v"(yb0), "v"(xb1), "s"(y1)
+      : "vcc");
+}
+__device__ __forceinline__ void x2_madd1(uint64_t& aa, uint32_t& oa, uint64_t& ab, uint32_t& ob, uint32_t xa,
+                                         uint32_t ya, uint32_t xb, uint32_t yb) {
+  uint64_t cb;
+  asm("v_mad_u64_u32 %0, vcc, %5, %6, %0\n\t"
+      "v_mad_u64_u32 %1, %4, %7, %8, %1\n\t"
+      "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
+      "v_addc_co_u32_e64 %3, %4, 0, %3, %4"
+      : "+v"(aa), "+v"(ab), "+v"(oa), "+v"(ob), "=&s"(cb)
+      : "v"(xa), "v"(ya), "v"(xb), "v"(yb)
+      : "vcc");
+}
+__device__ __forceinline__ void x2_maddc(uint64_t& aa, uint32_t& oa, uint64_t& ab, uint32_t& ob, uint32_t xa,
+                                         uint32_t xb, uint32_t y) {  // y uniform
+  uint64_t cb;
+  asm("v_mad_u64_u32 %0, vcc, %5, %7, %0\n\t"
+      "v_mad_u64_u32 %1, %4, %6, %7, %1\n\t"
+      "v_addc_co_u32_e32 %2, vcc, 0, %2, vcc\n\t"
+      "v_addc_co_u32_e64 %3, %4, 0, %3, %4"
+      : "+v"(aa), "+v"(ab), "+v"(oa), "+v"(ob), "=&s"(cb)
+      : "v"(xa), "v"(xb), "s"(y)
+      : "vcc");
+}
+template <class F>
+__device__ __forceinline__ void mul_x2(const Fe& a, const Fe& b, const Fe& c, const Fe& d, Fe& oa, Fe& oc) {
+  uint32_t ma[8], mc[8], ra[8], rc[8];
+  uint64_t A = 0, C = 0;
+  uint32_t va = 0, vc = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#pragma unroll
+    for (int i = 0; i < k; i++) {
+      if (F::P[k - i]) x2_madd2(A, va, C, vc, a.w[i], b.w[k - i], ma[i], c.w[i], d.w[k - i], mc[i], F::P[k - i]);
+      else x2_madd1(A, va, C, vc, a.w[i], b.w[k - i], c.w[i], d.w[k - i]);
+    }
+    x2_madd1(A, va, C, vc, a.w[k], b.w[0], c.w[k], d.w[0]);
+    ma[k] = (uint32_t)A * F::NP;
+    mc[k] = (uint32_t)C * F::NP;
+    x2_maddc(A, va, C, vc, ma[k], mc[k], F::P[0]);
+    A = (A >> 32) | ((uint64_t)va << 32);
+    C = (C >> 32) | ((uint64_t)vc << 32);
+    va = vc = 0;
+  }
+#pragma unroll
+  for (int k = 8; k < 15; k++) {
+#pragma unroll
+    for (int i = k - 7; i < 8; i++) {
+      if (F::P[k - i]) x2_madd2(A, va, C, vc, a.w[i], b.w[k - i], ma[i], c.w[i], d.w[k - i], mc[i], F::P[k - i]);
+      else x2_madd1(A, va, C, vc, a.w[i], b.w[k - i], c.w[i], d.w[k - i]);
+    }
+    ra[k - 8] = (uint32_t)A;
+    rc[k - 8] = (uint32_t)C;
+    A = (A >> 32) | ((uint64_t)va << 32);
+    C = (C >> 32) | ((uint64_t)vc << 32);
+    va = vc = 0;
+  }
+  ra[7] = (uint32_t)A;
+  rc[7] = (uint32_t)C;
+  Fe x, y;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    x.w[j] = ra[j];
+    y.w[j] = rc[j];
+  }
+  oa = reduce_once<F>(x);
+  oc = reduce_once<F>(y);
+}
+
 // mul (b2f_field.h, product scanning) vs mul_cios (the operand-scanning form it replaced) on
 // pseudo-random operands below p (top word reduced mod p's top word) and on 0, 1, p - 1: count of
 // differing products
@@ -76,8 +161,10 @@ __global__ void check(uint32_t* bad, int n) {
       if (threadIdx.x & 2u) b = a;
     }
     const Fe x = mul<F>(a, b), y = mul_cios<F>(a, b), z = mul2<F>(a, b);
+    Fe u, v;
+    mul_x2<F>(a, b, b, a, u, v);
     uint32_t d = 0;
-    for (int i = 0; i < 8; i++) d |= (x.w[i] ^ y.w[i]) | (z.w[i] ^ y.w[i]);
+    for (int i = 0; i < 8; i++) d |= (x.w[i] ^ y.w[i]) | (z.w[i] ^ y.w[i]) | (u.w[i] ^ y.w[i]) | (v.w[i] ^ y.w[i]);
     if (d) atomicAdd(bad, 1u);
   }
 }
@@ -88,9 +175,15 @@ __global__ __launch_bounds__(256) void k(const Fe* in, Fe* out, int n) {
 #pragma unroll
   for (int c = 0; c < CH; c++) acc[c] = in[(threadIdx.x + c) & 255];
   const Fe b = in[256 + (blockIdx.x & 15)];
-  for (int i = 0; i < n; i++)
+  for (int i = 0; i < n; i++) {
+    if (V == 3) {
 #pragma unroll
-    for (int c = 0; c < CH; c++) acc[c] = V == 0 ? mul<F>(acc[c], b) : V == 1 ? mul_cios<F>(acc[c], b) : mul2<F>(acc[c], b);
+      for (int c = 0; c + 1 < CH; c += 2) mul_x2<F>(acc[c], b, acc[c + 1], b, acc[c], acc[c + 1]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < CH; c++) acc[c] = V == 0 ? mul<F>(acc[c], b) : V == 1 ? mul_cios<F>(acc[c], b) : mul2<F>(acc[c], b);
+    }
+  }
   Fe s = acc[0];
 #pragma unroll
   for (int c = 1; c < CH; c++) s = add<F>(s, acc[c]);
@@ -149,6 +242,9 @@ int main() {
   }
   RUNL(Pallas, 0, 1, 48) RUNL(Pallas, 0, 2, 48) RUNL(Pallas, 0, 1, 64) RUNL(Pallas, 0, 2, 64)
   RUNL(Bn254, 0, 1, 48) RUNL(Bn254, 0, 2, 48) RUNL(Bn254, 0, 1, 64) RUNL(Bn254, 0, 2, 64)
+  // variant 3: the two chains of a lane through mul_x2 (interleaved in each asm block)
+  RUN(Pallas, 3, 2) RUN(Bn254, 3, 2)
+  RUNL(Pallas, 3, 2, 48) RUNL(Pallas, 3, 2, 64) RUNL(Bn254, 3, 2, 48) RUNL(Bn254, 3, 2, 64)
   {
     uint32_t* bad;
     hipMalloc(&bad, 8);
@@ -157,7 +253,7 @@ int main() {
     hipLaunchKernelGGL(check<Bn254>, dim3(1024), dim3(256), 0, 0, bad + 1, 16);
     uint32_t h[2];
     hipMemcpy(h, bad, 8, hipMemcpyDeviceToHost);
-    printf("mul / mul2 (product scanning) vs mul_cios mismatches over 4.2M products: pallas %u bn254 %u\n", h[0], h[1]);
+    printf("mul / mul2 / mul_x2 (product scanning) vs mul_cios mismatches over 4.2M products: pallas %u bn254 %u\n", h[0], h[1]);
   }
   {
     float ms = timeit([&] { hipLaunchKernelGGL(madk, dim3(blocks), dim3(256), 0, 0, (uint64_t*)out, 1024); });
