@@ -352,20 +352,8 @@ hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0
   hipLaunchKernelGGL(pm_table_kernel<F>, dim3((uint32_t)((tab + 255) / 256)), dim3(256), 0, s, prm,
                      n_hi, m.OL, m.BL, m.OH, m.gm);
   // every column set's factors in one launch, then their grand products side by side, chained
-  // (set c starts where set c - 1 closed). The sigma columns (stores, independent of z) run on the
-  // side stream from here, beside the factor pass (products), and the inversions follow them
-  // there; run_end's join covers both. (Between the grand product's halves, beside the
-  // inversions, they made the inversions' 450 us on the critical path instead: r04n.)
-  hipError_t e;
-  if (d_sigma) {
-    hipStream_t ss = side.s2 ? side.s2 : s;
-    if (side.s2) {
-      if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(pm_sigma_kernel<F>, dim3((uint32_t)((n_rows + 255) / 256)), dim3(256), 0, ss, I,
-                       d_pool, n_rows, m.OL, m.OH, mont, d_sigma, out_rows);
-  }
+  // (set c starts where set c - 1 closed); the sigma columns go between the two halves of the
+  // grand product, beside its inversions on the side stream
 #ifdef B2F_PM_SEPARATE  // diagnostics: the factor pass and gp_chunk as two launches
   const bool fused = false;
 #else
@@ -379,8 +367,11 @@ hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0
     hipLaunchKernelGGL(pm_factor_kernel<F>, dim3((uint32_t)((usable + 255) / 256), sets), dim3(256), 0, s,
                        I, d_pool, d_advice, total_rows, row0, usable, chunk_len, m.BL, m.OH, m.gm, m.num,
                        m.den);
-  e = gp::run_begin<F>(sets, usable, m.num, m.den, m.zs, sticky, side, s, fused);
+  hipError_t e = gp::run_begin<F>(sets, usable, m.num, m.den, m.zs, sticky, side, s, fused);
   if (e != hipSuccess) return e;
+  if (d_sigma)
+    hipLaunchKernelGGL(pm_sigma_kernel<F>, dim3((uint32_t)((n_rows + 255) / 256)), dim3(256), 0, s, I,
+                       d_pool, n_rows, m.OL, m.OH, mont, d_sigma, out_rows);
   e = gp::run_end<F>(sets, usable, mont, d_z, out_rows * 4, m.num, m.den, m.zs, nullptr, nullptr, s,
                      m.seed, side);
   if (e != hipSuccess) return e;
