@@ -33,11 +33,11 @@ sys.path.insert(0, os.path.join(ROOT, "zk-odst_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # The prover columns are bound by 256-bit Montgomery products: tools/mulbench.hip measures the
 # product b2f_field.h uses (product scanning, two word products per asm block, round 4) at up to
-# 150-152 G products/s chip-wide in pasta Fp and 129 in BN254 Fr (profiles/r04l_mulbench.txt,
-# r04n_mulbench.txt: the best of its variants of the same code; the CIOS form before it: 114 / 105).
-# Products per row: lookup = 2 (permute: num, den factors) + 4 (grand product); permutation:
-# counted per call from the circuit's copy cycles (the permutation leg below).
-MULBENCH_GPS = {"pallas": 151.0, "bn254": 129.0}
+# 158 G products/s chip-wide in pasta Fp and 129 in BN254 Fr (profiles/r04o_mulbench.txt: the best
+# of its variants and occupancies for the same code -- 3 waves per SIMD is as fast as 8; the CIOS
+# form before it: 114 / 105). Products per row: lookup = 2 (permute: num, den factors) + 4 (grand
+# product); permutation: counted per call from the circuit's copy cycles (the permutation leg).
+MULBENCH_GPS = {"pallas": 158.0, "bn254": 129.5}
 LOOKUP_PRODUCTS_PER_ROW = 6
 # 1 in BN254 Fr Montgomery form (R mod r) as four little-endian int64 limbs
 FR_ONE_MONT = [int.from_bytes((0x0e0a77c19a07df2f666ea36f7879462e36fc76959f60cd29ac96341c4ffffffb
