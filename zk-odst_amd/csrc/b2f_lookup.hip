@@ -8,9 +8,9 @@
 // is a table row, so the sort is a counting sort over the 2^16 table rows in the order of
 // their compressed values:
 //   table pass (once per theta): T[x] = theta^2 tag(x) + theta x + spread(x) for x < 2^16,
-//     sorted by canonical value (buckets of the top 64-bit limb, each sorted in LDS by a
-//     workgroup, ties of the top limb -- about 2^-33 likely -- ordered by the lower limbs),
-//     giving the rank order x_of_rank[r] and Ts[r] = T[x_of_rank[r]];
+//     sorted by canonical value (one radix sort by the top 64-bit limb, ties -- about 2^-33
+//     likely -- ordered by the lower limbs), giving the rank order x_of_rank[r] and
+//     Ts[r] = T[x_of_rank[r]];
 //   count:   histogram of the dense cell (a_1) over the circuit's rows (LDS-privatised, four
 //            workgroups per circuit, a quarter of the bins each), with the row check (tag,
 //            dense, spread) in table (first failing row reported);
@@ -26,6 +26,8 @@
 //            inversion per circuit, 4 products per row) writes the z column.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "../../include/b2f.h"
 #include "b2f_field.h"
@@ -66,7 +68,8 @@ __device__ __forceinline__ uint32_t tag16(uint32_t x) { return x < 256u ? 0u : (
 // ------------------------------------------------------------------ table pass (per theta)
 template <class F>
 __global__ __launch_bounds__(256) void lk_table_kernel(Chal ch, Fe* __restrict__ Tx,
-                                                       uint64_t* __restrict__ key) {
+                                                       uint64_t* __restrict__ key,
+                                                       uint32_t* __restrict__ perm) {
   const uint32_t x = blockIdx.x * 256 + threadIdx.x;
   const Fe th = field::to_mont<F>(field::load_words(ch.theta));
   const Fe th2 = field::mul<F>(th, th);
@@ -78,108 +81,44 @@ __global__ __launch_bounds__(256) void lk_table_kernel(Chal ch, Fe* __restrict__
 #pragma unroll
   for (int k = 0; k < 4; k++)
     key[(uint64_t)k * TROWS + x] = (uint64_t)c.w[2 * k] | ((uint64_t)c.w[2 * k + 1] << 32);
+  perm[x] = x;
 }
 
-// The rank order of the 2^16 table values (x_of_rank, and Ts[r] = Tx[x_of_rank[r]]) in one
-// launch: workgroup b owns the values whose top 64-bit limb falls in bucket b (the limb's top 8
-// bits below the modulus' top limb; the canonical values are spread uniformly, ~256 per bucket).
-// Each workgroup reads all 2^16 top limbs once (512 KiB from L2), counting every bucket in LDS
-// (its output offset is the count of the buckets before it) and collecting its own members, then
-// sorts them with a bitonic network in LDS by (top limb, the three lower limbs, x) -- the lower
-// limbs read only on a tie of the top limbs (about 2^-33 likely) -- and writes its ranks. This is
-// the order a stable sort by the full 256-bit value gives. A bucket over SB_CAP members (only a
-// pathological theta) takes a quadratic count of smaller members instead: slow, still exact.
-// (A rocprim radix sort by the top limb, a tie fix and a rank gather took 86 us per call, r04o.)
-constexpr int SB_BUCKETS = 256, SB_THREADS = 256, SB_CAP = 1024;
-__device__ __forceinline__ bool sb_less(const uint64_t* __restrict__ key, uint64_t ka, uint32_t a, uint64_t kb,
-                                        uint32_t b) {
-  if (ka != kb) return ka < kb;
-  for (int l = 2; l >= 0; l--) {
-    const uint64_t x = key[(uint64_t)l * TROWS + a], y = key[(uint64_t)l * TROWS + b];
-    if (x != y) return x < y;
+// After one radix sort by the top 64-bit limb of the canonical value: a run of equal top limbs
+// (about 2^-33 likely for 2^16 uniform values, but possible) is put in order by the three lower
+// limbs, in place, by the thread at the run's start (insertion sort). The rank order is then the
+// order of the full 256-bit values, as four LSD passes over the limbs would give.
+__global__ __launch_bounds__(256) void lk_tie_fix_kernel(const uint64_t* __restrict__ key,
+                                                         const uint64_t* __restrict__ top,
+                                                         uint32_t* __restrict__ perm) {
+  const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+  const uint64_t k = top[r];
+  if ((r > 0 && top[r - 1] == k) || r + 1 >= TROWS || top[r + 1] != k) return;
+  uint32_t e = r + 1;
+  while (e < TROWS && top[e] == k) e++;
+  auto less = [&](uint32_t a, uint32_t b) {
+    for (int l = 2; l >= 0; l--) {
+      const uint64_t x = key[(uint64_t)l * TROWS + a], y = key[(uint64_t)l * TROWS + b];
+      if (x != y) return x < y;
+    }
+    return false;
+  };
+  for (uint32_t i = r + 1; i < e; i++) {
+    const uint32_t v = perm[i];
+    uint32_t j = i;
+    while (j > r && less(v, perm[j - 1])) {
+      perm[j] = perm[j - 1];
+      j--;
+    }
+    perm[j] = v;
   }
-  return a < b;
 }
-__global__ __launch_bounds__(SB_THREADS) void lk_bucket_sort_kernel(const uint64_t* __restrict__ key,
-                                                                   const Fe* __restrict__ Tx, uint32_t shift,
-                                                                   uint32_t* __restrict__ x_of_rank,
-                                                                   Fe* __restrict__ Ts) {
-  __shared__ uint32_t hist[SB_BUCKETS];
-  __shared__ uint64_t sk[SB_CAP];
-  __shared__ uint32_t sx[SB_CAP];
-  __shared__ uint32_t n_mine, base;
-  const uint32_t b = blockIdx.x, t = threadIdx.x;
-  const uint64_t* top = key + 3ull * TROWS;
-  hist[t] = 0;
-  if (t == 0) n_mine = 0;
-  __syncthreads();
-  for (uint32_t x = t; x < (uint32_t)TROWS; x += SB_THREADS) {
-    const uint64_t k = top[x];
-    const uint32_t q = (uint32_t)(k >> shift) < (uint32_t)SB_BUCKETS ? (uint32_t)(k >> shift) : SB_BUCKETS - 1u;
-    atomicAdd(&hist[q], 1u);
-    if (q == b) {
-      const uint32_t i = atomicAdd(&n_mine, 1u);
-      if (i < (uint32_t)SB_CAP) {
-        sk[i] = k;
-        sx[i] = x;
-      }
-    }
-  }
-  __syncthreads();
-  if (t == 0) {
-    uint32_t o = 0;
-    for (uint32_t q = 0; q < b; q++) o += hist[q];
-    base = o;
-  }
-  __syncthreads();
-  const uint32_t n = n_mine;
-  if (n > (uint32_t)SB_CAP) {  // quadratic fallback over the global limbs
-    for (uint32_t x = t; x < (uint32_t)TROWS; x += SB_THREADS) {
-      const uint64_t k = top[x];
-      const uint32_t q = (uint32_t)(k >> shift) < (uint32_t)SB_BUCKETS ? (uint32_t)(k >> shift) : SB_BUCKETS - 1u;
-      if (q != b) continue;
-      uint32_t r = 0;
-      for (uint32_t y = 0; y < (uint32_t)TROWS; y++) {
-        const uint64_t ky = top[y];
-        const uint32_t qy = (uint32_t)(ky >> shift) < (uint32_t)SB_BUCKETS ? (uint32_t)(ky >> shift) : SB_BUCKETS - 1u;
-        if (qy == b && sb_less(key, ky, y, k, x)) r++;
-      }
-      x_of_rank[base + r] = x;
-      Ts[base + r] = Tx[x];
-    }
-    return;
-  }
-  uint32_t m = 1;  // padded size: a power of two >= n (pads sort last)
-  while (m < n) m <<= 1;
-  for (uint32_t i = n + t; i < m; i += SB_THREADS) {
-    sk[i] = ~0ull;
-    sx[i] = 0xffffffffu;
-  }
-  __syncthreads();
-  for (uint32_t size = 2; size <= m; size <<= 1) {
-    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      for (uint32_t i = t; i < m / 2; i += SB_THREADS) {
-        const uint32_t lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-        const bool up = (lo & size) == 0;
-        const uint64_t ka = sk[lo], kb = sk[hi];
-        const uint32_t xa = sx[lo], xb = sx[hi];
-        // pads (x = ~0) compare greater than every member
-        const bool b_less = xb == 0xffffffffu ? false : (xa == 0xffffffffu ? true : sb_less(key, kb, xb, ka, xa));
-        if (b_less == up) {
-          sk[lo] = kb;
-          sk[hi] = ka;
-          sx[lo] = xb;
-          sx[hi] = xa;
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (uint32_t i = t; i < n; i += SB_THREADS) {
-    const uint32_t x = sx[i];
-    x_of_rank[base + i] = x;
-    Ts[base + i] = Tx[x];
-  }
+
+__global__ __launch_bounds__(256) void lk_rank_kernel(const Fe* __restrict__ Tx,
+                                                      const uint32_t* __restrict__ perm,
+                                                      Fe* __restrict__ Ts) {
+  const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+  Ts[r] = Tx[perm[r]];
 }
 
 // ------------------------------------------------------------------ per-circuit passes
@@ -551,7 +490,9 @@ struct Carve {
   Fe* Tx;
   Fe* Ts;
   uint64_t* key;   // 4 x TROWS canonical limbs
-  uint32_t* perm;  // TROWS: x_of_rank
+  uint64_t* kout;  // TROWS
+  uint32_t* perm;  // TROWS
+  uint32_t* perm2;
   uint32_t* count;  // group x TROWS
   uint32_t* pos;
   uint32_t* dcnt;
@@ -562,8 +503,17 @@ struct Carve {
   Fe* den;
   Fe* zs;  // group x gp::scratch_elems
   Fe* dpart;  // (group + 1) x DP_PARTS (lk_dtot_kernel)
+  void* sort_tmp;
+  size_t sort_bytes;
   size_t total;
 };
+
+size_t sort_temp_bytes() {
+  size_t bytes = 0;
+  (void)rocprim::radix_sort_pairs((void*)nullptr, bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                  (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)TROWS, 0, 64);
+  return bytes;
+}
 
 Carve carve(void* base, uint32_t group, uint64_t usable) {
   Carve k;
@@ -577,7 +527,9 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.Tx = (Fe*)take(sizeof(Fe) * TROWS);
   k.Ts = (Fe*)take(sizeof(Fe) * TROWS);
   k.key = (uint64_t*)take(8ull * 4 * TROWS);
+  k.kout = (uint64_t*)take(8ull * TROWS);
   k.perm = (uint32_t*)take(4ull * TROWS);
+  k.perm2 = (uint32_t*)take(4ull * TROWS);
   k.count = (uint32_t*)take(4ull * TROWS * group);
   k.pos = (uint32_t*)take(4ull * TROWS * group);
   k.dcnt = (uint32_t*)take(4ull * TROWS * group);
@@ -588,6 +540,8 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);
   k.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * group);
   k.dpart = (Fe*)take(sizeof(Fe) * DP_PARTS * (group + 1));
+  k.sort_bytes = sort_temp_bytes();
+  k.sort_tmp = take(k.sort_bytes);
   k.total = off;
   return k;
 }
@@ -599,12 +553,18 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
                       uint32_t group, int* sticky, const gp::Side& side, hipStream_t s) {
   Carve k = carve(scratch, group, usable_rows);
   const dim3 tb(TROWS / 256);
-  hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key);
-  // buckets of the top limb: its top 8 bits below the modulus' top limb (every bucket < 256)
-  const uint64_t ptop = ((uint64_t)F::P[7] << 32) | F::P[6];
-  const uint32_t shift = (uint32_t)(63 - __builtin_clzll(ptop)) - 7u;
-  uint32_t* pa = k.perm;
-  hipLaunchKernelGGL(lk_bucket_sort_kernel, dim3(SB_BUCKETS), dim3(SB_THREADS), 0, s, k.key, k.Tx, shift, pa, k.Ts);
+  hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm);
+  // one radix sort by the top limb of the canonical value (< 2^63: both moduli are < 2^255),
+  // then ties in the top limb ordered by the lower limbs
+  uint32_t* pa = k.perm2;
+  {
+    size_t bytes = k.sort_bytes;
+    hipError_t e = rocprim::radix_sort_pairs(k.sort_tmp, bytes, k.key + 3ull * TROWS, k.kout, k.perm, pa,
+                                             (size_t)TROWS, 0, 63, s);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(lk_tie_fix_kernel, tb, dim3(256), 0, s, k.key, k.kout, pa);
+  hipLaunchKernelGGL(lk_rank_kernel, tb, dim3(256), 0, s, k.Tx, pa, k.Ts);
   hipError_t e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s);
   if (e != hipSuccess) return e;
   // Per group: the count / scan / permute passes over all its circuits at once (a workgroup
