@@ -576,28 +576,29 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   if ((e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s)) != hipSuccess) return e;
   // Per group: the count / scan / permute passes over all its circuits at once (a workgroup
   // count per circuit that fills the chip), then the grand products. The den totals' inverses
-  // D^-1 come from the rows on the side stream (lk_dtot_kernel, lk_dinv_kernel), forked after
-  // the group's scans (so after the previous group's gp_write, which read the same D^-1 slots):
-  // the inversions' latency hides behind the permute and chunk passes. (r04m: with D taken from the den chunk totals, each half of
+  // D^-1 come from the rows on the side stream (lk_dtot_kernel, lk_dinv_kernel) -- for the
+  // first group right after the table pass, for a later one forked after the previous group's
+  // gp_write (which read the same D^-1 slots) -- so the inversions' latency hides behind the
+  // count, scan and permute passes. (r04m: with D taken from the den chunk totals, each half of
   // the group's inversion still held its gp_write 25-52 us after two-way pipelining, 1.24-1.27
   // ms per call.)
   for (uint32_t c0 = 0; c0 < n_circuits; c0 += group) {
     const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
     const gp::Scratch zk = gp::scratch_of(k.zs, g, usable_rows);
+    if (c0 > 0) {
+      if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
                        total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
     if (c0 == 0 && (e = hipStreamWaitEvent(s, side.join, 0)) != hipSuccess) return e;  // the table pass
-    hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
-    hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
-                       k.part, k.pos, k.dcnt, k.lp, k.samp);
-    // the D^-1 chain beside the permute pass and the chunk pass (r04r: forked before the scans it
-    // stretched lk_scan_sums 24 -> 94 us)
-    if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(lk_dtot_kernel<F>, dim3(DP_PARTS, g + 1), dim3(DP_THREADS), 0, side.s2, d_advice,
                        total_rows, d_row_begin, c0, g, usable_rows, k.Tx, ch, k.dpart);
     hipLaunchKernelGGL(lk_dinv_kernel<F>, dim3(g), dim3(DP_PARTS), 0, side.s2, k.dpart, g, zk.dt, sticky);
     if ((e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;
+    hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
+    hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
+                       k.part, k.pos, k.dcnt, k.lp, k.samp);
     // permute: ~4096 rows per workgroup
     const uint32_t px = (uint32_t)((usable_rows + 4095) / 4096);
     hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
