@@ -553,49 +553,38 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
                       uint32_t group, int* sticky, const gp::Side& side, hipStream_t s) {
   Carve k = carve(scratch, group, usable_rows);
   const dim3 tb(TROWS / 256);
-  hipError_t e;
-  // The table pass depends on theta only, the first group's count pass on the cells only: the
-  // table pass (table, radix sort, tie fix, ranks: ~85 us of small launches) runs on the side
-  // stream beside the count pass, and the scans wait for both. (In line, in front of the count
-  // pass: r04o.) The side stream then carries each group's D^-1 chain.
-  if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
-  if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
-  hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, side.s2, ch, k.Tx, k.key, k.perm);
+  hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm);
   // one radix sort by the top limb of the canonical value (< 2^63: both moduli are < 2^255),
   // then ties in the top limb ordered by the lower limbs
   uint32_t* pa = k.perm2;
   {
     size_t bytes = k.sort_bytes;
-    if ((e = rocprim::radix_sort_pairs(k.sort_tmp, bytes, k.key + 3ull * TROWS, k.kout, k.perm, pa,
-                                       (size_t)TROWS, 0, 63, side.s2)) != hipSuccess)
-      return e;
+    hipError_t e = rocprim::radix_sort_pairs(k.sort_tmp, bytes, k.key + 3ull * TROWS, k.kout, k.perm, pa,
+                                             (size_t)TROWS, 0, 63, s);
+    if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(lk_tie_fix_kernel, tb, dim3(256), 0, side.s2, k.key, k.kout, pa);
-  hipLaunchKernelGGL(lk_rank_kernel, tb, dim3(256), 0, side.s2, k.Tx, pa, k.Ts);
-  if ((e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;  // the table pass
-  if ((e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(lk_tie_fix_kernel, tb, dim3(256), 0, s, k.key, k.kout, pa);
+  hipLaunchKernelGGL(lk_rank_kernel, tb, dim3(256), 0, s, k.Tx, pa, k.Ts);
+  hipError_t e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s);
+  if (e != hipSuccess) return e;
   // Per group: the count / scan / permute passes over all its circuits at once (a workgroup
   // count per circuit that fills the chip), then the grand products. The den totals' inverses
-  // D^-1 come from the rows on the side stream (lk_dtot_kernel, lk_dinv_kernel) -- for the
-  // first group right after the table pass, for a later one forked after the previous group's
-  // gp_write (which read the same D^-1 slots) -- so the inversions' latency hides behind the
-  // count, scan and permute passes. (r04m: with D taken from the den chunk totals, each half of
-  // the group's inversion still held its gp_write 25-52 us after two-way pipelining, 1.24-1.27
-  // ms per call.)
+  // D^-1 come from the rows on the side stream (lk_dtot_kernel, lk_dinv_kernel), forked at the
+  // group's start (after the previous group's gp_write, which read the same D^-1 slots), so the
+  // inversions' latency hides behind the count, scan and permute passes. (r04m: with D taken from
+  // the den chunk totals, each half of the group's inversion still held its gp_write 25-52 us
+  // after two-way pipelining, 1.24-1.27 ms per call.)
   for (uint32_t c0 = 0; c0 < n_circuits; c0 += group) {
     const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
     const gp::Scratch zk = gp::scratch_of(k.zs, g, usable_rows);
-    if (c0 > 0) {
-      if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
-                       total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
-    if (c0 == 0 && (e = hipStreamWaitEvent(s, side.join, 0)) != hipSuccess) return e;  // the table pass
+    if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(lk_dtot_kernel<F>, dim3(DP_PARTS, g + 1), dim3(DP_THREADS), 0, side.s2, d_advice,
                        total_rows, d_row_begin, c0, g, usable_rows, k.Tx, ch, k.dpart);
     hipLaunchKernelGGL(lk_dinv_kernel<F>, dim3(g), dim3(DP_PARTS), 0, side.s2, k.dpart, g, zk.dt, sticky);
     if ((e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;
+    hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
+                       total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
     hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
     hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
                        k.part, k.pos, k.dcnt, k.lp, k.samp);
