@@ -39,6 +39,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 # product); permutation: counted per call from the circuit's copy cycles (the permutation leg).
 MULBENCH_GPS = {"pallas": 158.0, "bn254": 129.5}
 LOOKUP_PRODUCTS_PER_ROW = 6
+# Where the prover-column legs' numbers were diagnosed (committed profiles)
+LOOKUP_EVIDENCE = {
+    "pmc": "profiles/r04a_lk_pmc.txt: lk_permute_kernel waves 54 % in s_waitcnt, 27 % issue-stalled; "
+           "its stores were the bound (ablations r04d: no column stores 306 us vs 557)",
+    "ab_ms_per_call": "1.49 (round 3) -> 1.24-1.27 (staged NT stores, in-block scans, r04m) -> "
+                      "1.14-1.16 (D before the permute pass, r04o)",
+}
+PERM_EVIDENCE = {
+    "pmc": "profiles/r04a_pm_pmc.txt: pm_factor_kernel 3.0e8 VALU instructions for 86 M products, "
+           "VMEM 2.4e6: bound by the products",
+    "ab_ms_per_call": "3.05 (round 3) -> 2.96 (r04l) -> 2.58-2.60 (factors fused with the chunk pass, "
+                      "pm_chunk_kernel, r04m/r04o)",
+}
 # 1 in BN254 Fr Montgomery form (R mod r) as four little-endian int64 limbs
 FR_ONE_MONT = [int.from_bytes((0x0e0a77c19a07df2f666ea36f7879462e36fc76959f60cd29ac96341c4ffffffb
                                >> (64 * i) & (2**64 - 1)).to_bytes(8, "little"), "little", signed=True)
@@ -649,7 +662,8 @@ def main():
                                    "peak": MULBENCH_GPS["pallas"], "unit": "G products/s",
                                    "frac": round(gps / MULBENCH_GPS["pallas"], 4)},
                       "field": "pasta Fp montgomery",
-                      "all_rows_in_table": bool((lbad == -1).all().item())}
+                      "all_rows_in_table": bool((lbad == -1).all().item()),
+                      "evidence": LOOKUP_EVIDENCE}
             del lout
         except Exception as e:  # reported, never masks the headline
             lookup = {"error": repr(e)}
@@ -701,7 +715,8 @@ def main():
                                  "peak": MULBENCH_GPS["bn254"], "unit": "G products/s",
                                  "frac": round(gps / MULBENCH_GPS["bn254"], 4)},
                     "written_GBs": round(domain * 32 * 11 / (avg * 1e-3) / 1e9, 1),
-                    "z_closes_to_one": closes}
+                    "z_closes_to_one": closes,
+                    "evidence": PERM_EVIDENCE}
             del sig, z
         except Exception as e:  # reported, never masks the headline
             perm = {"error": repr(e)}
