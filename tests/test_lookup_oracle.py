@@ -60,3 +60,28 @@ def test_batch_invert():
     vals = [int(v) + 1 for v in rng.integers(0, 2**62, 50)]
     inv = lk.batch_invert(vals)
     assert all(v * w % lk.P == 1 for v, w in zip(vals, inv))
+
+
+@pytest.mark.parametrize("p", [lk.P, lk.P_BN254])
+def test_den_total_equals_num_total(p):
+    """The identity the GPU's lk_dtot_kernel rests on (lookup columns): A' is a
+    permutation of A and S' one of S, so prod_p (A'_p + beta)(S'_p + gamma) = prod_p (A_p + beta)
+    * prod_p (S_p + gamma) -- the grand product's den total is known from the rows and the table
+    alone, before any permuted column exists. Also z[p + 1] = N_p / D_p with that D."""
+    usable = (1 << 16) + 501
+    a0, a1, a2 = _rows(usable, zero_frac=0.5)
+    theta, beta, gamma = _chal(p)
+    A, S, Ap, Sp, z = lk.columns(a0, a1, a2, usable, theta, beta, gamma, p)
+    den = num_a = num_s = 1
+    for i in range(usable):
+        den = den * (Ap[i] + beta) % p * (Sp[i] + gamma) % p
+        num_a = num_a * (A[i] + beta) % p
+        num_s = num_s * (S[i] + gamma) % p
+    assert den == num_a * num_s % p
+    # the S part is the same for every circuit: the table once, then row 0's value
+    tv = lk.table_values(theta, p)
+    s_part = 1
+    for x in range(1 << 16):
+        s_part = s_part * (tv[x] + gamma) % p
+    s_part = s_part * pow(tv[0] + gamma, usable - (1 << 16), p) % p
+    assert s_part == num_s
