@@ -825,9 +825,6 @@ struct b2f_ctx {
   // down-sweep (b2f_gprod.h), forked from and joined back to the caller's stream
   hipStream_t s2;
   hipEvent_t ev_fork, ev_join;
-  // the lookup's side work (its den totals and their inversions) at the lowest stream priority:
-  // it has slack, and at normal priority its workgroups took slots from the passes beside it
-  hipStream_t s_low;
 };
 
 namespace {
@@ -892,11 +889,6 @@ constexpr int fused_mode() { return 27; }
 // the side stream and events of the grand products (created on first use)
 int ensure_side(b2f_ctx* ctx) {
   if (!ctx->s2) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
-  if (!ctx->s_low) {
-    int least = 0, greatest = 0;
-    HIPCHK(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
-    HIPCHK(ctx, hipStreamCreateWithPriority(&ctx->s_low, hipStreamNonBlocking, least));
-  }
   if (!ctx->ev_fork) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
   if (!ctx->ev_join) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
   return B2F_OK;
@@ -1111,7 +1103,6 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
-  if (ctx->s_low) (void)hipStreamDestroy(ctx->s_low);
   (void)hipHostFree(ctx->h_pm_inst);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   delete ctx;
@@ -1465,7 +1456,7 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
   int tk = timed_begin(ctx, B2F_KERNEL_LOOKUP, s);
   HIPCHK(ctx, launch_lookup(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, theta, beta,
                             gamma, form, d_out, out_rows, d_first_bad, ctx->d_lk, group,
-                            ctx->d_status + 2, ctx->s_low, ctx->ev_fork, ctx->ev_join, s));
+                            ctx->d_status + 2, ctx->s2, ctx->ev_fork, ctx->ev_join, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
