@@ -54,6 +54,9 @@ extern "C" {
 #define B2F_ERR_INPUT 6     /* malformed EIP-152 input (length != 213 or f not 0/1) */
 #define B2F_ERR_FIELD 7     /* (at b2f_sync) a grand product's denominator product is zero: a
                                challenge collides with a cell value, its z column is meaningless */
+#define B2F_ERR_CHECK 8     /* (at b2f_sync) a prover-column call's internal cross-check failed
+                               (the lookup's permuted columns do not multiply to the product of
+                               its input columns): its columns are wrong -- a library defect */
 
 /* One EIP-152 compression: the reference's Blake2fWitness{rounds, h, m, t, f}
  * (blake2f.rs:208-239), 216 bytes, naturally aligned. f must be 0 or 1. */
@@ -246,7 +249,7 @@ B2F_API int b2f_spread_table_dev(b2f_ctx* ctx, uint64_t usable_rows, uint32_t fo
  * + usable_rows - 1 (rows past total_rows read as zero rows, i.e. table row 0), and the
  * table columns hold the 2^16 spread-table rows then the row-0 default up to usable_rows
  * (the layouter's fill_from_row). usable_rows = 2^k - blinding_factors - 1 is the caller's,
- * in [2^16, 2^32). Challenges theta, beta, gamma: canonical field elements (4 LE u64 limbs).
+ * in [2^16, 2^31]. Challenges theta, beta, gamma: canonical field elements (4 LE u64 limbs).
  * Output, per circuit c and column j, d_out[((c * 5 + j) * out_rows + row) * 4 + limb]:
  *   j = 0  A:  compressed input   theta^2 a_0 + theta a_1 + a_2   (rows < usable_rows)
  *   j = 1  S:  compressed table                                     (rows < usable_rows)

@@ -27,10 +27,11 @@ MAX_ROUNDS = 1 << 20
 KERNEL_NAMES = ["record", "fill", "eval", "export", "fill_eval", "lookup", "perm"]  # B2F_KERNEL_*
 FP_CANONICAL, FP_MONTGOMERY, FP_BN254_CANONICAL, FP_BN254_MONTGOMERY = 0, 1, 2, 3  # B2F_FP_*
 
-OK, ERR_ARG, ERR_ROUNDS, ERR_ROWS, ERR_HIP, ERR_LAYOUT, ERR_INPUT, ERR_FIELD = range(8)
+OK, ERR_ARG, ERR_ROUNDS, ERR_ROWS, ERR_HIP, ERR_LAYOUT, ERR_INPUT, ERR_FIELD, ERR_CHECK = range(9)
 STATUS_NAMES = {OK: "OK", ERR_ARG: "B2F_ERR_ARG", ERR_ROUNDS: "B2F_ERR_ROUNDS",
                 ERR_ROWS: "B2F_ERR_ROWS", ERR_HIP: "B2F_ERR_HIP", ERR_LAYOUT: "B2F_ERR_LAYOUT",
-                ERR_INPUT: "B2F_ERR_INPUT", ERR_FIELD: "B2F_ERR_FIELD"}
+                ERR_INPUT: "B2F_ERR_INPUT", ERR_FIELD: "B2F_ERR_FIELD",
+                ERR_CHECK: "B2F_ERR_CHECK"}
 
 
 class B2FError(RuntimeError):

@@ -1417,8 +1417,8 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
     return set_err(ctx, B2F_ERR_ARG, "lookup: null buffer");
   if (form > B2F_FP_BN254_MONTGOMERY) return set_err(ctx, B2F_ERR_ARG, "lookup: unknown form %u", form);
   if ((uintptr_t)d_out & 15) return set_err(ctx, B2F_ERR_ARG, "lookup: d_out must be 16-byte aligned");
-  if (usable_rows < (1ull << 16) || usable_rows >= (1ull << 32))
-    return set_err(ctx, B2F_ERR_ROWS, "lookup: usable_rows %llu not in [2^16, 2^32)",
+  if (usable_rows < (1ull << 16) || usable_rows > (1ull << 31))
+    return set_err(ctx, B2F_ERR_ROWS, "lookup: usable_rows %llu not in [2^16, 2^31]",
                    (unsigned long long)usable_rows);
   if (out_rows < usable_rows + 1)
     return set_err(ctx, B2F_ERR_ROWS, "lookup: out_rows < usable_rows + 1");
@@ -1437,10 +1437,10 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
   if (n_circuits == 0) return B2F_OK;
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(ctx, hipSetDevice(ctx->device));
-  // circuits per pass: per-circuit scratch is 1 MiB (count, pos, D, LP, samples) + 64 B per
-  // row (num, den) + the grand product's chunk scratch; keep it under 1 GiB
-  const uint64_t per = (4ull << 18) + usable_rows * 64 + ((usable_rows + 63) / 64) * 64;
-  uint32_t group = (uint32_t)((1ull << 30) / per);
+  // circuits per pass: at most 2^24 rows (128 circuits of 2^17), enough workgroups to fill
+  // the chip several times over; per-circuit scratch is 1.1 MiB (count, pos, D, LP, samples) +
+  // 224 B per 1,024-row block (num products, prefixes, look-back state)
+  uint32_t group = (uint32_t)((1ull << 24) / usable_rows);
   if (group < 1) group = 1;
   if (group > n_circuits) group = n_circuits;
   const size_t need = lookup_scratch_bytes(group, usable_rows);
@@ -1646,6 +1646,8 @@ B2F_API int b2f_sync(b2f_ctx* ctx, void* stream) {
     return set_err(ctx, B2F_ERR_LAYOUT, "row offsets are not the LAYOUT v1 prefix sums");
   if (bits & (1 << B2F_ERR_FIELD))
     return set_err(ctx, B2F_ERR_FIELD, "a grand product's denominator is zero (challenge collision)");
+  if (bits & (1 << B2F_ERR_CHECK))
+    return set_err(ctx, B2F_ERR_CHECK, "lookup: the permuted columns' den product differs from the input side's");
   return B2F_OK;
 }
 

@@ -21,9 +21,11 @@
 //            start gets S'[p] = Ts[r]; the j-th repeated row gets leftover item L - 1 - j
 //            (halo2 hands leftovers out in ascending order, each to the last open repeated
 //            row), found by binary search of LP;
-//   z:       the permute pass also writes each row's factors num = (A + beta)(S + gamma) and
-//            den = (A' + beta)(S' + gamma); the grand product over them (b2f_gprod.h: one
-//            inversion per circuit, 4 products per row) writes the z column.
+//   z:       the same pass forms each row's factors num = (A + beta)(S + gamma) and
+//            den = (A' + beta)(S' + gamma) in registers and writes the grand product z in one
+//            go: the num side's block prefix and D^-1 come from a side-stream pre-pass over the
+//            trace (D = prod num = prod den), the den side's suffix over blocks from a decoupled
+//            look-back (lk_zpass_kernel below).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -187,7 +189,12 @@ __global__ __launch_bounds__(CNT_THREADS) void lk_count_kernel(
 // pass): lk_scan_sums writes each part's totals, lk_scan_write adds the totals of the parts
 // before it and scans its own ranks. (One 1,024-thread workgroup per circuit holding 64 ranks per
 // thread kept the gathered counts in scratch and used 64 of the 256 CUs.)
-constexpr int SAMPLE = TROWS / 16;  // every 16th pos / lp entry, for the permute searches
+#ifndef B2F_LK_SAMP
+#define B2F_LK_SAMP 32  // pos / lp sample stride of the z pass's LDS search tables
+#endif
+constexpr int SAMP = B2F_LK_SAMP;
+static_assert(SAMP == 16 || SAMP == 32, "sample stride: a multiple of the scan's 16 ranks per thread");
+constexpr int SAMPLE = TROWS / SAMP;  // every SAMP-th pos / lp entry, for the z pass's searches
 constexpr int SC_PARTS = 16, SC_THREADS = 256, SC_PER = TROWS / (SC_PARTS * SC_THREADS);
 static_assert(SC_PER == 16, "one search sample per thread");
 
@@ -287,8 +294,10 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
   uint4* P4 = reinterpret_cast<uint4*>(pos + (uint64_t)c * TROWS + r0);
   uint4* D4 = reinterpret_cast<uint4*>(dcnt + (uint64_t)c * TROWS + r0);
   uint4* L4 = reinterpret_cast<uint4*>(lp + (uint64_t)c * TROWS + r0);
-  samp[(uint64_t)c * 2 * SAMPLE + (r0 >> 4)] = ec;  // r0 is a multiple of 16: a search sample
-  samp[(uint64_t)c * 2 * SAMPLE + SAMPLE + (r0 >> 4)] = el;
+  if (r0 % SAMP == 0) {  // a search sample
+    samp[(uint64_t)c * 2 * SAMPLE + r0 / SAMP] = ec;
+    samp[(uint64_t)c * 2 * SAMPLE + SAMPLE + r0 / SAMP] = el;
+  }
 #pragma unroll
   for (int i = 0; i < SC_PER / 4; i++) {
     uint32_t pq[4], dq[4], lq[4];
@@ -309,77 +318,277 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
   }
 }
 
-// The grand product's den total D before the permute pass: A' is a permutation of A and S' one
-// of S (the leftover items are exactly the table rows no run start took, row 0 with its
-// usable - 2^16 + 1 multiplicity), so D = prod_p den_p = prod_p num_p = prod_p (A_p + beta) *
-// prod_p (S_p + gamma). lk_dtot_kernel forms both from the rows -- A_p = Tx[dense cell] and
-// S_p = Tx[p] (row 0's value past the table) -- one product per row: workgroups (pt, c < g) the
-// A part of circuit c, workgroups (pt, g) the S part (the same for every circuit); lk_dinv
-// multiplies the partial products and inverts D. All on the side stream, beside the count, scan
-// and permute passes, so no inversion waits in front of gp_write. (A power per histogram bin,
-// (Tx[x] + beta)^count[x], ran lanes of one wave through different exponents: 362 us beside
-// the permute pass, r04n.) Rows bin by their low 16 bits in every pass, so the identity holds
-// whether or not every row is in the table, and D = 0 still flags a zero factor.
-constexpr int DP_PARTS = 16, DP_THREADS = 256;
+// ------------------------------------------------------------------ the grand product, one pass
+// z[p + 1] = N_p / D_p with N_p = prod_{i <= p} num_i, D_p = prod_{i <= p} den_i,
+// num_i = (A_i + beta)(S_i + gamma), den_i = (A'_i + beta)(S'_i + gamma). The rows are cut into
+// look-back blocks of LB rows (one lk_zpass workgroup each, ZR consecutive rows per lane), and
+//   z[p + 1] = (Nbefore_b D^-1) (Dafter_b) (N-prefix of the lanes before, in the block)
+//              (D-suffix of the lanes after, in the block) (Nloc_p Dsuf_p, inside the lane)
+// where Nbefore_b = the num product of the blocks before b and Dafter_b = the den product of
+// the blocks after b. Both directions are available in ONE pass because the num side never
+// depends on the permutation: A and S are known from the trace and the table alone, so
+// lk_npart / lk_nscan form every block's num product, their prefix, the total D = prod num_i
+// and D^-1 on the side stream, beside the count and scan passes (A' is a permutation of A and
+// S' one of S -- the leftover items are exactly the table rows no run start took, row 0 with
+// its usable - 2^16 + 1 multiplicity -- so prod den_i = prod num_i = D). The den side comes from
+// the permuted columns the pass itself forms; its suffix over blocks is a decoupled look-back
+// in descending block order (workgroups take tickets, so a block only ever waits for blocks
+// whose workgroups already run). The pass writes the five columns once and nothing else: no
+// factor, prefix or chunk slot makes a round trip through HBM (round 4's permute pass +
+// gp_chunk + gp_write moved 384 B per row; this pass 164).
+// Check: block 0's inclusive den product is D_den = prod den_i from the permuted
+// columns, which must equal the num-side D; a difference (wrong A' or S') sets B2F_ERR_CHECK.
+#ifndef B2F_ZP_WAVES
+#define B2F_ZP_WAVES 4  // lk_zpass_kernel waves per SIMD (ZR = 2: 128 VGPRs)
+#endif
+#ifndef B2F_ZR
+#define B2F_ZR 2
+#endif
+constexpr int ZR = B2F_ZR;       // rows per lane
+static_assert(ZR == 2 || ZR == 4, "rows per lane");
+constexpr int ZT = 256;          // lanes per look-back block (lk_zpass workgroup)
+constexpr int LB = ZT * ZR;      // rows per look-back block
+__host__ __device__ inline uint64_t n_lb(uint64_t usable) { return (usable + LB - 1) / LB; }
+
+// Diagnostics (variant builds with -DB2F_LK_CLOCK only): per-phase s_memtime totals of
+// lk_zpass_kernel summed over waves, read by b2f_debug_lk_clock (tools/lk_clock.py).
+#ifdef B2F_LK_CLOCK
+// [11] resident workgroups now, [12] their maximum, [13] / [14] first start / last end tick
+__device__ unsigned long long g_lk_clock[16];
+#define LKCLK_DECL                                                           \
+  uint64_t lk_t = __builtin_amdgcn_s_memtime();                             \
+  if (threadIdx.x == 0) {                                                   \
+    atomicMin(&g_lk_clock[13], (unsigned long long)lk_t);                   \
+    atomicMax(&g_lk_clock[12], atomicAdd(&g_lk_clock[11], 1ull) + 1);        \
+  }
+#define LKCLK_END                                                           \
+  if (threadIdx.x == 0) {                                                   \
+    atomicMax(&g_lk_clock[14], (unsigned long long)__builtin_amdgcn_s_memtime()); \
+    atomicAdd(&g_lk_clock[11], ~0ull);                                      \
+  }
+#define LKCLK(i)                                                                 \
+  do {                                                                           \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();                          \
+    if (lane == 0) atomicAdd(&g_lk_clock[i], (unsigned long long)(now_ - lk_t)); \
+    lk_t = now_;                                                                 \
+  } while (0)
+#else
+#define LKCLK_DECL
+#define LKCLK_END
+#define LKCLK(i) \
+  do {           \
+  } while (0)
+#endif
+
+__device__ __forceinline__ Fe shfl_fe(const Fe& v, int src) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.w[i] = (uint32_t)__shfl((int)v.w[i], src, 64);
+  return r;
+}
+__device__ __forceinline__ Fe shfl_xor_fe(const Fe& v, int m) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.w[i] = (uint32_t)__shfl_xor((int)v.w[i], m, 64);
+  return r;
+}
+// the product of the 64 lanes' values, in every lane
 template <class F>
-__global__ __launch_bounds__(DP_THREADS) void lk_dtot_kernel(const uint32_t* __restrict__ adv, uint64_t total_rows,
-                                                             const uint64_t* __restrict__ row_begin, uint32_t c0,
-                                                             uint32_t g, uint64_t usable, const Fe* __restrict__ Tx,
-                                                             Chal ch, Fe* __restrict__ part) {
-  const uint32_t pt = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
-  const bool s_part = c == g;
+__device__ __forceinline__ Fe wave_prod(Fe v) {
+#pragma unroll 1
+  for (int m = 32; m > 0; m >>= 1) v = field::mul<F>(v, shfl_xor_fe(v, m));
+  return v;
+}
+
+// Block num products, the A part: NP_LPB lanes per look-back block, each lane NP_RPL rows
+// NP_LPB apart (the product is order-free, so a load instruction reads NP_LPB consecutive cells
+// of each of the wave's blocks), two product chains per lane, then log2(NP_LPB) butterfly levels
+// inside the lane group (a whole-wave product per block cost 6 levels on 8 rows per lane).
+// Row y == g of the grid: the S part (S_i + gamma), the same for every circuit and every group,
+// so only the first group's launch has that row.
+constexpr int NP_RPL = 32;                 // rows per lane
+constexpr int NP_LPB = LB / NP_RPL;        // lanes per block
+constexpr int NP_BPW = 64 / NP_LPB;        // blocks per wave
+static_assert(NP_LPB >= 2 && NP_LPB <= 64 && (NP_LPB & (NP_LPB - 1)) == 0, "lane groups");
+template <class F>
+__global__ __launch_bounds__(256) void lk_npart_kernel(const uint32_t* __restrict__ adv, uint64_t total_rows,
+                                                       const uint64_t* __restrict__ row_begin, uint32_t c0,
+                                                       uint32_t g, uint64_t usable, uint64_t nb,
+                                                       const Fe* __restrict__ Tx, Chal ch,
+                                                       Fe* __restrict__ partA, Fe* __restrict__ partS) {
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, y = blockIdx.y;
+  const uint64_t b = ((uint64_t)blockIdx.x * 4 + wv) * NP_BPW + lane / NP_LPB;
+  const bool s_part = y == g;
   const Fe add = field::to_mont<F>(field::load_words(s_part ? ch.gamma : ch.beta));
-  const Circ k = s_part ? Circ{0, 0} : circ(row_begin, total_rows, usable, c0 + c);
-  const uint64_t per = (usable + DP_PARTS - 1) / DP_PARTS;
-  const uint64_t b = (uint64_t)pt * per, e = b + per < usable ? b + per : usable;
-  Fe acc = field::one<F>();
-  // four rows per step: their cell and table loads issued together, then two independent products
-  for (uint64_t p = b + t; p < e; p += 4 * DP_THREADS) {
+  const Circ k = s_part ? Circ{0, 0} : circ(row_begin, total_rows, usable, c0 + y);
+  const uint64_t base = b * LB + lane % NP_LPB;
+  Fe acc0 = field::one<F>(), acc1 = field::one<F>();
+#pragma unroll 1
+  for (int i0 = 0; i0 < NP_RPL; i0 += 4) {
     uint32_t x[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const uint64_t q = p + (uint64_t)u * DP_THREADS;
+      const uint64_t q = base + (uint64_t)NP_LPB * (i0 + u);
       x[u] = s_part ? (q < (uint64_t)TROWS ? (uint32_t)q : 0u)
                     : (q < k.n_in ? (adv[total_rows + k.first + q] & 0xffffu) : 0u);
     }
     Fe v[4];
 #pragma unroll
     for (int u = 0; u < 4; u++)
-      v[u] = p + (uint64_t)u * DP_THREADS < e ? field::add<F>(Tx[x[u]], add) : field::one<F>();
-    acc = field::mul<F>(acc, field::mul<F>(field::mul<F>(v[0], v[1]), field::mul<F>(v[2], v[3])));
+      v[u] = base + (uint64_t)NP_LPB * (i0 + u) < usable ? field::add<F>(Tx[x[u]], add) : field::one<F>();
+    acc0 = field::mul<F>(acc0, field::mul<F>(v[0], v[1]));
+    acc1 = field::mul<F>(acc1, field::mul<F>(v[2], v[3]));
   }
-  __shared__ Fe sp[DP_THREADS];
-  for (uint32_t w = DP_THREADS / 2; w > 0; w >>= 1) {
-    if (t >= w && t < 2 * w) sp[t] = acc;
-    __syncthreads();
-    if (t < w) acc = field::mul<F>(acc, sp[t + w]);
-    __syncthreads();
-  }
-  if (t == 0) part[(uint64_t)c * DP_PARTS + pt] = acc;
-}
-// D_c = prod_i (A part i of c) (S part i), a tree over the DP_PARTS pairs, then D^-1 in place (one
-// lane: gp::gp_inv's zero check and issue priority)
-template <class F>
-__global__ __launch_bounds__(DP_PARTS) void lk_dinv_kernel(const Fe* __restrict__ part, uint32_t g,
-                                                           Fe* __restrict__ dt, int* __restrict__ sticky) {
-  const uint32_t c = blockIdx.x, t = threadIdx.x;
-  __shared__ Fe sp[DP_PARTS];
-  Fe d = field::mul<F>(part[(uint64_t)c * DP_PARTS + t], part[(uint64_t)g * DP_PARTS + t]);
-  for (uint32_t w = DP_PARTS / 2; w > 0; w >>= 1) {
-    if (t >= w && t < 2 * w) sp[t] = d;
-    __syncthreads();
-    if (t < w) d = field::mul<F>(d, sp[t + w]);
-    __syncthreads();
-  }
-  if (t != 0) return;
-  __builtin_amdgcn_s_setprio(3);
-  if (sticky && field::is_zero(d)) atomicOr(sticky, 1 << B2F_ERR_FIELD);
-  dt[c] = field::inv_kaliski<F>(d);
+  Fe acc = field::mul<F>(acc0, acc1);
+#pragma unroll 1
+  for (int m = 1; m < NP_LPB; m <<= 1) acc = field::mul<F>(acc, shfl_xor_fe(acc, m));
+  if (lane % NP_LPB == 0 && b < nb) (s_part ? partS[b] : partA[(uint64_t)y * nb + b]) = acc;
 }
 
-// last index r with a[r] <= v (a nondecreasing over TROWS entries, a[0] <= v): the top 12
-// levels of the search over the workgroup's LDS sample s[k] = a[16 k], then the 16 entries
-// of that block (one 64-byte line, four loads in flight at once) in registers.
+// Per circuit: N_b = A part x S part, the exclusive prefix over blocks (runs per thread, a
+// Hillis-Steele scan of the run products in LDS), D = the total, D^-1 (one lane's inversion at
+// top issue priority; D = 0 -- a zero factor -- raises B2F_ERR_FIELD), then NK_b = Nbefore_b D^-1.
+constexpr int NS_T = 256;
+template <class F>
+__global__ __launch_bounds__(NS_T) void lk_nscan_kernel(uint64_t nb, const Fe* __restrict__ partA,
+                                                        const Fe* __restrict__ partS, Fe* __restrict__ NK,
+                                                        Fe* __restrict__ Dnum, int* __restrict__ sticky) {
+  __shared__ Fe sn[NS_T];
+  __shared__ Fe sdinv;
+  const uint32_t c = blockIdx.x, t = threadIdx.x;
+  const uint64_t per = (nb + NS_T - 1) / NS_T;
+  const uint64_t b0 = t * per < nb ? t * per : nb, e = b0 + per < nb ? b0 + per : nb;
+  const Fe* pa = partA + (uint64_t)c * nb;
+  Fe run = field::one<F>();
+  for (uint64_t b = b0; b < e; b++) run = field::mul<F>(run, field::mul<F>(pa[b], partS[b]));
+  Fe inc = run;
+  sn[t] = inc;
+  __syncthreads();
+  for (int off = 1; off < NS_T; off <<= 1) {
+    Fe x = inc;
+    if (t >= (uint32_t)off) x = field::mul<F>(sn[t - off], inc);
+    __syncthreads();
+    sn[t] = inc = x;
+    __syncthreads();
+  }
+  if (t == 0) {
+    const Fe D = sn[NS_T - 1];
+    Dnum[c] = D;
+    __builtin_amdgcn_s_setprio(3);
+    if (sticky && field::is_zero(D)) atomicOr(sticky, 1 << B2F_ERR_FIELD);
+    sdinv = field::inv_kaliski<F>(D);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  __syncthreads();
+  Fe rn = field::mul<F>(t ? sn[t - 1] : field::one<F>(), sdinv);
+  Fe* nk = NK + (uint64_t)c * nb;
+  for (uint64_t b = b0; b < e; b++) {
+    nk[b] = rn;
+    rn = field::mul<F>(rn, field::mul<F>(pa[b], partS[b]));
+  }
+}
+
+// Look-back state of a block: words 0..5 its den product (aggregate), 8..13 the den product of
+// it and every block after it (inclusive), word 15 its status (1 aggregate, 2 inclusive). An
+// element goes out as six 48-bit pieces, each in a u64 tagged in its top 16 bits and stored with
+// a relaxed agent-scope atomic: a reader that sees all six tags has the whole value, so no
+// release fence (and no L2 write-back) is needed; the status word (written after the pieces) is
+// what pollers read -- one word per block -- and a reader that finds a piece untagged polls
+// again. The state is zeroed before each launch.
+constexpr int LBS_WORDS = 16;
+constexpr uint64_t LB_M48 = (1ull << 48) - 1;
+constexpr uint64_t LB_TAG_AGG = 0xB2F1ull << 48, LB_TAG_INC = 0xB2F2ull << 48;
+__device__ __forceinline__ uint64_t lb_piece(const Fe& v, uint32_t k) {
+  const uint64_t L0 = v.w[0] | (uint64_t)v.w[1] << 32, L1 = v.w[2] | (uint64_t)v.w[3] << 32;
+  const uint64_t L2 = v.w[4] | (uint64_t)v.w[5] << 32, L3 = v.w[6] | (uint64_t)v.w[7] << 32;
+  const uint64_t w[6] = {L0 & LB_M48, (L0 >> 48 | L1 << 16) & LB_M48, (L1 >> 32 | L2 << 32) & LB_M48,
+                         (L2 >> 16) & LB_M48, L3 & LB_M48, L3 >> 48};
+  uint64_t r = w[0];
+#pragma unroll
+  for (uint32_t i = 1; i < 6; i++) r = k == i ? w[i] : r;
+  return r;
+}
+__device__ __forceinline__ Fe lb_join(const uint64_t (&w)[6]) {
+  const uint64_t L0 = (w[0] & LB_M48) | (w[1] << 48);
+  const uint64_t L1 = ((w[1] & LB_M48) >> 16) | (w[2] << 32);
+  const uint64_t L2 = ((w[2] & LB_M48) >> 32) | ((w[3] & LB_M48) << 16);
+  const uint64_t L3 = (w[4] & LB_M48) | (w[5] << 48);
+  Fe v;
+  v.w[0] = (uint32_t)L0; v.w[1] = (uint32_t)(L0 >> 32);
+  v.w[2] = (uint32_t)L1; v.w[3] = (uint32_t)(L1 >> 32);
+  v.w[4] = (uint32_t)L2; v.w[5] = (uint32_t)(L2 >> 32);
+  v.w[6] = (uint32_t)L3; v.w[7] = (uint32_t)(L3 >> 32);
+  return v;
+}
+__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lanes 0..5 of the calling wave publish v (the same in every lane) as the aggregate (kind 1) or
+// the inclusive value (kind 2) of block state st, then lane 0 its status
+__device__ __forceinline__ void lb_publish(uint64_t* st, uint32_t lane, const Fe& v, uint32_t kind) {
+  if (lane < 6) lb_store(st + (kind == 2 ? 8 : 0) + lane, lb_piece(v, lane) | (kind == 2 ? LB_TAG_INC : LB_TAG_AGG));
+  if (lane == 0) lb_store(st + 15, kind);
+}
+// the value of kind `kind` of block state st; false while a piece is not yet visible
+__device__ __forceinline__ bool lb_read(const uint64_t* st, uint32_t kind, Fe& v) {
+  uint64_t w[6];
+  const uint64_t tag = kind == 2 ? LB_TAG_INC : LB_TAG_AGG;
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    w[i] = lb_load(st + (kind == 2 ? 8 : 0) + i);
+    ok &= (w[i] & ~LB_M48) == tag;
+  }
+  v = lb_join(w);
+  return ok;
+}
+
+// One column's values of a wave's 64 ZR rows r0 .. (lane l holds rows r0 + ZR l + j in v[j]) to
+// dst rows below lim as 1 KiB runs: 128 / ZR lanes at a time stage their 128 rows in the wave's
+// LDS (a (2 ZR + 1) x 16-byte lane stride: conflict-free 16-byte writes) and the wave stores them
+// with four 1 KiB instructions.
+constexpr int ZLPS = 128 / ZR;          // lanes per staging round
+constexpr int ZLST = 2 * ZR + 1;        // uint4 per staged lane (padded)
+constexpr int ZSTAGE = ZLPS * ZLST;     // uint4 of staging per wave
+template <bool NT>
+__device__ __forceinline__ void wave_store_zr(uint64_t* dst, uint4* st, uint32_t lane, const Fe (&v)[ZR],
+                                              uint32_t r0, uint32_t lim) {
+  // the wave's rows are 128 ZR consecutive 16-byte chunks from a uniform base: chunk 256 h + 64 q
+  // + lane is staged at q (32 / ZR) ZLST + ZLST (lane / 2 ZR) + lane % 2 ZR of round h
+  uint4* d = reinterpret_cast<uint4*>(dst + 4ull * r0);
+  const uint32_t rem2 = lim > r0 ? (lim - r0 < 64u * ZR ? 2 * (lim - r0) : 128u * ZR) : 0u;  // chunks below lim
+  const uint32_t rd = ZLST * (lane / (2 * ZR)) + lane % (2 * ZR);
+#pragma unroll
+  for (uint32_t h = 0; h < ZR / 2; h++) {
+    if (lane / ZLPS == h) {
+      const uint32_t li = lane % ZLPS;
+#pragma unroll
+      for (int j = 0; j < ZR; j++) {
+        st[li * ZLST + 2 * j] = make_uint4(v[j].w[0], v[j].w[1], v[j].w[2], v[j].w[3]);
+        st[li * ZLST + 2 * j + 1] = make_uint4(v[j].w[4], v[j].w[5], v[j].w[6], v[j].w[7]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    uint4 x[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) x[q] = st[(32 / ZR) * ZLST * q + rd];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t ch = 256u * h + 64u * q + lane;
+      if (ch < rem2) gp::put16<NT>(d + ch, x[q]);
+    }
+  }
+}
+
+// last index r with a[r] <= v (a nondecreasing over TROWS entries, a[0] <= v): the top levels
+// of the search over the workgroup's LDS sample s[k] = a[SAMP k], then the SAMP entries of that
+// block (64 or 128 contiguous bytes, all loads in flight at once) in registers.
 __device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, const uint32_t* s,
                                             uint32_t v) {
   uint32_t lo = 0, hi = SAMPLE;  // last k with s[k] <= v, in [lo, hi)
@@ -387,104 +596,260 @@ __device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, cons
     const uint32_t mid = (lo + hi) >> 1;
     if (s[mid] <= v) lo = mid; else hi = mid;
   }
-  const uint4* blk = reinterpret_cast<const uint4*>(a + 16 * lo);
-  const uint4 q0 = blk[0], q1 = blk[1], q2 = blk[2], q3 = blk[3];
-  const uint32_t e[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-  uint32_t n = 0;  // entries <= v (e[0] = s[lo] <= v; nondecreasing)
+  const uint4* blk = reinterpret_cast<const uint4*>(a + SAMP * lo);
+  uint4 q[SAMP / 4];
 #pragma unroll
-  for (int i = 1; i < 16; i++) n += e[i] <= v ? 1u : 0u;
-  return 16 * lo + n;
+  for (int i = 0; i < SAMP / 4; i++) q[i] = blk[i];
+  uint32_t n = 0;  // entries <= v (the first = s[lo] <= v; nondecreasing)
+#pragma unroll
+  for (int i = 0; i < SAMP / 4; i++)
+    n += (i ? (q[i].x <= v ? 1u : 0u) : 0u) + (q[i].y <= v ? 1u : 0u) + (q[i].z <= v ? 1u : 0u) +
+         (q[i].w <= v ? 1u : 0u);
+  return SAMP * lo + n;
 }
 
-#ifndef B2F_LK_NT
-#define B2F_LK_NT 3  // non-temporal stores: 1 the columns, 2 the factors, 3 both (permute pass
-                     // 552 us write-back, 546 columns only, 358 both: the write-back lines
-                     // evicted the gathered tables)
-#endif
-// The four columns and the grand product's factors, a lane per row (grid-stride over 64-row
-// groups): A = Tx[x], S = Tx[p] (row 0's value past the table), A' = Ts[r] for the run r holding
-// p (binary search of pos: the top 12 levels in the workgroup's LDS sample), S' = A' at a run
-// start, else leftover item L - 1 - j for the j-th repeated row (halo2 hands leftovers out in
-// ascending order, each to the last open repeated row), found by binary search of LP. Each
-// column's 64 values of a wave go out as 1 KiB non-temporal stores (gp::wave_store_rows), the
-// factors to their chunk-interleaved slots (gp::wave_store_slots). Measured the searches cost
-// about what a separate rank-expansion pass (run-start / leftover marks and wave max-scans)
-// did, so they stay: r04e, 1.319 vs 1.321-1.332 ms per call.
-template <class F>
-__global__ __launch_bounds__(256) void lk_permute_kernel(
+// The five columns of one look-back block (LB = 256 ZR rows). Lane t of the workgroup owns rows
+// base + ZR t + j:
+//  1. searches: A' = Ts[r] for the run r holding p (binary search of pos: the top levels in the
+//     workgroup's LDS sample), S' = A' at a run start, else leftover item L - 1 - j for the j-th
+//     repeated row (halo2 hands leftovers out in ascending order, each to the last open repeated
+//     row), found by binary search of LP;
+//  2. the den side: A', S' staged and stored as 1 KiB runs, den_j = (A' + beta)(S' + gamma), the
+//     in-lane den suffix and the lane's den total; one wave scans the 256 den totals (suffix)
+//     and publishes the block's den product as its look-back aggregate at once;
+//  3. the num side: A = Tx[x] (x the dense cell), S = Tx[p] (row 0's value past the table),
+//     num_j, the in-lane num prefix, Q_j = Nloc_j Dsuf_(j+1); another wave scans the 256 num
+//     totals (prefix) while the den wave looks back over the blocks after this one (64 per step)
+//     for the den product after the block -- its predecessors have had the whole num side to
+//     publish -- and publishes its inclusive product;
+//  4. z[p + 1] = (num prefix before the lane) (den suffix after the lane, times NK_b Dafter_b) Q_j.
+// The scans run on waves chosen by the ticket, so the SIMDs share them; the LDS sample of the
+// searches is reused for the lane totals once every wave has searched.
+template <class F, bool MONT>
+__global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES))) void lk_zpass_kernel(
     const uint32_t* __restrict__ adv, uint64_t total_rows, const uint64_t* __restrict__ row_begin,
-    uint32_t c0, uint64_t usable, const Fe* __restrict__ Tx, const Fe* __restrict__ Ts,
-    bool mont, uint64_t* __restrict__ out, uint64_t out_rows, Chal ch, Fe* __restrict__ num,
-    Fe* __restrict__ den, const uint32_t* __restrict__ pos, const uint32_t* __restrict__ dcnt,
-    const uint32_t* __restrict__ lp, const uint32_t* __restrict__ samp) {
-  __shared__ uint4 stage[4][128];
-  const uint32_t c = blockIdx.y, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  __shared__ uint32_t sP[SAMPLE], sL[SAMPLE];
+    uint32_t c0, uint32_t g, uint64_t usable, uint64_t nb, const Fe* __restrict__ Tx,
+    const Fe* __restrict__ Ts, uint64_t* __restrict__ out, uint64_t out_rows, Chal ch,
+    const uint32_t* __restrict__ pos, const uint32_t* __restrict__ dcnt, const uint32_t* __restrict__ lp,
+    const uint32_t* __restrict__ samp, const Fe* __restrict__ NK, const Fe* __restrict__ Dnum,
+    uint64_t* __restrict__ lbs, uint32_t* __restrict__ ticket, int* __restrict__ sticky) {
+  // the search samples, then (after every wave has searched) the lane totals
+  static_assert(ZT == 256, "the scans take 4 lane totals per lane");
+  constexpr int SMEM = 2 * SAMPLE * 4 > 2 * ZT * 32 ? 2 * SAMPLE * 4 : 2 * ZT * 32;
+  __shared__ uint4 smem[SMEM / 16];
+  uint32_t* sP = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* sL = sP + SAMPLE;
+  Fe* sN = reinterpret_cast<Fe*>(smem);
+  Fe* sD = sN + ZT;
+  __shared__ uint4 stage[4][ZSTAGE];  // per wave: the column staging
+  __shared__ Fe sX[64], sDb;          // the den wave's exclusive values and block product, parked
+  __shared__ uint32_t s_tk;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  LKCLK_DECL
+  if (t == 0) s_tk = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint32_t tk = s_tk;
+  // descending block order: every circuit's last block first
+  const uint32_t c = tk % g;
+  const uint64_t b = nb - 1 - tk / g;
   {
     const uint4* sa = reinterpret_cast<const uint4*>(samp + (uint64_t)c * 2 * SAMPLE);
-    uint4* sp4 = reinterpret_cast<uint4*>(sP);
-    uint4* sl4 = reinterpret_cast<uint4*>(sL);
-    for (uint32_t i = threadIdx.x; i < (uint32_t)SAMPLE / 4; i += 256) {
-      sp4[i] = sa[i];
-      sl4[i] = sa[SAMPLE / 4 + i];
-    }
+    for (uint32_t i = t; i < (uint32_t)SAMPLE / 2; i += ZT) smem[i] = sa[i];
   }
-  __syncthreads();
-  uint4* st = stage[wv];
   const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
   const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
-  Fe* nm = num + (uint64_t)c * gp::elems(usable);
-  Fe* dn = den + (uint64_t)c * gp::elems(usable);
   const Circ k = circ(row_begin, total_rows, usable, c0 + c);
+  // 32-bit row arithmetic (usable <= 2^31, b2f_lookup_columns_dev)
+  const uint32_t us = (uint32_t)usable, n_in = (uint32_t)k.n_in;
+  const uint32_t* a1 = adv + total_rows + k.first;  // the circuit's dense cells
   const uint32_t* P = pos + (uint64_t)c * TROWS;
   const uint32_t* D = dcnt + (uint64_t)c * TROWS;
   const uint32_t* L = lp + (uint64_t)c * TROWS;
-  const uint32_t n_left = (uint32_t)usable - D[TROWS - 1];  // repeated rows = leftover items
+  const uint32_t n_left = us - D[TROWS - 1];  // repeated rows = leftover items
   uint64_t* o = out + (uint64_t)(c0 + c) * 5 * out_rows * 4;
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t base = (uint64_t)blockIdx.x * 256 + 64 * wv; base < usable; base += stride) {
-    const uint64_t p = base + lane;
-    const bool in = p < usable;
-    const uint32_t nv = (uint32_t)(usable - base < 64 ? usable - base : 64);
-    const uint32_t x = p < k.n_in ? (adv[total_rows + k.first + p] & 0xffffu) : 0u;
-    uint2 r = make_uint2(0u, 0u);  // ranks of A'[p] and S'[p]
-    if (in) {
-      r.x = last_le(P, sP, (uint32_t)p);
-      r.y = P[r.x] == (uint32_t)p ? r.x : last_le(L, sL, n_left - 1u - ((uint32_t)p - D[r.x]));
-    }
-#ifndef B2F_LK_ABL
-#define B2F_LK_ABL 0  // diagnostics (variant builds only): 1 no gathers, 2 no products, 4 no column stores
-#endif
-#if B2F_LK_ABL & 1
-    Fe a = beta, sv = gamma, ap = beta, sp = gamma;
-    a.w[0] ^= x; sv.w[0] ^= (uint32_t)p; ap.w[0] ^= r.x; sp.w[0] ^= r.y;
-#else
-    const Fe a = Tx[x];
-    const Fe sv = Tx[p < (uint64_t)TROWS ? (uint32_t)p : 0u];
-    const Fe ap = Ts[r.x];
-    const Fe sp = Ts[r.y];
-#endif
-    if (!(B2F_LK_ABL & 4)) {
-      gp::wave_store_rows<B2F_LK_NT & 1>(o + 4 * base, st, lane, out_form<F>(a, mont), nv);
-      gp::wave_store_rows<B2F_LK_NT & 1>(o + (out_rows + base) * 4, st, lane, out_form<F>(sv, mont), nv);
-      gp::wave_store_rows<B2F_LK_NT & 1>(o + (2 * out_rows + base) * 4, st, lane, out_form<F>(ap, mont), nv);
-      gp::wave_store_rows<B2F_LK_NT & 1>(o + (3 * out_rows + base) * 4, st, lane, out_form<F>(sp, mont), nv);
-    }
-    // the grand product's factors (A + beta)(S + gamma) / ((A' + beta)(S' + gamma)); rows past
-    // `usable` land in slots of the last tile that the grand product never reads
-    const uint64_t sb = (base / (gp::ZC * gp::ZC)) * (gp::ZC * gp::ZC) + (base / gp::ZC) % gp::ZC;
-    if (B2F_LK_ABL & 2) {
-      gp::wave_store_slots<(B2F_LK_NT >> 1) & 1>(nm + sb, st, lane, field::add<F>(field::add<F>(a, beta), field::add<F>(sv, gamma)));
-      gp::wave_store_slots<(B2F_LK_NT >> 1) & 1>(dn + sb, st, lane, field::add<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma)));
-    } else {
-      gp::wave_store_slots<(B2F_LK_NT >> 1) & 1>(nm + sb, st, lane, field::mul<F>(field::add<F>(a, beta), field::add<F>(sv, gamma)));
-      gp::wave_store_slots<(B2F_LK_NT >> 1) & 1>(dn + sb, st, lane, field::mul<F>(field::add<F>(ap, beta), field::add<F>(sp, gamma)));
+  const uint32_t base = (uint32_t)b * LB, p0 = base + ZR * t, r0 = base + 64u * ZR * wv;
+  uint4* st = stage[wv];
+  // lane totals sit transposed (entry i at (i % 4) 64 + i / 4): a scanning lane's 4 entries are
+  // 64 elements apart and its neighbours' adjacent (4-entry rows put lanes 128 B apart on the
+  // same banks)
+  auto pz = [](uint32_t i) { return (i & 3u) * 64u + (i >> 2); };
+  const uint32_t wn = tk & 3u, wd = (tk + 1) & 3u;  // the num-scan and den-scan waves
+  const uint32_t e0 = 4 * lane;                     // a scanning lane's first entry
+  __syncthreads();
+  LKCLK(0);
+  // 1. the searches
+  uint32_t x[ZR], ra[ZR], rs[ZR];
+#pragma unroll
+  for (int j = 0; j < ZR; j++) {
+    const uint32_t p = p0 + j;
+    x[j] = p < n_in ? (a1[p] & 0xffffu) : 0u;
+    ra[j] = rs[j] = 0;
+    if (p < us) {
+      ra[j] = last_le(P, sP, p);
+      rs[j] = P[ra[j]] == p ? ra[j] : last_le(L, sL, n_left - 1u - (p - D[ra[j]]));
     }
   }
+  LKCLK(1);
+  // 2. the den side: A', S' -> d[j] = den_j, the in-lane suffix sf[j] = prod_{i > j} d_i, dl
+  Fe a[ZR], d[ZR], v[ZR];
+#pragma unroll
+  for (int j = 0; j < ZR; j++) v[j] = Ts[ra[j]];
+#pragma unroll
+  for (int j = 0; j < ZR; j++) {
+    d[j] = field::add<F>(v[j], beta);
+    v[j] = gp::out_form<F>(v[j], MONT);
+  }
+  wave_store_zr<true>(o + 2 * out_rows * 4, st, lane, v, r0, us);
+#pragma unroll
+  for (int j = 0; j < ZR; j++) v[j] = Ts[rs[j]];
+#pragma unroll
+  for (int j = 0; j < ZR; j++) {
+    d[j] = p0 + j < us ? field::mul<F>(d[j], field::add<F>(v[j], gamma)) : field::one<F>();
+    v[j] = gp::out_form<F>(v[j], MONT);
+  }
+  wave_store_zr<true>(o + 3 * out_rows * 4, st, lane, v, r0, us);
+  Fe sf[ZR];
+  sf[ZR - 2] = d[ZR - 1];
+#pragma unroll
+  for (int j = ZR - 3; j >= 0; j--) sf[j] = field::mul<F>(d[j + 1], sf[j + 1]);
+  sD[pz(t)] = field::mul<F>(d[0], sf[0]);  // every wave has searched: the samples are free
+  __syncthreads();
+  LKCLK(2);
+  // the den wave: its in-lane scan (suffix order: entry i of the scan is lane total 255 - i) and
+  // the 6-level scan across its lanes; the block's product goes out as the aggregate at once
+  uint64_t* my = lbs + ((uint64_t)c * nb + b) * LBS_WORDS;
+  auto atd = [&](uint32_t i) { return pz(255u - i); };
+  if (wv == wd) {
+    Fe Pd = sD[atd(e0)];
+    sD[atd(e0)] = field::one<F>();
+#pragma unroll 1
+    for (uint32_t k2 = 1; k2 < 4; k2++) {
+      const Fe e = sD[atd(e0 + k2)];
+      sD[atd(e0 + k2)] = Pd;
+      Pd = field::mul<F>(Pd, e);
+    }
+#pragma unroll 1
+    for (int off = 1; off < 64; off <<= 1) {
+      const Fe y = shfl_fe(Pd, (int)lane - off);
+      const Fe m = field::mul<F>(y, Pd);
+      if (lane >= (uint32_t)off) Pd = m;
+    }
+    Fe X = shfl_fe(Pd, (int)lane - 1);
+    if (lane == 0) X = field::one<F>();
+    const Fe Db = shfl_fe(Pd, 63);
+    if (b + 1 < nb) lb_publish(my, lane, Db, 1);
+    sX[lane] = X;  // parked in LDS across the num side (registers are the limit there)
+    if (lane == 0) sDb = Db;
+  }
+  LKCLK(3);
+  // 3. the num side: A, S -> a[j] = num_j -> Nloc_j; Q_j = Nloc_j Dsuf_(j+1) (kept in v)
+#pragma unroll
+  for (int j = 0; j < ZR; j++) v[j] = Tx[x[j]];
+#pragma unroll
+  for (int j = 0; j < ZR; j++) {
+    a[j] = field::add<F>(v[j], beta);
+    v[j] = gp::out_form<F>(v[j], MONT);
+  }
+  wave_store_zr<true>(o, st, lane, v, r0, us);
+#pragma unroll
+  for (int j = 0; j < ZR; j++) v[j] = Tx[p0 + j < (uint32_t)TROWS ? p0 + j : 0u];
+#pragma unroll
+  for (int j = 0; j < ZR; j++) {
+    a[j] = p0 + j < us ? field::mul<F>(a[j], field::add<F>(v[j], gamma)) : field::one<F>();
+    v[j] = gp::out_form<F>(v[j], MONT);
+  }
+  wave_store_zr<true>(o + out_rows * 4, st, lane, v, r0, us);
+#pragma unroll
+  for (int j = 1; j < ZR; j++) a[j] = field::mul<F>(a[j - 1], a[j]);
+#pragma unroll
+  for (int j = 0; j < ZR - 1; j++) v[j] = field::mul<F>(a[j], sf[j]);
+  v[ZR - 1] = a[ZR - 1];
+  sN[pz(t)] = a[ZR - 1];
+  __syncthreads();
+  LKCLK(4);
+  if (wv == wn) {
+    // the num wave: the exclusive prefix of the 256 num totals, in place
+    Fe Pn = sN[pz(e0)];
+    sN[pz(e0)] = field::one<F>();
+#pragma unroll 1
+    for (uint32_t k2 = 1; k2 < 4; k2++) {
+      const Fe e = sN[pz(e0 + k2)];
+      sN[pz(e0 + k2)] = Pn;
+      Pn = field::mul<F>(Pn, e);
+    }
+#pragma unroll 1
+    for (int off = 1; off < 64; off <<= 1) {
+      const Fe y = shfl_fe(Pn, (int)lane - off);
+      const Fe m = field::mul<F>(y, Pn);
+      if (lane >= (uint32_t)off) Pn = m;
+    }
+    Fe Xn = shfl_fe(Pn, (int)lane - 1);
+    if (lane == 0) Xn = field::one<F>();
+    sN[pz(e0)] = Xn;
+#pragma unroll 1
+    for (uint32_t k2 = 1; k2 < 4; k2++) sN[pz(e0 + k2)] = field::mul<F>(Xn, sN[pz(e0 + k2)]);
+  } else if (wv == wd) {
+    // the den wave: the look-back over the blocks after b. Lane i watches block q0 + i's status
+    // word; the blocks up to the first inclusive one (fi) must all have published, then their
+    // values are read and multiplied.
+    Fe after = field::one<F>();
+    if (b + 1 < nb) {
+      uint64_t q0 = b + 1;
+      while (true) {
+        const uint64_t qb = q0 + lane;
+        const uint32_t s = qb < nb ? (uint32_t)lb_load(lbs + ((uint64_t)c * nb + qb) * LBS_WORDS + 15) : 2u;
+        const uint64_t inc = __ballot(s == 2), none = __ballot(s == 0);
+        const uint32_t fi = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+        const uint64_t need = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
+        LKCLK(10);
+        if (none & need) {
+          __builtin_amdgcn_s_sleep(8);
+          continue;
+        }
+        Fe val = field::one<F>();
+        bool ok = true;
+        if (lane <= fi && qb < nb) ok = lb_read(lbs + ((uint64_t)c * nb + qb) * LBS_WORDS, s, val);
+        if (__ballot(!ok)) {
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        // the product of lanes 0 .. min(fi, 63) (the others hold 1) into lane 0
+#pragma unroll 1
+        for (uint32_t m = 1; m <= fi && m < 64; m <<= 1) val = field::mul<F>(val, shfl_xor_fe(val, (int)m));
+        after = field::mul<F>(after, shfl_fe(val, 0));
+        if (fi < 64) break;
+        q0 += 64;
+      }
+    }
+    LKCLK(9);
+    const Fe incl = field::mul<F>(sDb, after);
+    lb_publish(my, lane, incl, 2);
+    if (lane == 0 && b == 0) {
+      // the den product of the permuted columns against the num side's D
+      const Fe dn = Dnum[c];
+      uint32_t diff = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) diff |= dn.w[i] ^ incl.w[i];
+      if (diff && sticky) atomicOr(sticky, 1 << B2F_ERR_CHECK);
+      field::store(o + 4 * out_rows * 4, gp::out_form<F>(field::one<F>(), MONT));  // z[0] = 1
+    }
+    // the block's factor NK_b Dafter_b (Nbefore_b D^-1 Dafter_b) rides on the den side's
+    // exclusive values, so a lane's K is one product: (num prefix) (den suffix)
+    const Fe X = field::mul<F>(sX[lane], field::mul<F>(NK[(uint64_t)c * nb + b], after));
+    sD[atd(e0)] = X;
+#pragma unroll 1
+    for (uint32_t k2 = 1; k2 < 4; k2++) sD[atd(e0 + k2)] = field::mul<F>(X, sD[atd(e0 + k2)]);
+  }
+  __syncthreads();
+  LKCLK(5);
+  // 4. z
+  const Fe K = field::mul<F>(sN[pz(t)], sD[pz(t)]);
+#pragma unroll
+  for (int j = 0; j < ZR; j++) v[j] = gp::out_form<F>(field::mul<F>(K, v[j]), MONT);
+  wave_store_zr<true>(o + 4 * out_rows * 4 + 4, st, lane, v, r0, us);
+  LKCLK(6);
+  LKCLK_END
 }
-
-using gp::ZC;
 
 struct Carve {
   Fe* Tx;
@@ -499,12 +864,14 @@ struct Carve {
   uint32_t* lp;
   uint32_t* samp;  // group x 2 x SAMPLE
   uint32_t* part;  // group x SC_PARTS x 3 (rank-scan part totals)
-  Fe* num;  // group x usable
-  Fe* den;
-  Fe* zs;  // group x gp::scratch_elems
-  Fe* dpart;  // (group + 1) x DP_PARTS (lk_dtot_kernel)
+  Fe* partA;  // group x nb: block num products, the A part
+  Fe* partS;  // nb: the S part (every circuit's)
+  Fe* NK;     // group x nb: Nbefore_b D^-1
+  Fe* Dnum;   // group: D from the num side
+  uint64_t* lbs;     // group x nb x LBS_WORDS look-back state, then the ticket counter
   void* sort_tmp;
   size_t sort_bytes;
+  size_t lbs_bytes;
   size_t total;
 };
 
@@ -524,6 +891,7 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
     off += (bytes + 255) & ~(size_t)255;
     return r;
   };
+  const uint64_t nb = n_lb(usable);
   k.Tx = (Fe*)take(sizeof(Fe) * TROWS);
   k.Ts = (Fe*)take(sizeof(Fe) * TROWS);
   k.key = (uint64_t*)take(8ull * 4 * TROWS);
@@ -536,10 +904,12 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.lp = (uint32_t*)take(4ull * TROWS * group);
   k.samp = (uint32_t*)take(8ull * SAMPLE * group);
   k.part = (uint32_t*)take(12ull * SC_PARTS * group);
-  k.num = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);  // chunk-interleaved (b2f_gprod.h)
-  k.den = (Fe*)take(sizeof(Fe) * gp::elems(usable) * group);
-  k.zs = (Fe*)take(sizeof(Fe) * gp::scratch_elems(usable) * group);
-  k.dpart = (Fe*)take(sizeof(Fe) * DP_PARTS * (group + 1));
+  k.partA = (Fe*)take(sizeof(Fe) * nb * group);
+  k.partS = (Fe*)take(sizeof(Fe) * nb);
+  k.NK = (Fe*)take(sizeof(Fe) * nb * group);
+  k.Dnum = (Fe*)take(sizeof(Fe) * group);
+  k.lbs_bytes = 8ull * LBS_WORDS * nb * group + 64;  // + the ticket counter
+  k.lbs = (uint64_t*)take(k.lbs_bytes);
   k.sort_bytes = sort_temp_bytes();
   k.sort_tmp = take(k.sort_bytes);
   k.total = off;
@@ -552,6 +922,7 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
                       uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad, void* scratch,
                       uint32_t group, int* sticky, const gp::Side& side, hipStream_t s) {
   Carve k = carve(scratch, group, usable_rows);
+  const uint64_t nb = n_lb(usable_rows);
   const dim3 tb(TROWS / 256);
   hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm);
   // one radix sort by the top limb of the canonical value (< 2^63: both moduli are < 2^255),
@@ -567,42 +938,46 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   hipLaunchKernelGGL(lk_rank_kernel, tb, dim3(256), 0, s, k.Tx, pa, k.Ts);
   hipError_t e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s);
   if (e != hipSuccess) return e;
-  // Per group: the count / scan / permute passes over all its circuits at once (a workgroup
-  // count per circuit that fills the chip), then the grand products. The den totals' inverses
-  // D^-1 come from the rows on the side stream (lk_dtot_kernel, lk_dinv_kernel), forked at the
-  // group's start (after the previous group's gp_write, which read the same D^-1 slots), so the
-  // inversions' latency hides behind the count, scan and permute passes. (r04m: with D taken from
-  // the den chunk totals, each half of the group's inversion still held its gp_write 25-52 us
-  // after two-way pipelining, 1.24-1.27 ms per call.)
+  // Per group: the num side (block products, their prefix, D and D^-1) on the side stream,
+  // forked at the group's start (after the previous group's z pass, which read the same NK
+  // slots), beside the count and rank-scan passes; then the z pass over all the group's circuits
+  // (a workgroup count that fills the chip).
   for (uint32_t c0 = 0; c0 < n_circuits; c0 += group) {
     const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
-    const gp::Scratch zk = gp::scratch_of(k.zs, g, usable_rows);
     if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL(lk_dtot_kernel<F>, dim3(DP_PARTS, g + 1), dim3(DP_THREADS), 0, side.s2, d_advice,
-                       total_rows, d_row_begin, c0, g, usable_rows, k.Tx, ch, k.dpart);
-    hipLaunchKernelGGL(lk_dinv_kernel<F>, dim3(g), dim3(DP_PARTS), 0, side.s2, k.dpart, g, zk.dt, sticky);
+    hipLaunchKernelGGL(lk_npart_kernel<F>, dim3((uint32_t)((nb + 4 * NP_BPW - 1) / (4 * NP_BPW)), g + (c0 == 0 ? 1 : 0)), dim3(256), 0,
+                       side.s2, d_advice, total_rows, d_row_begin, c0, g, usable_rows, nb, k.Tx, ch, k.partA,
+                       k.partS);
+    hipLaunchKernelGGL(lk_nscan_kernel<F>, dim3(g), dim3(NS_T), 0, side.s2, nb, k.partA, k.partS, k.NK, k.Dnum,
+                       sticky);
     if ((e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;
     hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
                        total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
     hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
     hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
                        k.part, k.pos, k.dcnt, k.lp, k.samp);
-    // permute: ~4096 rows per workgroup
-    const uint32_t px = (uint32_t)((usable_rows + 4095) / 4096);
-    hipLaunchKernelGGL(lk_permute_kernel<F>, dim3(px, g), dim3(256), 0, s, d_advice, total_rows,
-                       d_row_begin, c0, usable_rows, k.Tx, k.Ts, mont, d_out, out_rows, ch, k.num,
-                       k.den, k.pos, k.dcnt, k.lp, k.samp);
-    e = gp::run_begin<F>(g, usable_rows, k.num, k.den, k.zs, sticky, side, s, false, true);
-    if (e == hipSuccess)
-      e = gp::run_end<F>(g, usable_rows, mont, d_out + ((uint64_t)c0 * 5 + 4) * out_rows * 4, 5 * out_rows * 4,
-                         k.num, k.den, k.zs, nullptr, nullptr, s, nullptr, side);
-    if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(k.lbs, 0, 8ull * LBS_WORDS * nb * g + 64, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(s, side.join, 0)) != hipSuccess) return e;
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(k.lbs + LBS_WORDS * nb * g);
+    hipLaunchKernelGGL((mont ? lk_zpass_kernel<F, true> : lk_zpass_kernel<F, false>), dim3((uint32_t)(nb * g)),
+                       dim3(ZT), 0, s, d_advice, total_rows, d_row_begin, c0, g, usable_rows, nb, k.Tx, k.Ts,
+                       d_out, out_rows, ch, k.pos, k.dcnt, k.lp, k.samp, k.NK, k.Dnum, k.lbs, ticket, sticky);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;
 }
 
 }  // namespace
+
+#ifdef B2F_LK_CLOCK
+extern "C" __attribute__((visibility("default"))) int b2f_debug_lk_clock(uint64_t* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lk_clock), sizeof(g_lk_clock)) != hipSuccess) return B2F_ERR_HIP;
+  unsigned long long zero[16] = {};
+  zero[13] = ~0ull;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_lk_clock), zero, sizeof(zero)) == hipSuccess ? B2F_OK : B2F_ERR_HIP;
+}
+#endif
 
 size_t lookup_scratch_bytes(uint32_t group, uint64_t usable_rows) {
   return carve(nullptr, group, usable_rows).total;
