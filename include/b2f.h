@@ -54,9 +54,10 @@ extern "C" {
 #define B2F_ERR_INPUT 6     /* malformed EIP-152 input (length != 213 or f not 0/1) */
 #define B2F_ERR_FIELD 7     /* (at b2f_sync) a grand product's denominator product is zero: a
                                challenge collides with a cell value, its z column is meaningless */
-#define B2F_ERR_CHECK 8     /* (at b2f_sync) a prover-column call's internal cross-check failed
-                               (the lookup's permuted columns do not multiply to the product of
-                               its input columns): its columns are wrong -- a library defect */
+#define B2F_ERR_CHECK 8     /* (at b2f_sync) an internal cross-check failed -- a library defect:
+                               the lookup's permuted columns do not multiply to the product of
+                               its input columns (its columns are wrong), or the fused pass's
+                               long-instance segment list overflowed (its verdict reads unclean) */
 
 /* One EIP-152 compression: the reference's Blake2fWitness{rounds, h, m, t, f}
  * (blake2f.rs:208-239), 216 bytes, naturally aligned. f must be 0 or 1. */
@@ -307,6 +308,18 @@ B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, 
                                         uint64_t* d_sigma, uint64_t* d_z, uint64_t out_rows,
                                         void* stream);
 
+/* Keygen's permutation polynomials alone (halo2_proofs 0.3.0 plonk/permutation/keygen.rs
+ * build_pk: the sigma columns depend on the circuit's structure, not on a witness): the same
+ * d_sigma that b2f_permutation_columns_dev writes for the row map h_offsets[0..n], domain 2^k,
+ * omega, delta and `form` -- sigma_j(w^i) = delta^c' w^r' at d_sigma[(j * out_rows + i) * 4 +
+ * limb], j < 8, every row i < 2^k. A prover computes it once per circuit shape and then calls
+ * b2f_permutation_columns_dev with d_sigma = NULL per proof (the z columns never read sigma).
+ * h_offsets[n] - h_offsets[0] < 2^k, out_rows >= 2^k, d_sigma 16-byte aligned. Asynchronous on
+ * `stream` after the same short host setup. */
+B2F_API int b2f_permutation_sigma_dev(b2f_ctx* ctx, const uint64_t* h_offsets, size_t n, uint32_t k,
+                                      const uint64_t omega[4], const uint64_t delta[4], uint32_t form,
+                                      uint64_t* d_sigma, uint64_t out_rows, void* stream);
+
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel the
  * fill/eval calls launch (no host synchronization while recording). b2f_set_timing(ctx, 1)
  * clears the log and starts recording; b2f_kernel_times waits for the recorded events and
@@ -319,7 +332,8 @@ B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, 
 #define B2F_KERNEL_FILL_EVAL 4 /* fused trace expansion + constraint evaluation */
 #define B2F_KERNEL_LOOKUP 5 /* lookup-argument prover columns (all passes of one call) */
 #define B2F_KERNEL_PERM 6   /* permutation-argument prover columns (all passes of one call) */
-#define B2F_NUM_KERNELS 7
+#define B2F_KERNEL_PERM_SIGMA 7 /* permutation keygen: the sigma columns (b2f_permutation_sigma_dev) */
+#define B2F_NUM_KERNELS 8
 B2F_API int b2f_set_timing(b2f_ctx* ctx, int enable);
 B2F_API int b2f_kernel_times(b2f_ctx* ctx, double* total_ms, uint32_t* count);
 

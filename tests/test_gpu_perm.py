@@ -186,3 +186,47 @@ def test_zero_denominator_is_reported(engine, batch):
     batch.permutation_columns(engine, k, (1 << k) - 7, 3, 5, chunk_len=3, form=1, sigma=False)
     batch.lookup_columns(engine, [0], usable, 7, 3, 11, form=1)
     engine.sync(s)
+
+
+@pytest.mark.parametrize("form", [1, 2])
+def test_permutation_sigma_keygen_equals_columns_call(engine, batch, form):
+    """sigma is keygen (build_pk), so b2f_permutation_sigma_dev computes it
+    alone, once per circuit shape; it equals the sigma columns the full call writes (which the
+    oracle pins above), and the per-proof call without sigma writes the same z."""
+    import torch
+
+    k, usable = 12, (1 << 12) - 7
+    p = _p(form)
+    sig, z = batch.permutation_columns(engine, k, usable, 7, 11, chunk_len=3, form=form,
+                                       instances=(1, 4))
+    sk = batch.permutation_sigma(engine, k, form=form, instances=(1, 4))
+    _, z2 = batch.permutation_columns(engine, k, usable, 7, 11, chunk_len=3, form=form,
+                                      instances=(1, 4), sigma=False)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(sk, sig)
+    assert torch.equal(z2[:, :usable + 1], z[:, :usable + 1])
+    assert p  # the field of the form
+
+
+def test_permutation_sigma_argument_errors(engine, batch):
+    import b2f
+    import torch
+
+    s = torch.cuda.current_stream().cuda_stream
+    sig = torch.empty((8, 1 << 12, 4), dtype=torch.int64, device=batch.advice.device)
+    off = batch.offsets_host
+    w, d = pm.domain(pm.P_PALLAS, 12)
+    bad_off = off.copy()
+    bad_off[2] += 4
+    for kw, code in [({"k": 9}, b2f._lib.ERR_ARG), ({"k": 31}, b2f._lib.ERR_ARG),
+                     ({"form": 4}, b2f._lib.ERR_ARG), ({"delta": pm.P_PALLAS}, b2f._lib.ERR_ARG),
+                     ({"out_rows": 100}, b2f._lib.ERR_ROWS), ({"k": 10}, b2f._lib.ERR_ROWS),
+                     ({"offs": bad_off}, b2f._lib.ERR_LAYOUT)]:
+        a = dict(k=12, form=1, delta=d, out_rows=1 << 12, offs=off)
+        a.update(kw)
+        with pytest.raises(b2f.B2FError) as e:
+            engine.permutation_sigma_dev(a["offs"], a["k"], w, a["delta"], a["form"], sig.data_ptr(),
+                                         a["out_rows"], s)
+        assert e.value.code == code, kw
+    engine.permutation_sigma_dev(off, 12, w, d, 1, sig.data_ptr(), 1 << 12, s)
+    engine.sync(s)

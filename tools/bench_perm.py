@@ -1,6 +1,7 @@
-"""Throughput of the permutation-argument prover columns (b2f_permutation_columns_dev): a
-circuit of 2^k rows filled with 12-round instances, sigma + grand products timed with HIP
-events (b2f_kernel_times). One JSON line per form."""
+"""Throughput of the permutation-argument prover columns: a circuit of 2^k rows filled with
+12-round instances; the per-proof z call (b2f_permutation_columns_dev without sigma) and the
+keygen sigma call (b2f_permutation_sigma_dev) timed with HIP events (b2f_kernel_times). One
+JSON line per form."""
 import argparse
 import json
 import os
@@ -32,19 +33,24 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     eng.sync(s)
     for form in [int(f) for f in args.forms.split(",")]:
-        batch.permutation_columns(eng, args.k, usable, 3, 5, chunk_len=args.chunk, form=form)
+        batch.permutation_columns(eng, args.k, usable, 3, 5, chunk_len=args.chunk, form=form, sigma=False)
+        sig = batch.permutation_sigma(eng, args.k, form=form)
         eng.sync(s)
         eng.set_timing(True)
         for _ in range(args.reps):
-            sig, z = batch.permutation_columns(eng, args.k, usable, 3, 5, chunk_len=args.chunk,
-                                               form=form)
+            _, z = batch.permutation_columns(eng, args.k, usable, 3, 5, chunk_len=args.chunk,
+                                             form=form, sigma=False)
+            sig = batch.permutation_sigma(eng, args.k, form=form)
         eng.sync(s)
-        ms, cnt = eng.kernel_times()["perm"]
-        per = ms / cnt
+        kt = eng.kernel_times()
+        ms, cnt = kt["perm"]
+        sms, scnt = kt["perm_sigma"]
+        per, sper = ms / cnt, sms / scnt
         sets = (8 + args.chunk - 1) // args.chunk
-        print(json.dumps({"k": args.k, "instances": n_inst, "form": form, "chunk_len": args.chunk,
-                          "ms_per_call": round(per, 3), "rows_per_s": round(n_rows / per * 1e3),
-                          "written_GBps": round(n_rows * 32 * (8 + sets) / per / 1e6, 1)}))
+        print(json.dumps({"lib": args.lib or "product", "k": args.k, "instances": n_inst, "form": form,
+                          "chunk_len": args.chunk, "z_ms_per_call": round(per, 3),
+                          "sigma_ms_per_call": round(sper, 3), "rows_per_s": round(n_rows / per * 1e3),
+                          "z_written_GBps": round(usable * 32 * sets / per / 1e6, 1)}))
         del sig, z
 
 

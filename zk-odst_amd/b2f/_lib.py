@@ -24,7 +24,8 @@ CODE_COPY = 17
 CODE_FIXED = 18
 CODE_LAYOUT = 19
 MAX_ROUNDS = 1 << 20
-KERNEL_NAMES = ["record", "fill", "eval", "export", "fill_eval", "lookup", "perm"]  # B2F_KERNEL_*
+KERNEL_NAMES = ["record", "fill", "eval", "export", "fill_eval", "lookup", "perm",
+                "perm_sigma"]  # B2F_KERNEL_*
 FP_CANONICAL, FP_MONTGOMERY, FP_BN254_CANONICAL, FP_BN254_MONTGOMERY = 0, 1, 2, 3  # B2F_FP_*
 
 OK, ERR_ARG, ERR_ROUNDS, ERR_ROWS, ERR_HIP, ERR_LAYOUT, ERR_INPUT, ERR_FIELD, ERR_CHECK = range(9)
@@ -89,6 +90,7 @@ SIGNATURES = [
     ("b2f_permutation_mapping", U64, [ctypes.c_uint32, P, U64]),
     ("b2f_permutation_columns_dev", I32, [P, P, U64, P, SIZE, ctypes.c_uint32, U64, P, P, P, P,
                                           ctypes.c_uint32, ctypes.c_uint32, P, P, U64, P]),
+    ("b2f_permutation_sigma_dev", I32, [P, P, SIZE, ctypes.c_uint32, P, P, ctypes.c_uint32, P, U64, P]),
     ("b2f_sync", I32, [P, P]),
     ("b2f_fill", I32, [P, P, SIZE, P, P, P]),
     ("b2f_eval", I32, [P, P, P, P, SIZE, U64, P]),

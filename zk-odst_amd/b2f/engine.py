@@ -180,6 +180,15 @@ class Engine:
             int(usable_rows), lim[0], lim[1], lim[2], lim[3], int(chunk_len), int(form),
             _vp(d_sigma) if d_sigma else None, _vp(d_z), int(out_rows), _vp(stream)))
 
+    def permutation_sigma_dev(self, h_offsets, k, omega, delta, form, d_sigma, out_rows, stream=0):
+        """b2f_permutation_sigma_dev (keygen: the sigma columns alone); omega/delta Python ints."""
+        off = np.ascontiguousarray(h_offsets, dtype=np.uint64)
+        lim = [(ctypes.c_uint64 * 4)(*[(int(v) >> (64 * i)) & (2**64 - 1) for i in range(4)])
+               for v in (omega, delta)]
+        self._check(self.lib.b2f_permutation_sigma_dev(
+            self.ctx, _np_ptr(off), len(off) - 1, int(k), lim[0], lim[1], int(form), _vp(d_sigma),
+            int(out_rows), _vp(stream)))
+
     def debug_eval_path(self):
         """Path of the last eval_dev call (device-synchronizing): 0 the fast clean-check pass
         found the trace clean, 1 it flagged something and the exact eval kernel reported, 2 no
@@ -326,6 +335,23 @@ class DeviceBatch:
                                     chunk_len, form, sig.data_ptr() if sigma else 0,
                                     z.data_ptr(), n_rows, s)
         return sig, z
+
+    def permutation_sigma(self, eng, k, form=_lib.FP_MONTGOMERY, instances=None, stream=None):
+        """Keygen's sigma columns (int64 [8, 2^k, 4]) of the circuit holding instances
+        [i0, i1) = `instances` (default: all): b2f_permutation_sigma_dev, the same columns
+        permutation_columns returns, without a witness."""
+        from . import field
+
+        torch = self.torch
+        i0, i1 = (0, self.n) if instances is None else instances
+        off = self.offsets_host[i0:i1 + 1]
+        f = field.of_form(form)
+        n_rows = 1 << int(k)
+        sig = torch.empty((8, n_rows, 4), dtype=torch.int64, device=self.advice.device)
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        eng.permutation_sigma_dev(off, k, field.omega(f, int(k)), field.delta(f), form, sig.data_ptr(),
+                                  n_rows, s)
+        return sig
 
     def report_dict(self):
         raw = self.report.cpu().numpy().view(np.uint64)

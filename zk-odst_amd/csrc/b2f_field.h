@@ -8,15 +8,18 @@
 // eight u32 words in the same byte order, so an element is stored exactly as the crates hold
 // it in memory.
 //
-// Multiply: CIOS over 8 x 32-bit words in plain HIP. A 32 x 32 + 32 + 32-bit step never
-// exceeds 64 bits and lowers to v_mad_u64_u32; the constant words of the modulus fold (pallas
-// has three zero words, a unit low word and a power-of-two top word). Both moduli have a top
-// word below 2^31 - 1, so the "no-carry" form applies: the running sum keeps 8 words, the
+// Multiply: Montgomery product by product scanning (Comba) over 8 x 32-bit words: each column
+// of the 512-bit sum of a_i b_j and m_i p_j accumulates in a 64-bit VGPR pair by inline-asm
+// v_mad_u64_u32 whose carry goes into a third word by v_addc (mul below); the zero words of the
+// modulus are skipped (pallas has three). Both moduli have a top word below 2^31 - 1, so the
 // result is < 2p and one conditional subtraction finishes it (the oracle and halo2 use the
-// textbook form; the result is the same canonical residue).
+// textbook form; the result is the same canonical residue). mul_cios keeps the operand-scanning
+// form it replaced, as tools/mulbench.hip's cross-check.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "b2f_safegcd.h"
 
 namespace b2f {
 namespace field {
@@ -472,6 +475,25 @@ __device__ Fe inv_kaliski(const Fe& a) {
     Y.w[i] = y[i];
   }
   return mul<F>(mul<F>(X, Y), fe_const<F>(F::R2));
+}
+
+// Montgomery-form inverse by Bernstein-Yang divsteps (b2f_safegcd.h) on the integer A = aR:
+// A^-1 = a^-1 R^-1, then one product with R^3 gives a^-1 R. About 20 steps of 30 divsteps and
+// two 2x2-matrix updates of 9-limb vectors against Kaliski's ~270 single-bit steps of 8-word
+// work (inv_kaliski, kept as a cross-check); one lane, a = 0 gives 0.
+template <class F>
+__device__ Fe inv_safegcd(const Fe& a) {
+  uint32_t x[8], pw[8], o[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    x[i] = a.w[i];
+    pw[i] = F::P[i];
+  }
+  sgcd::inverse(x, pw, o);
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.w[i] = o[i];
+  return mul<F>(r, fe_const<F>(F::R3));
 }
 
 __device__ __forceinline__ bool is_zero(const Fe& a) {

@@ -1081,7 +1081,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
                 uint32_t* __restrict__ fixed, const TileDesc* __restrict__ desc,
                 b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
                 uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk,
-                const uint64_t* __restrict__ seg, uint32_t* __restrict__ redo) {
+                const uint64_t* __restrict__ seg, uint64_t seg_cap, uint32_t* __restrict__ redo) {
   using namespace hr2;
   __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS];
   uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
@@ -1166,7 +1166,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
         fresh = false;
       } else if (fresh) {  // a later segment m of a long instance (the list, after the instances):
                            // half-rounds h0 = m SEG_HR .. from the recorded states h0 - 1 and h0
-        if (qs >= seg[0]) break;
+        if (qs >= (seg[0] < seg_cap ? seg[0] : seg_cap)) break;  // an overflow raised B2F_ERR_CHECK
         const uint64_t e = seg[1 + qs];
         qs += W;
         const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)(e >> 32));
@@ -2274,8 +2274,9 @@ hipError_t launch_eval_fast(const uint32_t* d_adv, const uint32_t* d_fixed, cons
   const uint64_t edge_tiles = (uint64_t)n + ((total_rows / 4) + PAD_Q - 1) / PAD_Q;
   const uint64_t edge_wgs = (edge_tiles + WAVES - 1) / WAVES;
   const uint32_t grid_e = (uint32_t)(edge_wgs < (uint64_t)cu_count * per_cu[1] ? edge_wgs : (uint64_t)cu_count * per_cu[1]);
-  // 2 workgroups per CU: like the fused half-round launch, a narrower front of tiles in flight
-  // reads faster than every workgroup that fits (same-process A/B 9.77 vs 9.87 ms)
+  // 2 workgroups per CU (the fused half-round launch runs 3): for this load-bound pass a
+  // narrower front of tiles in flight reads faster than every workgroup that fits
+  // (same-process A/B 9.77 vs 9.87 ms)
   int ev_per_cu = per_cu[0] < 2 ? per_cu[0] : 2;
 #ifdef B2F_DIAG  // diagnostics: workgroups per CU of the half-round pass
   if (const char* v = getenv("B2F_EVAL_PERCU")) {
@@ -2312,7 +2313,8 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                             uint32_t* d_fixed, void* scratch, uint64_t tiles,
                             b2f_eval_report* d_rep, const int* d_status, uint64_t inj_row,
                             uint32_t inj_col, uint32_t inj_mask, int mode, int cu_count,
-                            unsigned long long* clk, const uint64_t* seg, hipStream_t s) {
+                            unsigned long long* clk, const uint64_t* seg, uint64_t seg_cap,
+                            hipStream_t s) {
   TileDesc* desc = reinterpret_cast<TileDesc*>(scratch);
   uint64_t* defer = reinterpret_cast<uint64_t*>(desc + tiles);
   uint32_t* redo = reinterpret_cast<uint32_t*>(defer + 1 + DEFER_CAP);
@@ -2369,7 +2371,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   case M:                                                                                          \
     hipLaunchKernelGGL(fused_hr_kernel<M>, dim3(grid), dim3(FW * WAVES), 0, s, d_in, n, d_off,     \
                        total_rows, rec, d_adv, d_fixed, desc, d_rep, d_status, inj, defer, DEFER_CAP, \
-                       clk, seg, redo);                                                            \
+                       clk, seg, seg_cap, redo);                                                   \
     if (B2F_EDGE_SEPARATE)                                                                         \
       hipLaunchKernelGGL(fused_edge_kernel<M>, dim3(grid_e), dim3(FW * WAVES), 0, s, d_in, n, d_off, \
                          total_rows, rec, d_adv, d_fixed, redo, d_rep, d_status, inj, defer,       \

@@ -12,7 +12,7 @@
 //              exclusive prefix of the num totals and exclusive suffix of the den totals (zn /
 //              zd per chunk) and the block's totals (tn / td) -- Hillis-Steele in LDS;
 //   gp_total:  the den total D from the block totals;
-//   gp_inv:    D^-1 (one lane's Kaliski inversion, ~100 us of latency) and the closing values.
+//   gp_inv:    D^-1 (one lane's divsteps inversion, b2f_safegcd.h) and the closing values.
 //              It depends only on gp_total, so it runs on a second stream beside the scan;
 //   gp_scan:   K'_b = seed N_before(b) prod_{b' > b} D_b' per block (K = K' D^-1) and seed N
 //              (the closing value seed N / D = z[usable] before its D^-1);
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(TOT_T) void gp_total(uint64_t n, const Fe* __restri
   if (t == 0) dt[c] = p;
 }
 
-// D^-1 in place of D (one lane per product: Kaliski, ~100 us of latency; it needs only gp_total,
+// D^-1 in place of D (one lane per product: divsteps, b2f_safegcd.h; it needs only gp_total,
 // so it runs on the side stream beside the scans and gp_block_down). D = 0: some den factor is zero (a challenge
 // collides with a cell value). halo2's batch_invert would leave that entry zero and the proof
 // would fail; here every z would come from a meaningless inverse, so the call reports
@@ -263,10 +263,12 @@ __global__ __launch_bounds__(64) void gp_inv(Fe* __restrict__ dt, int* __restric
   __builtin_amdgcn_s_setprio(3);
   const Fe D = dt[c];
   if (sticky && field::is_zero(D)) atomicOr(sticky, 1 << B2F_ERR_FIELD);
-#ifdef B2F_INV_EUCLID  // diagnostics: the plain binary extended Euclid
+#if defined(B2F_INV_EUCLID)  // diagnostics: the plain binary extended Euclid
   dt[c] = field::inv<F>(D);
-#else
+#elif defined(B2F_INV_KALISKI)  // diagnostics: Kaliski's almost-inverse (round 4's)
   dt[c] = field::inv_kaliski<F>(D);
+#else
+  dt[c] = field::inv_safegcd<F>(D);
 #endif
 }
 

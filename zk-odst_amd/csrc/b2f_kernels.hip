@@ -43,6 +43,10 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
 hipError_t launch_spread_table(uint64_t usable_rows, uint32_t form, uint64_t* d_out,
                                uint64_t out_rows, hipStream_t s);
 size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst, uint32_t chunk_len);
+size_t perm_sigma_scratch_bytes(uint32_t k);
+hipError_t launch_permutation_sigma(const uint64_t* d_inst, size_t n_inst, const uint32_t* d_pool, uint32_t k,
+                                    const uint64_t* omega, const uint64_t* delta, uint32_t form,
+                                    uint64_t* d_sigma, uint64_t out_rows, void* scratch, hipStream_t s);
 hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0,
                               const uint64_t* d_inst, size_t n_inst, const uint32_t* d_pool,
                               uint32_t k, uint64_t usable_rows, const uint64_t* omega,
@@ -63,7 +67,8 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
                             uint32_t* d_fixed, void* scratch, uint64_t tiles,
                             b2f_eval_report* d_rep, const int* d_status, uint64_t inj_row,
                             uint32_t inj_col, uint32_t inj_mask, int mode, int cu_count,
-                            unsigned long long* clk, const uint64_t* seg, hipStream_t s);  // b2f_fused.hip
+                            unsigned long long* clk, const uint64_t* seg, uint64_t seg_cap,
+                            hipStream_t s);  // b2f_fused.hip
 }
 
 namespace {
@@ -168,6 +173,9 @@ __global__ void __launch_bounds__(BLOCK) record_kernel(const b2f_input* __restri
     const uint64_t at = atomicAdd(reinterpret_cast<unsigned long long*>(seg), (unsigned long long)nseg);
     for (uint64_t m = 1; m <= nseg; m++)
       if (at + m - 1 < seg_cap) seg[1 + at + m - 1] = ((uint64_t)i << 32) | m;
+    // the list is sized from an upper bound on the states, so this never fires; if it did, the
+    // fused launch drains only seg_cap entries and the call must not read clean
+    if (at + nseg > seg_cap) raise_error(status, sticky, rep, B2F_ERR_CHECK);
   }
   auto dump = [&](void) {
     if (!keep_state(k++)) {
@@ -1262,7 +1270,7 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
   HIPCHK(ctx, launch_fill_eval(d_in, (uint32_t)n, d_offsets, total_rows, ctx->d_rec, d_advice,
                                d_fixed, ctx->d_fz, tiles, d_report, ctx->d_status,
                                ctx->inj_row, ctx->inj_col, ctx->inj_mask, fmode,
-                               ctx->cu_count, ctx->d_clock, ctx->d_seg, s));
+                               ctx->cu_count, ctx->d_clock, ctx->d_seg, ctx->seg_cap ? ctx->seg_cap - 1 : 0, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
@@ -1483,22 +1491,18 @@ B2F_API uint64_t b2f_permutation_mapping(uint32_t rounds, uint32_t* out, uint64_
   return m.size();
 }
 
-B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t total_rows,
-                                        const uint64_t* h_offsets, size_t n, uint32_t k,
-                                        uint64_t usable_rows, const uint64_t omega[4],
-                                        const uint64_t delta[4], const uint64_t beta[4],
-                                        const uint64_t gamma[4], uint32_t chunk_len, uint32_t form,
-                                        uint64_t* d_sigma, uint64_t* d_z, uint64_t out_rows,
-                                        void* stream) {
-  if (!ctx) return B2F_ERR_ARG;
-  if (!d_advice || !h_offsets || !omega || !delta || !beta || !gamma || !d_z || n == 0)
-    return set_err(ctx, B2F_ERR_ARG, "permutation: null buffer or no instances");
-  if (form > B2F_FP_BN254_MONTGOMERY) return set_err(ctx, B2F_ERR_ARG, "permutation: unknown form %u", form);
-  if (chunk_len < 1 || chunk_len > PM_COLS)
-    return set_err(ctx, B2F_ERR_ARG, "permutation: chunk_len %u not in [1, 8]", chunk_len);
-  if (k < 10 || k > 30) return set_err(ctx, B2F_ERR_ARG, "permutation: k %u not in [10, 30]", k);
-  if (((uintptr_t)d_z & 15) || ((uintptr_t)d_sigma & 15))
-    return set_err(ctx, B2F_ERR_ARG, "permutation: outputs must be 16-byte aligned");
+}  // extern "C"
+
+namespace {
+// The host part shared by the permutation calls: field checks, the instance row map, the mapping
+// patterns (built once per rounds, pooled on the device), the instance table (pinned staging,
+// async upload) and the scratch (need_scr bytes). *row0 / *used: the circuit's first trace row
+// and its rows. Whatever the caller launches next is stream-ordered after the table upload.
+int perm_setup(b2f_ctx* ctx, const char* what, const uint64_t* h_offsets, size_t n, uint32_t k,
+               uint32_t form, const uint64_t* const* elems, int n_elems, size_t need_scr,
+               hipStream_t s, uint64_t* row0, uint64_t* used) {
+  if (form > B2F_FP_BN254_MONTGOMERY) return set_err(ctx, B2F_ERR_ARG, "%s: unknown form %u", what, form);
+  if (k < 10 || k > 30) return set_err(ctx, B2F_ERR_ARG, "%s: k %u not in [10, 30]", what, k);
   static const uint64_t moduli[2][4] = {
       {0x992d30ed00000001ull, 0x224698fc094cf91bull, 0, 0x4000000000000000ull},
       {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull, 0x30644e72e131a029ull}};
@@ -1508,33 +1512,25 @@ B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, 
       if (v[i] != p[i]) return v[i] < p[i];
     return false;
   };
-  if (!canon(omega) || !canon(delta) || !canon(beta) || !canon(gamma))
-    return set_err(ctx, B2F_ERR_ARG, "permutation: omega/delta/beta/gamma not canonical field elements");
-  const uint64_t n_rows = 1ull << k;
-  const uint64_t row0 = h_offsets[0];
+  for (int i = 0; i < n_elems; i++)
+    if (!canon(elems[i])) return set_err(ctx, B2F_ERR_ARG, "%s: omega/delta/beta/gamma not canonical field elements", what);
+  *row0 = h_offsets[0];
   std::vector<uint32_t> need;
   for (size_t i = 0; i < n; i++) {
     const uint64_t R = h_offsets[i + 1] - h_offsets[i];
     if (h_offsets[i + 1] < h_offsets[i] || R < FIXED_ROWS || (R - FIXED_ROWS) % ROUND_ROWS ||
         (R - FIXED_ROWS) / ROUND_ROWS > B2F_MAX_ROUNDS)
-      return set_err(ctx, B2F_ERR_LAYOUT, "permutation: offsets[%zu..%zu] is not an instance", i, i + 1);
+      return set_err(ctx, B2F_ERR_LAYOUT, "%s: offsets[%zu..%zu] is not an instance", what, i, i + 1);
     need.push_back((uint32_t)((R - FIXED_ROWS) / ROUND_ROWS));
   }
-  const uint64_t used = h_offsets[n] - row0;
-  if (h_offsets[n] > total_rows) return set_err(ctx, B2F_ERR_ROWS, "permutation: instances past total_rows");
-  if (used > usable_rows || usable_rows >= n_rows)
-    return set_err(ctx, B2F_ERR_ROWS, "permutation: need used rows %llu <= usable_rows %llu < 2^k",
-                   (unsigned long long)used, (unsigned long long)usable_rows);
-  if (out_rows < usable_rows + 1 || (d_sigma && out_rows < n_rows))
-    return set_err(ctx, B2F_ERR_ROWS, "permutation: out_rows too small");
-  hipStream_t s = (hipStream_t)stream;
+  *used = h_offsets[n] - *row0;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   // mapping patterns: build the missing ones, rebuild the device pool if it lacks any
   bool rebuild = false;
   for (uint32_t r : need) {
     if (!ctx->pm_pat.count(r)) {
       std::vector<uint32_t> m;
-      if (!perm_mapping(r, m)) return set_err(ctx, B2F_ERR_ROUNDS, "permutation: rounds %u", r);
+      if (!perm_mapping(r, m)) return set_err(ctx, B2F_ERR_ROUNDS, "%s: rounds %u", what, r);
       ctx->pm_pat[r] = std::move(m);
     }
     if (!ctx->pm_pool_off.count(r)) rebuild = true;
@@ -1569,9 +1565,8 @@ B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, 
   }
   if (!ctx->pm_inst_ev) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->pm_inst_ev, hipEventDisableTiming));
   uint64_t* it = ctx->h_pm_inst;
-  for (size_t i = 0; i <= n; i++) it[i] = h_offsets[i] - row0;
+  for (size_t i = 0; i <= n; i++) it[i] = h_offsets[i] - *row0;
   for (size_t i = 0; i < n; i++) it[n + 1 + i] = ctx->pm_pool_off[need[i]];
-  const size_t need_scr = perm_scratch_bytes(k, usable_rows, n, chunk_len);
   if (m > ctx->pm_inst_cap || need_scr > ctx->pm_cap) {
     HIPCHK(ctx, hipStreamSynchronize(s));
     if (m > ctx->pm_inst_cap) {
@@ -1593,12 +1588,72 @@ B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, 
   HIPCHK(ctx, hipMemcpyAsync(ctx->d_pm_inst, it, 8 * m, hipMemcpyHostToDevice, s));
   HIPCHK(ctx, hipEventRecord(ctx->pm_inst_ev, s));
   ctx->pm_inst_ev_live = true;
+  return B2F_OK;
+}
+}  // namespace
+
+extern "C" {
+
+B2F_API int b2f_permutation_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t total_rows,
+                                        const uint64_t* h_offsets, size_t n, uint32_t k,
+                                        uint64_t usable_rows, const uint64_t omega[4],
+                                        const uint64_t delta[4], const uint64_t beta[4],
+                                        const uint64_t gamma[4], uint32_t chunk_len, uint32_t form,
+                                        uint64_t* d_sigma, uint64_t* d_z, uint64_t out_rows,
+                                        void* stream) {
+  if (!ctx) return B2F_ERR_ARG;
+  if (!d_advice || !h_offsets || !omega || !delta || !beta || !gamma || !d_z || n == 0)
+    return set_err(ctx, B2F_ERR_ARG, "permutation: null buffer or no instances");
+  if (chunk_len < 1 || chunk_len > PM_COLS)
+    return set_err(ctx, B2F_ERR_ARG, "permutation: chunk_len %u not in [1, 8]", chunk_len);
+  if (k < 10 || k > 30) return set_err(ctx, B2F_ERR_ARG, "permutation: k %u not in [10, 30]", k);
+  if (((uintptr_t)d_z & 15) || ((uintptr_t)d_sigma & 15))
+    return set_err(ctx, B2F_ERR_ARG, "permutation: outputs must be 16-byte aligned");
+  const uint64_t n_rows = 1ull << k;
+  if (h_offsets[n] > total_rows) return set_err(ctx, B2F_ERR_ROWS, "permutation: instances past total_rows");
+  if (h_offsets[n] - h_offsets[0] > usable_rows || usable_rows >= n_rows)
+    return set_err(ctx, B2F_ERR_ROWS, "permutation: need used rows %llu <= usable_rows %llu < 2^k",
+                   (unsigned long long)(h_offsets[n] - h_offsets[0]), (unsigned long long)usable_rows);
+  if (out_rows < usable_rows + 1 || (d_sigma && out_rows < n_rows))
+    return set_err(ctx, B2F_ERR_ROWS, "permutation: out_rows too small");
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t* elems[4] = {omega, delta, beta, gamma};
+  uint64_t row0 = 0, used = 0;
+  if (int rc = perm_setup(ctx, "permutation", h_offsets, n, k, form, elems, 4,
+                          perm_scratch_bytes(k, usable_rows, n, chunk_len), s, &row0, &used))
+    return rc;
   if (int rc = ensure_side(ctx)) return rc;
   int tk = timed_begin(ctx, B2F_KERNEL_PERM, s);
   HIPCHK(ctx, launch_permutation(d_advice, total_rows, row0, ctx->d_pm_inst, n, ctx->d_pm_pool, k,
                                  usable_rows, omega, delta, beta, gamma, chunk_len, form, d_sigma,
                                  d_z, out_rows, ctx->d_pm, ctx->d_status + 2, ctx->s2, ctx->ev_fork,
                                  ctx->ev_join, s));
+  timed_end(ctx, tk, s);
+  return B2F_OK;
+}
+
+B2F_API int b2f_permutation_sigma_dev(b2f_ctx* ctx, const uint64_t* h_offsets, size_t n, uint32_t k,
+                                      const uint64_t omega[4], const uint64_t delta[4], uint32_t form,
+                                      uint64_t* d_sigma, uint64_t out_rows, void* stream) {
+  if (!ctx) return B2F_ERR_ARG;
+  if (!h_offsets || !omega || !delta || !d_sigma || n == 0)
+    return set_err(ctx, B2F_ERR_ARG, "permutation sigma: null buffer or no instances");
+  if ((uintptr_t)d_sigma & 15) return set_err(ctx, B2F_ERR_ARG, "permutation sigma: d_sigma must be 16-byte aligned");
+  if (k < 10 || k > 30) return set_err(ctx, B2F_ERR_ARG, "permutation sigma: k %u not in [10, 30]", k);
+  const uint64_t n_rows = 1ull << k;
+  if (h_offsets[n] - h_offsets[0] >= n_rows)
+    return set_err(ctx, B2F_ERR_ROWS, "permutation sigma: the instances need %llu rows >= 2^k",
+                   (unsigned long long)(h_offsets[n] - h_offsets[0]));
+  if (out_rows < n_rows) return set_err(ctx, B2F_ERR_ROWS, "permutation sigma: out_rows < 2^k");
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t* elems[2] = {omega, delta};
+  uint64_t row0 = 0, used = 0;
+  if (int rc = perm_setup(ctx, "permutation sigma", h_offsets, n, k, form, elems, 2, perm_sigma_scratch_bytes(k),
+                          s, &row0, &used))
+    return rc;
+  int tk = timed_begin(ctx, B2F_KERNEL_PERM_SIGMA, s);
+  HIPCHK(ctx, launch_permutation_sigma(ctx->d_pm_inst, n, ctx->d_pm_pool, k, omega, delta, form, d_sigma,
+                                       out_rows, ctx->d_pm, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
@@ -1647,7 +1702,8 @@ B2F_API int b2f_sync(b2f_ctx* ctx, void* stream) {
   if (bits & (1 << B2F_ERR_FIELD))
     return set_err(ctx, B2F_ERR_FIELD, "a grand product's denominator is zero (challenge collision)");
   if (bits & (1 << B2F_ERR_CHECK))
-    return set_err(ctx, B2F_ERR_CHECK, "lookup: the permuted columns' den product differs from the input side's");
+    return set_err(ctx, B2F_ERR_CHECK, "internal cross-check failed (lookup den product vs input side, or "
+                                       "the fused pass's segment list overflowed)");
   return B2F_OK;
 }
 

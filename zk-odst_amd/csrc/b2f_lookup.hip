@@ -476,7 +476,7 @@ __global__ __launch_bounds__(NS_T) void lk_nscan_kernel(uint64_t nb, const Fe* _
     Dnum[c] = D;
     __builtin_amdgcn_s_setprio(3);
     if (sticky && field::is_zero(D)) atomicOr(sticky, 1 << B2F_ERR_FIELD);
-    sdinv = field::inv_kaliski<F>(D);
+    sdinv = field::inv_safegcd<F>(D);
     __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();

@@ -25,6 +25,10 @@
 namespace b2f {
 
 size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst, uint32_t chunk_len);
+size_t perm_sigma_scratch_bytes(uint32_t k);
+hipError_t launch_permutation_sigma(const uint64_t* d_inst, size_t n_inst, const uint32_t* d_pool, uint32_t k,
+                                    const uint64_t* omega, const uint64_t* delta, uint32_t form,
+                                    uint64_t* d_sigma, uint64_t out_rows, void* scratch, hipStream_t s);
 hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0,
                               const uint64_t* d_inst, size_t n_inst, const uint32_t* d_pool,
                               uint32_t k, uint64_t usable_rows, const uint64_t* omega,
@@ -378,7 +382,42 @@ hipError_t run_perm(const uint32_t* d_advice, uint64_t total_rows, uint64_t row0
   return hipGetLastError();
 }
 
+// keygen: the sigma columns alone (the tables they read, then pm_sigma_kernel)
+template <class F>
+hipError_t run_perm_sigma(const Inst& I, const uint32_t* d_pool, uint32_t k, const Params& prm, bool mont,
+                          uint64_t* d_sigma, uint64_t out_rows, void* scratch, hipStream_t s) {
+  Carve m = carve(scratch, k, 0, 1);
+  const uint64_t n_rows = 1ull << k, n_hi = n_rows / LO;
+  const uint64_t tab = n_hi > (uint64_t)NCOL * LO ? n_hi : (uint64_t)NCOL * LO;
+  hipLaunchKernelGGL(pm_table_kernel<F>, dim3((uint32_t)((tab + 255) / 256)), dim3(256), 0, s, prm,
+                     n_hi, m.OL, m.BL, m.OH, m.gm);
+  hipLaunchKernelGGL(pm_sigma_kernel<F>, dim3((uint32_t)((n_rows + 255) / 256)), dim3(256), 0, s, I,
+                     d_pool, n_rows, m.OL, m.OH, mont, d_sigma, out_rows);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+size_t perm_sigma_scratch_bytes(uint32_t k) { return carve(nullptr, k, 0, 1).total; }
+
+hipError_t launch_permutation_sigma(const uint64_t* d_inst, size_t n_inst, const uint32_t* d_pool, uint32_t k,
+                                    const uint64_t* omega, const uint64_t* delta, uint32_t form,
+                                    uint64_t* d_sigma, uint64_t out_rows, void* scratch, hipStream_t s) {
+  Params prm;
+  for (int i = 0; i < 4; i++) {
+    prm.omega[i] = omega[i];
+    prm.delta[i] = delta[i];
+    prm.beta[i] = i == 0;  // BL (beta times the coset table) is not used by the sigma pass
+    prm.gamma[i] = 0;
+  }
+  Inst I;
+  I.start = d_inst;
+  I.pat = d_inst + n_inst + 1;
+  I.n = (uint32_t)n_inst;
+  const bool mont = (form & 1u) != 0;
+  if (form >> 1) return run_perm_sigma<field::Bn254>(I, d_pool, k, prm, mont, d_sigma, out_rows, scratch, s);
+  return run_perm_sigma<field::Pallas>(I, d_pool, k, prm, mont, d_sigma, out_rows, scratch, s);
+}
 
 size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t, uint32_t chunk_len) {
   return carve(nullptr, k, usable_rows, (NCOL + chunk_len - 1) / chunk_len).total;
