@@ -478,16 +478,27 @@ def main():
     kern = kernel_table(ktimes)
     big = [k for k in kern if k != "record"]
     dom = max(big, key=lambda k: kern[k]["avg_ms"])
-    traffic = None
+    # PMC traffic: only a record collected from these very kernel sources
+    # counts -- the record carries the source stamp it was measured under (tools/pmc_traffic.py)
+    traffic, traffic_src = None, None
     try:
         with open(args.traffic) as fh:
             tr = json.load(fh)
         key = "%s_%d_%s" % (dom, n, "mix" if mix else args.rounds)
-        traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+        rec = tr.get(key, {})
+        stamp = b2f._lib.source_stamp()
+        if rec.get("source_stamp") == stamp:
+            traffic = rec.get("hbm_bytes_per_launch")
+            traffic_src = {"file": os.path.relpath(args.traffic, ROOT), "key": key,
+                           "source_stamp": stamp, "kernels": rec.get("kernels")}
+        else:
+            traffic_src = {"file": os.path.relpath(args.traffic, ROOT), "key": key,
+                           "stale": "recorded under sources %s, running %s" % (rec.get("source_stamp"), stamp)}
     except (OSError, ValueError):
         pass
     roof = {"bound": "hbm", "achieved": kern[dom]["achieved_GBs"], "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": kern[dom]["frac"], "traffic": traffic, "kernel": dom}
+            "unit": "GB/s", "frac": kern[dom]["frac"], "traffic": traffic, "kernel": dom,
+            "traffic_record": traffic_src}
 
     def headline():
         """The contract's fields of the JSON line, complete once the headline loop is done."""
@@ -541,8 +552,8 @@ def main():
     if world == 1 and args.floor_reps > 0:
         try:
             deng = b2f.Engine(local, diag=True)
-            samples = {"fill_floor": [], "fill_eval": [], "fill": [], "eval_floor": [],
-                       "eval": []}
+            samples = {"fill_floor": [], "stream_floor": [], "fill_eval": [], "fill": [],
+                       "eval_floor": [], "eval": []}
 
             def one(e, fn, kname, var=None, val=None):
                 if var:
@@ -558,6 +569,7 @@ def main():
 
             for _ in range(args.floor_reps):
                 samples["fill_floor"].append(one(deng, batch.fill, "fill", "B2F_DIAG_FILL", "2"))
+                samples["stream_floor"].append(one(deng, batch.fill, "fill", "B2F_DIAG_FILL", "4"))
                 samples["fill_eval"].append(one(eng, batch.fill_evaluate, "fill_eval"))
                 samples["fill"].append(one(eng, batch.fill, "fill"))
                 samples["eval_floor"].append(one(deng, batch.evaluate, "eval", "B2F_DIAG_EVAL", "1"))
@@ -578,6 +590,9 @@ def main():
                       "eval_over_floor": round(med["eval"] / med["eval_floor"], 4),
                       "fill_eval_over_fill_floor": round(med["fill_eval"] / med["fill_floor"], 4),
                       "fill_eval_over_fill_floor_min": round(mn["fill_eval"] / mn["fill_floor"], 4),
+                      "stream_floor_ms": round(med["stream_floor"], 4),
+                      "fill_eval_over_stream_floor": round(med["fill_eval"] / med["stream_floor"], 4),
+                      "fill_eval_over_fill_min": round(mn["fill_eval"] / mn["fill"], 4),
                       "note": "ratios of medians (and of minima) over interleaved reps"}
         except (OSError, b2f.B2FError) as e:
             floors = {"error": repr(e)}

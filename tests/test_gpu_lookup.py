@@ -162,8 +162,10 @@ def test_spread_table_columns(engine, form):
 def test_lookup_zero_factor_reported_then_clean(engine, trace, form, which):
     """beta = -A[row] makes (A + beta) and (A' + beta) zero for that row's value, and
     gamma = -T[x] makes (S + gamma) and (S' + gamma) zero for table row x, so the den total is
-    zero: the call reports B2F_ERR_FIELD at b2f_sync (D from the histogram, inversion on the side
-    stream), and the next call with sound challenges syncs clean and closes to one."""
+    zero: the call reports B2F_ERR_FIELD at b2f_sync (D = the num side's product, lk_nscan_kernel
+    on the side stream), and the next call with sound challenges syncs clean -- with no
+    B2F_ERR_CHECK, i.e. the permuted columns' den product equals the num side's D -- and its z
+    ends at one (N / D by construction; the sync is the check that matters)."""
     import lookup as lk
     import torch
 
@@ -197,9 +199,10 @@ def test_lookup_zero_factor_reported_then_clean(engine, trace, form, which):
 
 
 def test_lookup_group_of_circuits_equal_oracle(engine, trace):
-    """Five circuits in one call, one group: each circuit's D^-1 comes from its histogram on the
-    side stream (lk_dpart_kernel) while the permute pass runs, and one grand product covers the
-    group. Every circuit's five columns equal the restatement, BN254 Montgomery form."""
+    """Five circuits in one call, one group: each circuit's num block products, their prefix and
+    D^-1 come from the trace on the side stream (lk_npart_kernel, lk_nscan_kernel) while the count
+    and rank-scan passes run, and one z pass (lk_zpass_kernel, a den-side look-back per circuit)
+    covers the group. Every circuit's five columns equal the restatement, BN254 Montgomery form."""
     import lookup as lk
     import torch
 
@@ -224,11 +227,13 @@ def test_lookup_group_of_circuits_equal_oracle(engine, trace):
 
 
 def test_lookup_two_groups_equal_within_call(engine, trace):
-    """More circuits than one group holds (1 GiB of scratch per group: 15 circuits of 2^20 rows),
-    so the call loops over two groups, each forking its own D^-1 chain to the side stream after
-    its count pass and reusing the count / D scratch of the group before. Circuit 16 (group 2)
-    repeats circuit 5's rows (group 1): all five columns bit-identical, and every z closes to one
-    (Montgomery form). A group that read the previous group's counts or D^-1 would differ."""
+    """More circuits than one group holds (at most 2^24 rows per group: 16 circuits of 2^20
+    rows), so the call loops over two groups, each forking its own num-side chain (block
+    products, prefix, D^-1) to the side stream at its start and reusing the count / NK /
+    look-back scratch of the group before (the S part of the block products is computed once, by
+    the first group). Circuit 16 (group 2) repeats circuit 5's rows (group 1): all five columns
+    bit-identical, the sync clean (no B2F_ERR_CHECK) and every z ends at one (Montgomery form). A
+    group that read the previous group's counts, NK or look-back state would differ."""
     import torch
 
     form = 1

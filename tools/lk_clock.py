@@ -38,7 +38,7 @@ def main():
                                           rb.data_ptr(), nc, usable, th, be, ga, 1,
                                           out.data_ptr(), usable + 1, bad.data_ptr(), s)
     clk = ctypes.CDLL(lib).b2f_debug_lk_clock
-    buf = (ctypes.c_uint64 * 16)()
+    buf = (ctypes.c_uint64 * 24)()
     call()
     eng.sync(s)
     clk(buf)
@@ -50,6 +50,11 @@ def main():
     clk(buf)
     tot = {PHASES[i]: round(buf[i] / reps / 1e6, 3) for i in PHASES}
     tot["max resident workgroups"] = buf[12]
+    tot["polls per call"] = buf[15] / reps
+    tot["blocks combined per call"] = buf[7] / reps
+    tot["polls: block b+1 unpublished"] = buf[16] / reps
+    tot["polls: a farther block unpublished"] = buf[17] / reps
+    tot["reads: status before pieces"] = buf[18] / reps
     tot["span of the calls, 1e6 ticks"] = round((buf[14] - buf[13]) / 1e6, 3)
     print(json.dumps({"lib": lib, "unit": "1e6 s_memtime ticks per call, summed over waves", **tot}))
 

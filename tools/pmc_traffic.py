@@ -16,6 +16,9 @@ import os
 import sys
 
 
+names_of = collections.defaultdict(set)  # kind -> the kernel names aggregated into it
+
+
 def per_kernel(d, counter):
     vals = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -35,6 +38,7 @@ def per_kernel(d, counter):
                 continue
             per_dispatch[r["Dispatch_Id"]] += float(r["Counter_Value"])
             names[r["Dispatch_Id"]] = kind
+            names_of[kind].add(k.split("(")[0])
         for disp, v in per_dispatch.items():
             vals[names[disp]].append(v)
     return {k: sum(v) / len(v) for k, v in vals.items() if v}
@@ -46,11 +50,17 @@ def main():
     fetch = per_kernel(fetch_dir, "FETCH_SIZE")
     write = per_kernel(write_dir, "WRITE_SIZE")
     # the fused path is two launches per step (half-round tiles, then init/final/zero tiles)
+    for kk in ("fill_eval_edge", "eval_part"):
+        names_of[{"fill_eval_edge": "fill_eval", "eval_part": "eval"}[kk]] |= names_of.pop(kk, set())
     for d in (fetch, write):
         if "fill_eval_edge" in d:
             d["fill_eval"] = d.get("fill_eval", 0.0) + d.pop("fill_eval_edge")
         if "eval_part" in d:  # per launch; two launches (half-round, edge) per eval call
             d["eval"] = d.get("eval", 0.0) + 2 * d.pop("eval_part")
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "zk-odst_amd"))
+    from b2f import _lib
+
+    stamp = _lib.source_stamp()
     res = json.load(open(out)) if os.path.exists(out) else {}
     for kind in ("fill", "eval", "fill_eval"):
         if kind not in fetch or kind not in write:
@@ -60,7 +70,8 @@ def main():
         res["%s_%s" % (kind, suffix)] = {
             "fetch_size_kib_raw": fetch[kind], "write_size_kib": write[kind],
             "fetch_bytes_corrected": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
-            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB x1024"}
+            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB x1024",
+            "kernels": sorted(names_of[kind]), "source_stamp": stamp}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))

@@ -35,6 +35,23 @@ STATUS_NAMES = {OK: "OK", ERR_ARG: "B2F_ERR_ARG", ERR_ROUNDS: "B2F_ERR_ROUNDS",
                 ERR_CHECK: "B2F_ERR_CHECK"}
 
 
+def source_stamp():
+    """A 16-hex-digit hash of the sources libb2f.so is built from (zk-odst_amd/csrc/*, the
+    Makefile, include/b2f.h): measurement records (PMC traffic) carry it, so bench.py can tell
+    whether a record describes the kernels it is running. Reads files only; the GPU box has no
+    .git, so a commit id would not do."""
+    import glob
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(PKG_ROOT, "csrc", "*"))) + [os.path.join(PKG_ROOT, "Makefile"),
+                                                                       HEADER]
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(os.path.basename(f).encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
 class B2FError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__("%s: %s" % (STATUS_NAMES.get(code, code), msg))

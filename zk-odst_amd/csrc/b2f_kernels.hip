@@ -336,6 +336,25 @@ __global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_i
   }
 }
 
+// Diagnostics (B2F_DIAG_FILL=4 in the diagnostics library): a second store floor for the fill,
+// a plain non-temporal 16-byte stream of zeros over the same 11 columns in address order (each
+// column front to back, grid-stride, nothing else per chunk): what the box's write path does
+// for these 60 GB with no tile structure at all.
+#ifdef B2F_DIAG
+__global__ void __launch_bounds__(BLOCK) store_stream_kernel(uint32_t* __restrict__ adv,
+                                                            uint32_t* __restrict__ fixed,
+                                                            uint64_t total_rows) {
+  const uint64_t per_col = total_rows >> 2, chunks = 11 * per_col;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+  for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < chunks; j += stride) {
+    const uint64_t c = j / per_col, q = j - c * per_col;
+    u32x4* dst = reinterpret_cast<u32x4*>((c < 10 ? adv + c * total_rows : fixed) + 4 * q);
+    __builtin_nontemporal_store(z, dst);
+  }
+}
+#endif
+
 // --------------------------------------------------------------------------- eval kernel
 //
 // Software-pipelined over 1024-row tiles dealt round-robin to persistent workgroups (3 per
@@ -1215,6 +1234,15 @@ B2F_API int b2f_fill_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const ui
   if (rc) return rc;
   uint32_t wgs = grid_for(ctx, nt, diag_mode("B2F_FILL_WGS", 8));
   int tk = timed_begin(ctx, B2F_KERNEL_FILL, s);
+#ifdef B2F_DIAG
+  if (diag_mode("B2F_DIAG_FILL", FILL_FULL) == 4) {
+    hipLaunchKernelGGL(store_stream_kernel, dim3(ctx->cu_count * 8), dim3(BLOCK), 0, s, d_advice, d_fixed,
+                       total_rows);
+    HIPCHK(ctx, hipGetLastError());
+    timed_end(ctx, tk, s);
+    return B2F_OK;
+  }
+#endif
   switch (diag_mode("B2F_DIAG_FILL", FILL_FULL)) {
 #define B2F_FILL(M)                                                                            \
   case M:                                                                                      \

@@ -338,6 +338,13 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
 // gp_chunk + gp_write moved 384 B per row; this pass 164).
 // Check: block 0's inclusive den product is D_den = prod den_i from the permuted
 // columns, which must equal the num-side D; a difference (wrong A' or S') sets B2F_ERR_CHECK.
+// LKMUL: the z pass's field products; a diagnostics build (-DB2F_LK_NOPROD, wrong results)
+// replaces them by additions to time the pass without its products
+#ifdef B2F_LK_NOPROD
+#define LKMUL(x, y) field::add<F>(x, y)
+#else
+#define LKMUL(x, y) field::mul<F>(x, y)
+#endif
 #ifndef B2F_ZP_WAVES
 #define B2F_ZP_WAVES 4  // lk_zpass_kernel waves per SIMD (ZR = 2: 128 VGPRs)
 #endif
@@ -354,7 +361,7 @@ __host__ __device__ inline uint64_t n_lb(uint64_t usable) { return (usable + LB 
 // lk_zpass_kernel summed over waves, read by b2f_debug_lk_clock (tools/lk_clock.py).
 #ifdef B2F_LK_CLOCK
 // [11] resident workgroups now, [12] their maximum, [13] / [14] first start / last end tick
-__device__ unsigned long long g_lk_clock[16];
+__device__ unsigned long long g_lk_clock[24];
 #define LKCLK_DECL                                                           \
   uint64_t lk_t = __builtin_amdgcn_s_memtime();                             \
   if (threadIdx.x == 0) {                                                   \
@@ -520,11 +527,25 @@ __device__ __forceinline__ Fe lb_join(const uint64_t (&w)[6]) {
   v.w[6] = (uint32_t)L3; v.w[7] = (uint32_t)(L3 >> 32);
   return v;
 }
-__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
+#ifndef B2F_LB_MODE
+#define B2F_LB_MODE 0  // look-back state access (A/B): 0 agent-scope atomic load / store, 1 stores
+                       // as atomic exchanges, 2 loads as memory-side atomic adds of a runtime 0,
+                       // 3 an agent-scope acquire fence before every poll
+#endif
+__device__ __forceinline__ uint64_t lb_load(const uint64_t* p, uint64_t zero) {
+#if B2F_LB_MODE == 2
+  return __hip_atomic_fetch_add(const_cast<uint64_t*>(p), zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  (void)zero;
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 __device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
+#if B2F_LB_MODE == 1
+  (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 // lanes 0..5 of the calling wave publish v (the same in every lane) as the aggregate (kind 1) or
 // the inclusive value (kind 2) of block state st, then lane 0 its status
@@ -533,13 +554,13 @@ __device__ __forceinline__ void lb_publish(uint64_t* st, uint32_t lane, const Fe
   if (lane == 0) lb_store(st + 15, kind);
 }
 // the value of kind `kind` of block state st; false while a piece is not yet visible
-__device__ __forceinline__ bool lb_read(const uint64_t* st, uint32_t kind, Fe& v) {
+__device__ __forceinline__ bool lb_read(const uint64_t* st, uint32_t kind, Fe& v, uint64_t zero) {
   uint64_t w[6];
   const uint64_t tag = kind == 2 ? LB_TAG_INC : LB_TAG_AGG;
   bool ok = true;
 #pragma unroll
   for (int i = 0; i < 6; i++) {
-    w[i] = lb_load(st + (kind == 2 ? 8 : 0) + i);
+    w[i] = lb_load(st + (kind == 2 ? 8 : 0) + i, zero);
     ok &= (w[i] & ~LB_M48) == tag;
   }
   v = lb_join(w);
@@ -632,7 +653,7 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     const Fe* __restrict__ Ts, uint64_t* __restrict__ out, uint64_t out_rows, Chal ch,
     const uint32_t* __restrict__ pos, const uint32_t* __restrict__ dcnt, const uint32_t* __restrict__ lp,
     const uint32_t* __restrict__ samp, const Fe* __restrict__ NK, const Fe* __restrict__ Dnum,
-    uint64_t* __restrict__ lbs, uint32_t* __restrict__ ticket, int* __restrict__ sticky) {
+    uint64_t* __restrict__ lbs, uint32_t* __restrict__ ticket, int* __restrict__ sticky, uint64_t lb_zero) {
   // the search samples, then (after every wave has searched) the lane totals
   static_assert(ZT == 256, "the scans take 4 lane totals per lane");
   constexpr int SMEM = 2 * SAMPLE * 4 > 2 * ZT * 32 ? 2 * SAMPLE * 4 : 2 * ZT * 32;
@@ -704,15 +725,17 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
   for (int j = 0; j < ZR; j++) v[j] = Ts[rs[j]];
 #pragma unroll
   for (int j = 0; j < ZR; j++) {
-    d[j] = p0 + j < us ? field::mul<F>(d[j], field::add<F>(v[j], gamma)) : field::one<F>();
+    d[j] = p0 + j < us ? LKMUL(d[j], field::add<F>(v[j], gamma)) : field::one<F>();
     v[j] = gp::out_form<F>(v[j], MONT);
   }
   wave_store_zr<true>(o + 3 * out_rows * 4, st, lane, v, r0, us);
   Fe sf[ZR];
   sf[ZR - 2] = d[ZR - 1];
 #pragma unroll
-  for (int j = ZR - 3; j >= 0; j--) sf[j] = field::mul<F>(d[j + 1], sf[j + 1]);
-  sD[pz(t)] = field::mul<F>(d[0], sf[0]);  // every wave has searched: the samples are free
+  for (int j = ZR - 3; j >= 0; j--) sf[j] = LKMUL(d[j + 1], sf[j + 1]);
+  const Fe dl = LKMUL(d[0], sf[0]);
+  __syncthreads();  // every wave has searched: the samples' memory takes the lane totals
+  sD[pz(t)] = dl;
   __syncthreads();
   LKCLK(2);
   // the den wave: its in-lane scan (suffix order: entry i of the scan is lane total 255 - i) and
@@ -726,12 +749,12 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     for (uint32_t k2 = 1; k2 < 4; k2++) {
       const Fe e = sD[atd(e0 + k2)];
       sD[atd(e0 + k2)] = Pd;
-      Pd = field::mul<F>(Pd, e);
+      Pd = LKMUL(Pd, e);
     }
 #pragma unroll 1
     for (int off = 1; off < 64; off <<= 1) {
       const Fe y = shfl_fe(Pd, (int)lane - off);
-      const Fe m = field::mul<F>(y, Pd);
+      const Fe m = LKMUL(y, Pd);
       if (lane >= (uint32_t)off) Pd = m;
     }
     Fe X = shfl_fe(Pd, (int)lane - 1);
@@ -755,14 +778,14 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
   for (int j = 0; j < ZR; j++) v[j] = Tx[p0 + j < (uint32_t)TROWS ? p0 + j : 0u];
 #pragma unroll
   for (int j = 0; j < ZR; j++) {
-    a[j] = p0 + j < us ? field::mul<F>(a[j], field::add<F>(v[j], gamma)) : field::one<F>();
+    a[j] = p0 + j < us ? LKMUL(a[j], field::add<F>(v[j], gamma)) : field::one<F>();
     v[j] = gp::out_form<F>(v[j], MONT);
   }
   wave_store_zr<true>(o + out_rows * 4, st, lane, v, r0, us);
 #pragma unroll
-  for (int j = 1; j < ZR; j++) a[j] = field::mul<F>(a[j - 1], a[j]);
+  for (int j = 1; j < ZR; j++) a[j] = LKMUL(a[j - 1], a[j]);
 #pragma unroll
-  for (int j = 0; j < ZR - 1; j++) v[j] = field::mul<F>(a[j], sf[j]);
+  for (int j = 0; j < ZR - 1; j++) v[j] = LKMUL(a[j], sf[j]);
   v[ZR - 1] = a[ZR - 1];
   sN[pz(t)] = a[ZR - 1];
   __syncthreads();
@@ -775,19 +798,19 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     for (uint32_t k2 = 1; k2 < 4; k2++) {
       const Fe e = sN[pz(e0 + k2)];
       sN[pz(e0 + k2)] = Pn;
-      Pn = field::mul<F>(Pn, e);
+      Pn = LKMUL(Pn, e);
     }
 #pragma unroll 1
     for (int off = 1; off < 64; off <<= 1) {
       const Fe y = shfl_fe(Pn, (int)lane - off);
-      const Fe m = field::mul<F>(y, Pn);
+      const Fe m = LKMUL(y, Pn);
       if (lane >= (uint32_t)off) Pn = m;
     }
     Fe Xn = shfl_fe(Pn, (int)lane - 1);
     if (lane == 0) Xn = field::one<F>();
     sN[pz(e0)] = Xn;
 #pragma unroll 1
-    for (uint32_t k2 = 1; k2 < 4; k2++) sN[pz(e0 + k2)] = field::mul<F>(Xn, sN[pz(e0 + k2)]);
+    for (uint32_t k2 = 1; k2 < 4; k2++) sN[pz(e0 + k2)] = LKMUL(Xn, sN[pz(e0 + k2)]);
   } else if (wv == wd) {
     // the den wave: the look-back over the blocks after b. Lane i watches block q0 + i's status
     // word; the blocks up to the first inclusive one (fi) must all have published, then their
@@ -797,32 +820,51 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
       uint64_t q0 = b + 1;
       while (true) {
         const uint64_t qb = q0 + lane;
-        const uint32_t s = qb < nb ? (uint32_t)lb_load(lbs + ((uint64_t)c * nb + qb) * LBS_WORDS + 15) : 2u;
+#if B2F_LB_MODE == 3
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+        const uint32_t s = qb < nb ? (uint32_t)lb_load(lbs + ((uint64_t)c * nb + qb) * LBS_WORDS + 15, lb_zero) : 2u;
         const uint64_t inc = __ballot(s == 2), none = __ballot(s == 0);
         const uint32_t fi = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
         const uint64_t need = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
         LKCLK(10);
+#ifdef B2F_LK_CLOCK
+        {
+          const uint32_t s0 = __shfl((int)s, 0, 64);
+          if (lane == 0) {
+            atomicAdd(&g_lk_clock[15], 1ull);                         // polls
+            if (s0 == 0) atomicAdd(&g_lk_clock[16], 1ull);            // ... with block b + 1 unpublished
+            else if (none & need) atomicAdd(&g_lk_clock[17], 1ull);  // ... with a farther block unpublished
+          }
+        }
+#endif
         if (none & need) {
           __builtin_amdgcn_s_sleep(8);
           continue;
         }
         Fe val = field::one<F>();
         bool ok = true;
-        if (lane <= fi && qb < nb) ok = lb_read(lbs + ((uint64_t)c * nb + qb) * LBS_WORDS, s, val);
+        if (lane <= fi && qb < nb) ok = lb_read(lbs + ((uint64_t)c * nb + qb) * LBS_WORDS, s, val, lb_zero);
         if (__ballot(!ok)) {
+#ifdef B2F_LK_CLOCK
+          if (lane == 0) atomicAdd(&g_lk_clock[18], 1ull);  // status seen before its pieces
+#endif
           __builtin_amdgcn_s_sleep(2);
           continue;
         }
         // the product of lanes 0 .. min(fi, 63) (the others hold 1) into lane 0
 #pragma unroll 1
-        for (uint32_t m = 1; m <= fi && m < 64; m <<= 1) val = field::mul<F>(val, shfl_xor_fe(val, (int)m));
-        after = field::mul<F>(after, shfl_fe(val, 0));
+        for (uint32_t m = 1; m <= fi && m < 64; m <<= 1) val = LKMUL(val, shfl_xor_fe(val, (int)m));
+        after = LKMUL(after, shfl_fe(val, 0));
+#ifdef B2F_LK_CLOCK
+        if (lane == 0) atomicAdd(&g_lk_clock[7], (unsigned long long)fi + 1);  // blocks looked at
+#endif
         if (fi < 64) break;
         q0 += 64;
       }
     }
     LKCLK(9);
-    const Fe incl = field::mul<F>(sDb, after);
+    const Fe incl = LKMUL(sDb, after);
     lb_publish(my, lane, incl, 2);
     if (lane == 0 && b == 0) {
       // the den product of the permuted columns against the num side's D
@@ -835,17 +877,17 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     }
     // the block's factor NK_b Dafter_b (Nbefore_b D^-1 Dafter_b) rides on the den side's
     // exclusive values, so a lane's K is one product: (num prefix) (den suffix)
-    const Fe X = field::mul<F>(sX[lane], field::mul<F>(NK[(uint64_t)c * nb + b], after));
+    const Fe X = LKMUL(sX[lane], LKMUL(NK[(uint64_t)c * nb + b], after));
     sD[atd(e0)] = X;
 #pragma unroll 1
-    for (uint32_t k2 = 1; k2 < 4; k2++) sD[atd(e0 + k2)] = field::mul<F>(X, sD[atd(e0 + k2)]);
+    for (uint32_t k2 = 1; k2 < 4; k2++) sD[atd(e0 + k2)] = LKMUL(X, sD[atd(e0 + k2)]);
   }
   __syncthreads();
   LKCLK(5);
   // 4. z
-  const Fe K = field::mul<F>(sN[pz(t)], sD[pz(t)]);
+  const Fe K = LKMUL(sN[pz(t)], sD[pz(t)]);
 #pragma unroll
-  for (int j = 0; j < ZR; j++) v[j] = gp::out_form<F>(field::mul<F>(K, v[j]), MONT);
+  for (int j = 0; j < ZR; j++) v[j] = gp::out_form<F>(LKMUL(K, v[j]), MONT);
   wave_store_zr<true>(o + 4 * out_rows * 4 + 4, st, lane, v, r0, us);
   LKCLK(6);
   LKCLK_END
@@ -962,7 +1004,7 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
     uint32_t* ticket = reinterpret_cast<uint32_t*>(k.lbs + LBS_WORDS * nb * g);
     hipLaunchKernelGGL((mont ? lk_zpass_kernel<F, true> : lk_zpass_kernel<F, false>), dim3((uint32_t)(nb * g)),
                        dim3(ZT), 0, s, d_advice, total_rows, d_row_begin, c0, g, usable_rows, nb, k.Tx, k.Ts,
-                       d_out, out_rows, ch, k.pos, k.dcnt, k.lp, k.samp, k.NK, k.Dnum, k.lbs, ticket, sticky);
+                       d_out, out_rows, ch, k.pos, k.dcnt, k.lp, k.samp, k.NK, k.Dnum, k.lbs, ticket, sticky, 0ull);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;
@@ -973,7 +1015,7 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
 #ifdef B2F_LK_CLOCK
 extern "C" __attribute__((visibility("default"))) int b2f_debug_lk_clock(uint64_t* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lk_clock), sizeof(g_lk_clock)) != hipSuccess) return B2F_ERR_HIP;
-  unsigned long long zero[16] = {};
+  unsigned long long zero[24] = {};
   zero[13] = ~0ull;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_lk_clock), zero, sizeof(zero)) == hipSuccess ? B2F_OK : B2F_ERR_HIP;
 }
