@@ -160,11 +160,11 @@ __global__ void check(uint32_t* bad, int n) {
       b.w[0] = threadIdx.x & 1u;
       if (threadIdx.x & 2u) b = a;
     }
-    const Fe x = mul<F>(a, b), y = mul_cios<F>(a, b), z = mul2<F>(a, b);
+    const Fe x = mul_comba<F>(a, b), y = mul_cios<F>(a, b), z = mul2<F>(a, b), q = mul_asm<F>(a, b);
     Fe u, v;
     mul_x2<F>(a, b, b, a, u, v);
     uint32_t d = 0;
-    for (int i = 0; i < 8; i++) d |= (x.w[i] ^ y.w[i]) | (z.w[i] ^ y.w[i]) | (u.w[i] ^ y.w[i]) | (v.w[i] ^ y.w[i]);
+    for (int i = 0; i < 8; i++) d |= (x.w[i] ^ y.w[i]) | (z.w[i] ^ y.w[i]) | (u.w[i] ^ y.w[i]) | (v.w[i] ^ y.w[i]) | (q.w[i] ^ y.w[i]);
     if (d) atomicAdd(bad, 1u);
   }
 }
@@ -181,7 +181,8 @@ __global__ __launch_bounds__(256) void k(const Fe* in, Fe* out, int n) {
       for (int c = 0; c + 1 < CH; c += 2) mul_x2<F>(acc[c], b, acc[c + 1], b, acc[c], acc[c + 1]);
     } else {
 #pragma unroll
-      for (int c = 0; c < CH; c++) acc[c] = V == 0 ? mul<F>(acc[c], b) : V == 1 ? mul_cios<F>(acc[c], b) : mul2<F>(acc[c], b);
+      for (int c = 0; c < CH; c++)
+        acc[c] = V == 0 ? mul_comba<F>(acc[c], b) : V == 1 ? mul_cios<F>(acc[c], b) : V == 4 ? mul_asm<F>(acc[c], b) : mul2<F>(acc[c], b);
     }
   }
   Fe s = acc[0];
@@ -244,6 +245,10 @@ int main() {
   RUNL(Bn254, 0, 1, 48) RUNL(Bn254, 0, 2, 48) RUNL(Bn254, 0, 1, 64) RUNL(Bn254, 0, 2, 64)
   // variant 3: the two chains of a lane through mul_x2 (interleaved in each asm block)
   RUN(Pallas, 3, 2) RUN(Bn254, 3, 2)
+  // variant 4: mul_asm (b2f_mont_asm.h, one asm block per product)
+  RUN(Pallas, 4, 1) RUN(Pallas, 4, 2) RUN(Bn254, 4, 1) RUN(Bn254, 4, 2)
+  RUNL(Pallas, 4, 1, 48) RUNL(Pallas, 4, 1, 64) RUNL(Bn254, 4, 1, 48)
+  RUN(Pallas, 0, 1) RUN(Bn254, 0, 1)
   RUNL(Pallas, 3, 2, 48) RUNL(Pallas, 3, 2, 64) RUNL(Bn254, 3, 2, 48) RUNL(Bn254, 3, 2, 64)
   {
     uint32_t* bad;
@@ -253,7 +258,7 @@ int main() {
     hipLaunchKernelGGL(check<Bn254>, dim3(1024), dim3(256), 0, 0, bad + 1, 16);
     uint32_t h[2];
     hipMemcpy(h, bad, 8, hipMemcpyDeviceToHost);
-    printf("mul / mul2 / mul_x2 (product scanning) vs mul_cios mismatches over 4.2M products: pallas %u bn254 %u\n", h[0], h[1]);
+    printf("mul / mul2 / mul_x2 / mul_asm (product scanning) vs mul_cios mismatches over 4.2M products: pallas %u bn254 %u\n", h[0], h[1]);
   }
   {
     float ms = timeit([&] { hipLaunchKernelGGL(madk, dim3(blocks), dim3(256), 0, 0, (uint64_t*)out, 1024); });

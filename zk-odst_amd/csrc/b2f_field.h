@@ -90,6 +90,8 @@ __device__ __forceinline__ Fe reduce_once(const Fe& t) {
   return borrow ? t : d;
 }
 
+#include "b2f_mont_asm.h"
+
 // Montgomery product a b / 2^256 mod p (a, b < p), product scanning (Comba): column k of the
 // 512-bit sum of a_i b_j and m_i p_j (i + j = k; m_k chosen so column k < 8 ends in a zero word)
 // accumulates in a 64-bit VGPR pair by v_mad_u64_u32, whose carry out of the 64-bit add goes
@@ -127,7 +129,7 @@ __device__ __forceinline__ void acc_madd2(uint64_t& acc, uint32_t& ov, uint32_t 
       : "vcc");
 }
 template <class F>
-__device__ __forceinline__ Fe mul(const Fe& a, const Fe& b) {
+__device__ __forceinline__ Fe mul_comba(const Fe& a, const Fe& b) {
   uint32_t m[8], r[8];
   uint64_t acc = 0;
   uint32_t ov = 0;
@@ -160,6 +162,19 @@ __device__ __forceinline__ Fe mul(const Fe& a, const Fe& b) {
 #pragma unroll
   for (int j = 0; j < 8; j++) o.w[j] = r[j];
   return reduce_once<F>(o);
+}
+
+// The product the kernels use: the same product scanning as one generated asm block per field
+// (b2f_mont_asm.h, tools/gen_mont_asm.py): the column accumulator stays in two fixed VGPR pairs
+// and pallas' p_0 = 1 and p_7 = 2^30 words cost no multiplies (88 v_mad_u64_u32 against 104;
+// BN254 128). mul_comba above is the per-step form it replaced (mulbench variant 0 vs 4).
+template <class F>
+__device__ __forceinline__ Fe mul(const Fe& a, const Fe& b) {
+#ifdef B2F_MUL_COMBA  // A/B builds only (tools/build_variant.sh)
+  return mul_comba<F>(a, b);
+#else
+  return mul_asm<F>(a, b);
+#endif
 }
 
 // The operand-scanning CIOS form the product had before (kept as the cross-check of mul in

@@ -345,11 +345,14 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
 #else
 #define LKMUL(x, y) field::mul<F>(x, y)
 #endif
+// Rows per lane and waves per SIMD: ZR = 4 at 3 waves (166 VGPRs, no spills with the asm
+// product of b2f_mont_asm.h; 7.25 products per row against 8.25 at ZR = 2) measured 1.12-1.15 ms
+// per 64 x 131,065-row call against 1.25-1.29 for ZR = 2 at 4 waves (128 VGPRs), r05m
 #ifndef B2F_ZP_WAVES
-#define B2F_ZP_WAVES 4  // lk_zpass_kernel waves per SIMD (ZR = 2: 128 VGPRs)
+#define B2F_ZP_WAVES 3
 #endif
 #ifndef B2F_ZR
-#define B2F_ZR 2
+#define B2F_ZR 4
 #endif
 constexpr int ZR = B2F_ZR;       // rows per lane
 static_assert(ZR == 2 || ZR == 4, "rows per lane");
