@@ -32,25 +32,30 @@ sys.path.insert(0, os.path.join(ROOT, "zk-odst_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # The prover columns are bound by 256-bit Montgomery products: tools/mulbench.hip measures the
-# product b2f_field.h uses (product scanning, two word products per asm block, round 4) at up to
-# 158 G products/s chip-wide in pasta Fp and 129 in BN254 Fr (profiles/r04o_mulbench.txt: the best
-# of its variants and occupancies for the same code -- 3 waves per SIMD is as fast as 8; the CIOS
-# form before it: 114 / 105). Products per row: lookup = 2 (permute: num, den factors) + 4 (grand
-# product); permutation: counted per call from the circuit's copy cycles (the permutation leg).
-MULBENCH_GPS = {"pallas": 158.0, "bn254": 129.5}
-LOOKUP_PRODUCTS_PER_ROW = 6
-# Where the prover-column legs' numbers were diagnosed (committed profiles)
+# product b2f_field.h uses (one generated asm block per product, b2f_mont_asm.h, round 5) at up to
+# 162 G products/s chip-wide in pasta Fp and 136 in BN254 Fr (profiles/r05m_mulbench.txt: the best
+# of its chain counts and occupancies for the same code; the round-4 per-step form: 153 / 127).
+# Products per row the lookup call executes (round 5's one-pass design, 4 rows per lane, 1,024-row
+# look-back blocks): the z pass 5.5 per row in the lanes (den factor, suffix, lane total; num
+# factor, prefix, Q; K and z) + ~2 per row in the block's scans and look-back, and lk_npart_kernel
+# ~1.2 (the num factor's A part, its block product and reduction) = 8.7. The permutation leg
+# counts its products per call from the circuit's copy cycles.
+MULBENCH_GPS = {"pallas": 162.2, "bn254": 136.3}
+LOOKUP_PRODUCTS_PER_ROW = 8.7
+LOOKUP_MIN_PRODUCTS_PER_ROW = 6  # num, den factors + a grand product's 4: round 4's count
+# Where the prover-column legs' numbers were diagnosed: committed records of earlier runs
+# (historical, not measured by this run; DESIGN.md §4-5 tells the story)
 LOOKUP_EVIDENCE = {
-    "pmc": "profiles/r04a_lk_pmc.txt: lk_permute_kernel waves 54 % in s_waitcnt, 27 % issue-stalled; "
-           "its stores were the bound (ablations r04d: no column stores 306 us vs 557)",
-    "ab_ms_per_call": "1.49 (round 3) -> 1.24-1.27 (staged NT stores, in-block scans, r04m) -> "
-                      "1.14-1.16 (D before the permute pass, r04o)",
+    "history_ms_per_call": "1.16 (round 4: permute pass + gp passes) -> 1.29-1.31 (one pass, r05h) -> "
+                           "1.12-1.15 (asm product, 4 rows per lane, r05m/n) -> 1.04-1.08 (block windows "
+                           "instead of row searches, r05p)",
+    "files": ["profiles/r05n_lk_clock_zr4.txt", "profiles/r05n_lookup_ab_noprod_zr4.jsonl",
+              "profiles/r05m_lookup_ab_comba_zr4.jsonl"],
 }
 PERM_EVIDENCE = {
-    "pmc": "profiles/r04a_pm_pmc.txt: pm_factor_kernel 3.0e8 VALU instructions for 86 M products, "
-           "VMEM 2.4e6: bound by the products",
-    "ab_ms_per_call": "3.05 (round 3) -> 2.96 (r04l) -> 2.58-2.60 (factors fused with the chunk pass, "
-                      "pm_chunk_kernel, r04m/r04o)",
+    "history_ms_per_call": "3.05 (round 3) -> 2.58-2.60 (factors fused with the chunk pass, r04o) -> "
+                           "2.15-2.19 (sigma as keygen, divsteps inversion, r05) -> 2.13 (asm product, r05m)",
+    "files": ["profiles/r04a_pm_pmc.txt", "profiles/r05m_perm_ab_comba.jsonl"],
 }
 # 1 in BN254 Fr Montgomery form (R mod r) as four little-endian int64 limbs
 FR_ONE_MONT = [int.from_bytes((0x0e0a77c19a07df2f666ea36f7879462e36fc76959f60cd29ac96341c4ffffffb
@@ -675,7 +680,11 @@ def main():
                       "products_per_row": LOOKUP_PRODUCTS_PER_ROW,
                       "roofline": {"bound": "field products", "achieved": round(gps, 1),
                                    "peak": MULBENCH_GPS["pallas"], "unit": "G products/s",
-                                   "frac": round(gps / MULBENCH_GPS["pallas"], 4)},
+                                   "frac": round(gps / MULBENCH_GPS["pallas"], 4),
+                                   # the same time priced at round 4's 6 products per row
+                                   "frac_at_6_per_row": round(gps * LOOKUP_MIN_PRODUCTS_PER_ROW
+                                                              / LOOKUP_PRODUCTS_PER_ROW
+                                                              / MULBENCH_GPS["pallas"], 4)},
                       "field": "pasta Fp montgomery",
                       "all_rows_in_table": bool((lbad == -1).all().item()),
                       "evidence": LOOKUP_EVIDENCE}

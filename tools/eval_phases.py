@@ -1,6 +1,8 @@
 """Eval-kernel phase breakdown (diagnostics): runs the EVAL_CLOCK variant (B2F_DIAG_EVAL=23)
 on a 2^18 x 12-round batch and prints, per wave of the workgroup, the share of s_memtime
-cycles spent in each phase of the tile loop. python tools/eval_phases.py [--batch N]"""
+cycles spent in each phase of the tile loop. python tools/eval_phases.py [--batch N]
+--fused M: the fused kernel's clocked variant instead; --fill: the split fill's (FILL_CLOCK,
+B2F_DIAG_FILL=11), so the two can be compared on one box."""
 import argparse
 import ctypes
 import os
@@ -16,6 +18,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 18)
     ap.add_argument("--fused", type=int, default=0,
                     help="the fused kernel's clocked variant: 155 (full), 130 (stores only), 128")
+    ap.add_argument("--fill", action="store_true", help="the split fill's clocked variant")
     args = ap.parse_args()
     import torch
 
@@ -29,8 +32,15 @@ def main():
     batch.fill(eng, s)
     run = batch.fill_evaluate if args.fused else batch.evaluate
     os.environ["B2F_DIAG_FUSED" if args.fused else "B2F_DIAG_EVAL"] = str(args.fused) if args.fused else "23"
+    kname = "fill_eval" if args.fused else "eval"
+    global PHASES
+    if args.fill:
+        os.environ.pop("B2F_DIAG_EVAL", None)
+        os.environ["B2F_DIAG_FILL"] = "11"
+        run = batch.fill
+        kname = "fill"
+        PHASES = ["next-ops", "cells", "stores", "loop", "drain", "-", "-", "-"]
     if args.fused:
-        global PHASES
         # fused_hr_kernel (the half-round launch, second form) tick points
         PHASES = ["load+words", "chains+publish", "operands+cells", "stage-wait", "stores",
                   "fast-checks", "exact+end", "vmcnt"]
@@ -41,10 +51,13 @@ def main():
     eng.set_timing(True)
     run(eng, s)
     eng.sync(s)
-    ms = eng.kernel_times()["fill_eval" if args.fused else "eval"][0]
+    ms = eng.kernel_times()[kname][0]
     eng._check(eng.lib.b2f_debug_clock(eng.ctx, out))
-    rep = batch.report_dict()
-    print(("fused" if args.fused else "eval") + " (clocked variant) %.3f ms, verdict clean: %s" % (ms, rep["first_failure"] == 2**64 - 1))
+    if args.fill:
+        print("fill (clocked variant) %.3f ms" % ms)
+    else:
+        rep = batch.report_dict()
+        print(kname + " (clocked variant) %.3f ms, verdict clean: %s" % (ms, rep["first_failure"] == 2**64 - 1))
     for w in range(4):
         row = [out[8 * w + k] for k in range(8)]
         tot = sum(row) or 1

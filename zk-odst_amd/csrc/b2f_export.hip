@@ -15,7 +15,8 @@
 // BN254 Fr (halo2curves 0.3.2 bn256::Fr, r < 2^254, no such short form of r): mont(x) =
 // x * (2^256 mod r) mod r with a 32-bit quotient from a fixed-point reciprocal
 // (field::from_u32: 16 word products; the generic Montgomery product by R^2 it replaced took
-// 72 and made this kernel VALU-bound, 4.9 ms at 2^25 rows).
+// 72 and made this kernel VALU-bound, 4.9 ms at 2^25 rows). Each lane forms one cell and swaps
+// a half with its store partner (export_fp_kernel<3>), so every cell is formed once.
 //
 // HBM-bound: 4 B read, 32 B written per cell. A wave writes 64 x 16 B = 1 KiB contiguous per
 // store instruction (lane l stores 16-byte chunk l of a 1 KiB span, i.e. half l & 1 of cell
@@ -117,6 +118,33 @@ __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
 #pragma unroll
     for (int h = 0; h < 10; h++) {
       u64x2* dst = reinterpret_cast<u64x2*>(out + (uint64_t)h * out_rows * 4);
+      if (FORM == 3) {
+        // BN254's per-cell product is the cost, and both lanes of a store pair need the same
+        // cell: each lane forms one whole cell of two consecutive passes instead (even lane:
+        // pass i's, odd lane: pass i + 1's), and the pair swaps the half the other one stores
+#pragma unroll
+        for (int i = 0; i < XSUB; i += 2) {
+          // a bitwise select: `half ? x[h][i + 1] : x[h][i]` became a dynamic index (x in scratch)
+          const uint32_t xa = x[h][i], xb = x[h][i + 1];
+          const field::Fe m = field::from_u32<field::Bn254>(xa ^ ((xa ^ xb) & (0u - half)));
+          uint32_t own[4], give[4];
+#pragma unroll
+          for (int w = 0; w < 4; w++) {
+            own[w] = half ? m.w[4 + w] : m.w[w];   // the half this lane stores of its own cell
+            give[w] = half ? m.w[w] : m.w[4 + w];  // the half its partner stores
+          }
+          uint32_t got[4];
+#pragma unroll
+          for (int w = 0; w < 4; w++)  // lane ^ 1: DPP quad_perm [1, 0, 3, 2]
+            got[w] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)give[w], 0xB1, 0xf, 0xf, false);
+          const u64x2 mine = u64x2{(uint64_t)own[0] | ((uint64_t)own[1] << 32), (uint64_t)own[2] | ((uint64_t)own[3] << 32)};
+          const u64x2 other = u64x2{(uint64_t)got[0] | ((uint64_t)got[1] << 32), (uint64_t)got[2] | ((uint64_t)got[3] << 32)};
+          const uint64_t c0 = r0 + i * CELLS_PER_ITER + (t >> 1), c1 = c0 + CELLS_PER_ITER;
+          if (c0 < nrows) __builtin_nontemporal_store(half ? other : mine, dst + 2 * c0 + half);
+          if (c1 < nrows) __builtin_nontemporal_store(half ? mine : other, dst + 2 * c1 + half);
+        }
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < XSUB; i++) {
         uint64_t cell = r0 + i * CELLS_PER_ITER + (t >> 1);
@@ -174,8 +202,8 @@ hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint6
                             int cu_count, hipStream_t s) {
   // persistent grid: 4 workgroups per CU (halo2 column h -> a_i by kAofH)
   uint64_t tiles = (nrows + XT - 1) / XT;
-  // 122 VGPRs: 4 waves/SIMD; BN254 Montgomery 140 VGPRs: 3 (every workgroup resident at once)
-  uint64_t want = (uint64_t)cu_count * (form == B2F_FP_BN254_MONTGOMERY ? 3 : 4);
+  // 122 VGPRs: 4 waves/SIMD (BN254 Montgomery, one cell per lane: 64), every workgroup resident
+  uint64_t want = (uint64_t)cu_count * 4;
   uint32_t gx = (uint32_t)(tiles < want ? tiles : want);
   if (gx == 0) return hipSuccess;
   if (form == B2F_FP_BN254_MONTGOMERY) {

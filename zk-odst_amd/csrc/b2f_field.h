@@ -9,12 +9,14 @@
 // it in memory.
 //
 // Multiply: Montgomery product by product scanning (Comba) over 8 x 32-bit words: each column
-// of the 512-bit sum of a_i b_j and m_i p_j accumulates in a 64-bit VGPR pair by inline-asm
-// v_mad_u64_u32 whose carry goes into a third word by v_addc (mul below); the zero words of the
-// modulus are skipped (pallas has three). Both moduli have a top word below 2^31 - 1, so the
-// result is < 2p and one conditional subtraction finishes it (the oracle and halo2 use the
-// textbook form; the result is the same canonical residue). mul_cios keeps the operand-scanning
-// form it replaced, as tools/mulbench.hip's cross-check.
+// of the 512-bit sum of a_i b_j and m_i p_j accumulates in a 64-bit VGPR pair by
+// v_mad_u64_u32 whose carry goes into a third word by v_addc. `mul` is that product as one
+// generated inline-asm block per field (b2f_mont_asm.h, tools/gen_mont_asm.py: the accumulator
+// in two fixed VGPR pairs, pallas' p_0 = 1 and p_7 = 2^30 words without multiplies); mul_comba
+// is the same scheme as per-step asm (round 4) and mul_cios the operand-scanning form before it,
+// both kept as tools/mulbench.hip's cross-checks. Both moduli have a top word below 2^31 - 1, so
+// the result is < 2p and one conditional subtraction finishes it (the oracle and halo2 use the
+// textbook form; the result is the same canonical residue).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -167,7 +169,9 @@ __device__ __forceinline__ Fe mul_comba(const Fe& a, const Fe& b) {
 // The product the kernels use: the same product scanning as one generated asm block per field
 // (b2f_mont_asm.h, tools/gen_mont_asm.py): the column accumulator stays in two fixed VGPR pairs
 // and pallas' p_0 = 1 and p_7 = 2^30 words cost no multiplies (88 v_mad_u64_u32 against 104;
-// BN254 128). mul_comba above is the per-step form it replaced (mulbench variant 0 vs 4).
+// BN254 128). mul_comba above is the per-step form it replaced (mulbench variant 0 vs 4,
+// profiles/r05m_mulbench.txt: pallas 162 vs 153 G products/s, BN254 133-135 vs 126; in the
+// kernels: lookup call 1.27 vs 1.31 ms, permutation z call 2.13 vs 2.21, r05m).
 template <class F>
 __device__ __forceinline__ Fe mul(const Fe& a, const Fe& b) {
 #ifdef B2F_MUL_COMBA  // A/B builds only (tools/build_variant.sh)

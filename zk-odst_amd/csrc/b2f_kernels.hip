@@ -258,8 +258,10 @@ __global__ void tile_info_kernel(const uint64_t* __restrict__ off, uint32_t n, u
 
 
 // MODE (diagnostics; the product uses FILL_FULL): bit 0 = compute the cells (else zeros),
-// bit 1 = non-temporal stores (else plain stores).
-enum { FILL_COMPUTE = 1, FILL_NT = 2, FILL_FULL = 3 };
+// bit 1 = non-temporal stores (else plain stores), bit 3 = per-phase s_memtime totals per wave
+// slot into clk (b2f_debug_clock; phases: next tile's operand loads issued, cells formed -- the
+// wait for this tile's loads included --, stores issued, loop, final vmcnt drain).
+enum { FILL_COMPUTE = 1, FILL_NT = 2, FILL_FULL = 3, FILL_CLOCK = 8 };
 
 // Tiles of 1024 rows are dealt round-robin over the (persistent) workgroups, so at any time
 // the chip writes a narrow band of every column: one DRAM-friendly front per column instead
@@ -280,8 +282,17 @@ __global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_i
                                                     uint32_t* __restrict__ fixed,
                                                     const int* __restrict__ status,
                                                     const TileInfo* __restrict__ tinfo,
-                                                    uint64_t n_tiles) {
+                                                    uint64_t n_tiles,
+                                                    unsigned long long* __restrict__ clk) {
   __shared__ uint32_t rows[ROW_TABLE_WORDS];
+  uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
+  auto tick = [&](int k) {
+    if (MODE & FILL_CLOCK) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      if (k >= 0) ck[k] += now - tp;
+      tp = now;
+    }
+  };
   __shared__ __attribute__((aligned(16))) uint32_t sgiv[40 + 16];  // SIGMA bytes, IV
   const int tid = threadIdx.x;
   if (tid < ROW_TABLE_WORDS) rows[tid] = (&c_rows.r[0][0])[tid];
@@ -306,11 +317,14 @@ __global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_i
   };
   uint64_t t = blockIdx.x;
   QuadOps P;
+  tick(-1);
   if (t < n_tiles) ops(P, t);
+  tick(0);
   for (; t < n_tiles; t += G) {
     QuadOps Pn;
     Pn.rounds = ~0u;
     if (t + G < n_tiles) ops(Pn, t + G);
+    tick(0);
     const uint64_t gq = t * BLOCK + tid;
     if (gq < total_quads) {
       Quad Q;
@@ -322,6 +336,13 @@ __global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_i
         else
           quad_cells_ops(Q, P, IV);  // init and final regions
       }
+      if (MODE & FILL_CLOCK) {  // the cells must exist before the clock reads: a use of them
+        uint32_t sink = 0;
+#pragma unroll
+        for (int c = 0; c < 10; c++) sink ^= Q.c[c][0];
+        asm volatile("" ::"v"(sink));
+      }
+      tick(1);
       const uint64_t row = 4 * gq;
 #pragma unroll
       for (int c = 0; c < 11; c++) {
@@ -332,7 +353,17 @@ __global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_i
         else *dst = v;
       }
     }
+    tick(2);
     P = Pn;
+    tick(3);
+  }
+  if (MODE & FILL_CLOCK) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tick(4);
+    if ((tid & 63) == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) atomicAdd(&clk[8 * (tid >> 6) + k], (unsigned long long)ck[k]);
+    }
   }
 }
 
@@ -1243,15 +1274,20 @@ B2F_API int b2f_fill_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const ui
     return B2F_OK;
   }
 #endif
-  switch (diag_mode("B2F_DIAG_FILL", FILL_FULL)) {
+  const int fmode = diag_mode("B2F_DIAG_FILL", FILL_FULL);
+  if ((fmode & FILL_CLOCK) && !ctx->d_clock) {
+    HIPCHK(ctx, hipMalloc(&ctx->d_clock, 32 * sizeof(unsigned long long)));
+    HIPCHK(ctx, hipMemset(ctx->d_clock, 0, 32 * sizeof(unsigned long long)));
+  }
+  switch (fmode) {
 #define B2F_FILL(M)                                                                            \
   case M:                                                                                      \
     hipLaunchKernelGGL(fill_kernel<M>, dim3(wgs), dim3(BLOCK), 0, s, d_in, nn, d_offsets,      \
                        total_rows, ctx->d_rec, d_advice, d_fixed, ctx->d_status, ctx->d_tiles, \
-                       nt);                                                                    \
+                       nt, ctx->d_clock);                                                      \
     break;
 #ifdef B2F_DIAG
-    B2F_FILL(0) B2F_FILL(1) B2F_FILL(2)
+    B2F_FILL(0) B2F_FILL(1) B2F_FILL(2) B2F_FILL(FILL_FULL | FILL_CLOCK)
 #endif
     default: B2F_FILL(3)
 #undef B2F_FILL

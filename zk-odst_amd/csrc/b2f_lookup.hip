@@ -71,8 +71,9 @@ __device__ __forceinline__ uint32_t tag16(uint32_t x) { return x < 256u ? 0u : (
 template <class F>
 __global__ __launch_bounds__(256) void lk_table_kernel(Chal ch, Fe* __restrict__ Tx,
                                                        uint64_t* __restrict__ key,
-                                                       uint32_t* __restrict__ perm) {
+                                                       uint32_t* __restrict__ perm, Fe* __restrict__ bg) {
   const uint32_t x = blockIdx.x * 256 + threadIdx.x;
+  if (x < 2) bg[x] = field::to_mont<F>(field::load_words(x ? ch.gamma : ch.beta));  // for the z pass
   const Fe th = field::to_mont<F>(field::load_words(ch.theta));
   const Fe th2 = field::mul<F>(th, th);
   const Fe t = field::add<F>(field::add<F>(field::mul<F>(th2, field::from_u32<F>(tag16(x))),
@@ -187,23 +188,27 @@ __global__ __launch_bounds__(CNT_THREADS) void lk_count_kernel(
 // The rank-order scan of a circuit's counts, split over SC_PARTS workgroups per circuit of
 // SC_THREADS threads x SC_PER consecutive ranks (the counts gathered into registers once per
 // pass): lk_scan_sums writes each part's totals, lk_scan_write adds the totals of the parts
-// before it and scans its own ranks. (One 1,024-thread workgroup per circuit holding 64 ranks per
+// before it and scans its own ranks. Four running sums: rows (pos = a run's first row), runs
+// (dcnt, inclusive), leftover items (a rank's table multiplicity not taken by a run start) and
+// leftover ranks -- the ranks with leftover items are written compacted (lrank, lstart = their
+// first leftover index), so a block of rows' leftover items span at most one entry per item. (One 1,024-thread workgroup per circuit holding 64 ranks per
 // thread kept the gathered counts in scratch and used 64 of the 256 CUs.)
 #ifndef B2F_LK_SAMP
-#define B2F_LK_SAMP 32  // pos / lp sample stride of the z pass's LDS search tables
+#define B2F_LK_SAMP 32  // pos / lstart sample stride of lk_block_kernel's LDS search tables
 #endif
 constexpr int SAMP = B2F_LK_SAMP;
 static_assert(SAMP == 16 || SAMP == 32, "sample stride: a multiple of the scan's 16 ranks per thread");
-constexpr int SAMPLE = TROWS / SAMP;  // every SAMP-th pos / lp entry, for the z pass's searches
+constexpr int SAMPLE = TROWS / SAMP;  // every SAMP-th pos / lstart entry, for lk_block_kernel
 constexpr int SC_PARTS = 16, SC_THREADS = 256, SC_PER = TROWS / (SC_PARTS * SC_THREADS);
 static_assert(SC_PER == 16, "one search sample per thread");
 
 // the counts of this thread's SC_PER ranks (rank order read as 16-byte vectors), the index of the
-// rank holding table row 0 (-1: none), and the three sums: rows, runs, leftover table multiplicity
+// rank holding table row 0 (-1: none), and the four sums: rows, runs, leftover table
+// multiplicity, ranks with leftovers
 struct RankRun {
   uint32_t nv[SC_PER];
   int iz;
-  uint32_t sc, sd, sl;
+  uint32_t sc, sd, sl, sr;
 };
 __device__ __forceinline__ RankRun rank_run(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ cnt,
                                             uint32_t r0, uint32_t mult0) {
@@ -219,13 +224,15 @@ __device__ __forceinline__ RankRun rank_run(const uint32_t* __restrict__ perm, c
     R.nv[4 * i + 3] = cnt[x.w];
     R.iz = x.x == 0 ? 4 * i : x.y == 0 ? 4 * i + 1 : x.z == 0 ? 4 * i + 2 : x.w == 0 ? 4 * i + 3 : R.iz;
   }
-  R.sc = R.sd = R.sl = 0;
+  R.sc = R.sd = R.sl = R.sr = 0;
 #pragma unroll
   for (int i = 0; i < SC_PER; i++) {
     const uint32_t n = R.nv[i];
+    const uint32_t m = (i == R.iz ? mult0 : 1u) - (n ? 1u : 0u);
     R.sc += n;
     R.sd += n ? 1u : 0u;
-    R.sl += (i == R.iz ? mult0 : 1u) - (n ? 1u : 0u);
+    R.sl += m;
+    R.sr += m ? 1u : 0u;
   }
   return R;
 }
@@ -236,71 +243,73 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_sums(const uint32_t* __res
   const uint32_t pt = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
   const uint32_t mult0 = (uint32_t)(usable - TROWS + 1);  // table row 0 fills the rest
   const RankRun R = rank_run(perm, count + (uint64_t)c * TROWS, (pt * SC_THREADS + t) * SC_PER, mult0);
-  __shared__ uint32_t s[3][SC_THREADS];
+  __shared__ uint32_t s[4][SC_THREADS];
   s[0][t] = R.sc;
   s[1][t] = R.sd;
   s[2][t] = R.sl;
+  s[3][t] = R.sr;
   __syncthreads();
   for (uint32_t w = SC_THREADS / 2; w > 0; w >>= 1) {
     if (t < w) {
-      s[0][t] += s[0][t + w];
-      s[1][t] += s[1][t + w];
-      s[2][t] += s[2][t + w];
+#pragma unroll
+      for (int q = 0; q < 4; q++) s[q][t] += s[q][t + w];
     }
     __syncthreads();
   }
-  if (t < 3) part[((uint64_t)c * SC_PARTS + pt) * 3 + t] = s[t][0];
+  if (t < 4) part[((uint64_t)c * SC_PARTS + pt) * 4 + t] = s[t][0];
 }
 
 __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __restrict__ perm,
                                                             const uint32_t* __restrict__ count,
                                                             uint64_t usable, const uint32_t* __restrict__ part,
                                                             uint32_t* __restrict__ pos, uint32_t* __restrict__ dcnt,
-                                                            uint32_t* __restrict__ lp, uint32_t* __restrict__ samp) {
+                                                            uint32_t* __restrict__ lrank, uint32_t* __restrict__ lstart,
+                                                            uint32_t* __restrict__ samp, uint32_t* __restrict__ nlr) {
   const uint32_t pt = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
   const uint32_t mult0 = (uint32_t)(usable - TROWS + 1);
   const uint32_t r0 = (pt * SC_THREADS + t) * SC_PER;
   const RankRun R = rank_run(perm, count + (uint64_t)c * TROWS, r0, mult0);
-  uint32_t bc = 0, bd = 0, bl = 0;  // totals of the parts before this one
+  uint32_t bsum[4] = {0, 0, 0, 0};  // totals of the parts before this one
   for (uint32_t q = 0; q < pt; q++) {
-    const uint32_t* pq = part + ((uint64_t)c * SC_PARTS + q) * 3;
-    bc += pq[0];
-    bd += pq[1];
-    bl += pq[2];
+    const uint32_t* pq = part + ((uint64_t)c * SC_PARTS + q) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; i++) bsum[i] += pq[i];
   }
-  __shared__ uint32_t s[3][SC_THREADS];
-  s[0][t] = R.sc;
-  s[1][t] = R.sd;
-  s[2][t] = R.sl;
+  __shared__ uint32_t s[4][SC_THREADS];
+  const uint32_t own[4] = {R.sc, R.sd, R.sl, R.sr};
+  uint32_t inc[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    s[i][t] = own[i];
+    inc[i] = own[i];
+  }
   __syncthreads();
-  uint32_t ic = R.sc, id = R.sd, il = R.sl;
   for (uint32_t off = 1; off < SC_THREADS; off <<= 1) {  // inclusive Hillis-Steele
-    uint32_t a = 0, b = 0, d = 0;
+    uint32_t a[4] = {0, 0, 0, 0};
     if (t >= off) {
-      a = s[0][t - off];
-      b = s[1][t - off];
-      d = s[2][t - off];
+#pragma unroll
+      for (int i = 0; i < 4; i++) a[i] = s[i][t - off];
     }
     __syncthreads();
-    ic += a;
-    id += b;
-    il += d;
-    s[0][t] = ic;
-    s[1][t] = id;
-    s[2][t] = il;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      inc[i] += a[i];
+      s[i][t] = inc[i];
+    }
     __syncthreads();
   }
-  uint32_t ec = bc + ic - R.sc, ed = bd + id - R.sd, el = bl + il - R.sl;  // exclusive
+  // exclusive: rows, runs, leftover items, leftover ranks
+  uint32_t ec = bsum[0] + inc[0] - own[0], ed = bsum[1] + inc[1] - own[1], el = bsum[2] + inc[2] - own[2],
+           er = bsum[3] + inc[3] - own[3];
   uint4* P4 = reinterpret_cast<uint4*>(pos + (uint64_t)c * TROWS + r0);
   uint4* D4 = reinterpret_cast<uint4*>(dcnt + (uint64_t)c * TROWS + r0);
-  uint4* L4 = reinterpret_cast<uint4*>(lp + (uint64_t)c * TROWS + r0);
-  if (r0 % SAMP == 0) {  // a search sample
-    samp[(uint64_t)c * 2 * SAMPLE + r0 / SAMP] = ec;
-    samp[(uint64_t)c * 2 * SAMPLE + SAMPLE + r0 / SAMP] = el;
-  }
+  uint32_t* LR = lrank + (uint64_t)c * TROWS;
+  uint32_t* LS = lstart + (uint64_t)c * TROWS;
+  uint32_t* SP = samp + (uint64_t)c * 2 * SAMPLE;
+  if (r0 % SAMP == 0) SP[r0 / SAMP] = ec;  // a pos sample
 #pragma unroll
   for (int i = 0; i < SC_PER / 4; i++) {
-    uint32_t pq[4], dq[4], lq[4];
+    uint32_t pq[4], dq[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const uint32_t n = R.nv[4 * i + j];
@@ -308,14 +317,19 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
       pq[j] = ec;
       ed += n ? 1u : 0u;
       dq[j] = ed;
-      lq[j] = el;
+      if (m) {
+        LR[er] = r0 + 4 * i + j;
+        LS[er] = el;
+        if (er % SAMP == 0) SP[SAMPLE + er / SAMP] = el;  // an lstart sample
+        er++;
+      }
       ec += n;
       el += m;
     }
     P4[i] = make_uint4(pq[0], pq[1], pq[2], pq[3]);
     D4[i] = make_uint4(dq[0], dq[1], dq[2], dq[3]);
-    L4[i] = make_uint4(lq[0], lq[1], lq[2], lq[3]);
   }
+  if (pt == SC_PARTS - 1 && t == SC_THREADS - 1) nlr[c] = er;  // ranks with leftovers
 }
 
 // ------------------------------------------------------------------ the grand product, one pass
@@ -345,11 +359,13 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
 #else
 #define LKMUL(x, y) field::mul<F>(x, y)
 #endif
-// Rows per lane and waves per SIMD: ZR = 4 at 3 waves (166 VGPRs, no spills with the asm
-// product of b2f_mont_asm.h; 7.25 products per row against 8.25 at ZR = 2) measured 1.12-1.15 ms
-// per 64 x 131,065-row call against 1.25-1.29 for ZR = 2 at 4 waves (128 VGPRs), r05m
+// Rows per lane and waves per SIMD: ZR = 4 (7.25 products per row in the lanes against 8.25 at
+// ZR = 2) at 4 waves: 128 VGPRs with 8 spilled (beta and gamma are uniform loads, the asm product
+// of b2f_mont_asm.h keeps its accumulator in 4 fixed VGPRs). Measured per 64 x 131,065-row call:
+// ZR = 2 at 4 waves 1.25-1.29 ms, ZR = 4 at 3 waves 1.12-1.15 (r05m), and with the block windows
+// of lk_block_kernel 3 waves 1.04-1.05 against 4 waves 1.01-1.03 (r05q, same process)
 #ifndef B2F_ZP_WAVES
-#define B2F_ZP_WAVES 3
+#define B2F_ZP_WAVES 4
 #endif
 #ifndef B2F_ZR
 #define B2F_ZR 4
@@ -610,34 +626,96 @@ __device__ __forceinline__ void wave_store_zr(uint64_t* dst, uint4* st, uint32_t
   }
 }
 
-// last index r with a[r] <= v (a nondecreasing over TROWS entries, a[0] <= v): the top levels
-// of the search over the workgroup's LDS sample s[k] = a[SAMP k], then the SAMP entries of that
-// block (64 or 128 contiguous bytes, all loads in flight at once) in registers.
-__device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, const uint32_t* s,
-                                            uint32_t v) {
-  uint32_t lo = 0, hi = SAMPLE;  // last k with s[k] <= v, in [lo, hi)
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (s[mid] <= v) lo = mid; else hi = mid;
-  }
-  const uint4* blk = reinterpret_cast<const uint4*>(a + SAMP * lo);
+// lk_block_kernel's searches: the last index r < lim with a[r] <= v (a nondecreasing, a[0] <= v).
+// The top levels run over the workgroup's LDS sample s[k] = a[SAMP k] (ns valid samples) as a
+// fixed-step branchless binary search, then the SAMP entries of that block (64 or 128
+// contiguous bytes) are counted in registers; eq tells whether one of them equals v.
+static_assert((SAMPLE & (SAMPLE - 1)) == 0, "fixed-step search");
+__device__ __forceinline__ uint32_t le_sample(const uint32_t* s, uint32_t v, uint32_t ns) {
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t step = SAMPLE / 2; step > 0; step >>= 1) lo = lo + step < ns && s[lo + step] <= v ? lo + step : lo;
+  return lo;
+}
+__device__ __forceinline__ uint32_t le_block(const uint32_t* __restrict__ a, uint32_t kb, uint32_t v, uint32_t lim,
+                                             bool& eq) {
+  const uint4* blk = reinterpret_cast<const uint4*>(a + SAMP * kb);
   uint4 q[SAMP / 4];
 #pragma unroll
   for (int i = 0; i < SAMP / 4; i++) q[i] = blk[i];
-  uint32_t n = 0;  // entries <= v (the first = s[lo] <= v; nondecreasing)
+  const uint32_t i0 = SAMP * kb;
+  uint32_t n = 0, e = 0;
 #pragma unroll
-  for (int i = 0; i < SAMP / 4; i++)
-    n += (i ? (q[i].x <= v ? 1u : 0u) : 0u) + (q[i].y <= v ? 1u : 0u) + (q[i].z <= v ? 1u : 0u) +
-         (q[i].w <= v ? 1u : 0u);
-  return SAMP * lo + n;
+  for (int i = 0; i < SAMP / 4; i++) {
+    const uint32_t w[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const bool in = i0 + 4 * i + u < lim;
+      n += in && w[u] <= v ? 1u : 0u;
+      e |= in && w[u] == v ? 1u : 0u;
+    }
+  }
+  eq = e != 0;
+  return i0 + n - 1;  // the block's first entry s[kb] <= v
+}
+
+// Per look-back block (rows [base, end), end = min(base + LB, usable)) of every circuit: the pos
+// ranks of its first and last rows (every row of the block lies in a run of that rank window),
+// J0 / J1 = the repeated rows (those that are not a run's first row) before base / before end,
+// and the window of compacted leftover ranks holding leftover indices [n_left - J1,
+// n_left - 1 - J0], which the block's repeated rows take (the j-th repeated row takes
+// n_left - 1 - j). J(p) = p - dcnt[ra(p)] + [p starts its run]. One thread per block; the z pass
+// then finds every row's runs from these windows without searching.
+constexpr int BLK_WORDS = 8;
+constexpr int BK_T = 128;
+__global__ __launch_bounds__(BK_T) void lk_block_kernel(uint64_t usable, uint64_t nb, const uint32_t* __restrict__ pos,
+                                                        const uint32_t* __restrict__ dcnt,
+                                                        const uint32_t* __restrict__ lstart,
+                                                        const uint32_t* __restrict__ samp,
+                                                        const uint32_t* __restrict__ nlr, uint32_t* __restrict__ blk) {
+  __shared__ uint4 ss[2 * SAMPLE / 4];
+  const uint32_t c = blockIdx.y, t = threadIdx.x;
+  {
+    const uint4* sa = reinterpret_cast<const uint4*>(samp + (uint64_t)c * 2 * SAMPLE);
+    for (uint32_t i = t; i < (uint32_t)SAMPLE / 2; i += BK_T) ss[i] = sa[i];
+  }
+  __syncthreads();
+  const uint32_t* sP = reinterpret_cast<const uint32_t*>(ss);
+  const uint32_t* sL = sP + SAMPLE;
+  const uint32_t us = (uint32_t)usable;
+  const uint32_t* P = pos + (uint64_t)c * TROWS;
+  const uint32_t* D = dcnt + (uint64_t)c * TROWS;
+  const uint32_t* LS = lstart + (uint64_t)c * TROWS;
+  const uint32_t n_left = us - D[TROWS - 1], nr = nlr[c], nsl = (nr + SAMP - 1) / SAMP;
+  for (uint64_t b = (uint64_t)blockIdx.x * BK_T + t; b < nb; b += (uint64_t)gridDim.x * BK_T) {
+    const uint32_t base = (uint32_t)b * LB, end = us - base < (uint32_t)LB ? us : base + LB;
+    bool st;
+    const uint32_t r0 = le_block(P, le_sample(sP, base, SAMPLE), base, TROWS, st);
+    const uint32_t J0 = base - D[r0] + (st ? 1u : 0u);
+    const uint32_t r1 = le_block(P, le_sample(sP, end - 1, SAMPLE), end - 1, TROWS, st);
+    uint32_t J1 = n_left;
+    if (end < us) {
+      const uint32_t re = le_block(P, le_sample(sP, end, SAMPLE), end, TROWS, st);
+      J1 = end - D[re] + (st ? 1u : 0u);
+    }
+    uint32_t k0 = 1, k1 = 0;  // empty
+    if (J1 > J0) {
+      k0 = le_block(LS, le_sample(sL, n_left - J1, nsl), n_left - J1, nr, st);
+      k1 = le_block(LS, le_sample(sL, n_left - 1 - J0, nsl), n_left - 1 - J0, nr, st);
+    }
+    uint4* o = reinterpret_cast<uint4*>(blk + ((uint64_t)c * nb + b) * BLK_WORDS);
+    o[0] = make_uint4(r0, r1, J0, J1);
+    o[1] = make_uint4(k0, k1, 0u, 0u);
+  }
 }
 
 // The five columns of one look-back block (LB = 256 ZR rows). Lane t of the workgroup owns rows
 // base + ZR t + j:
-//  1. searches: A' = Ts[r] for the run r holding p (binary search of pos: the top levels in the
-//     workgroup's LDS sample), S' = A' at a run start, else leftover item L - 1 - j for the j-th
-//     repeated row (halo2 hands leftovers out in ascending order, each to the last open repeated
-//     row), found by binary search of LP;
+//  1. the runs: A' = Ts[r] for the run r holding p, S' = A' at a run start, else leftover item
+//     n_left - 1 - j for the j-th repeated row (halo2 hands leftovers out in ascending order,
+//     each to the last open repeated row). The workgroup scatters the runs of its pos window and
+//     the leftover ranks of its lstart window (lk_block_kernel) into LDS tables indexed by row
+//     and by leftover index, so each row reads its ranks instead of searching;
 //  2. the den side: A', S' staged and stored as 1 KiB runs, den_j = (A' + beta)(S' + gamma), the
 //     in-lane den suffix and the lane's den total; one wave scans the 256 den totals (suffix)
 //     and publishes the block's den product as its look-back aggregate at once;
@@ -647,22 +725,23 @@ __device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, cons
 //     for the den product after the block -- its predecessors have had the whole num side to
 //     publish -- and publishes its inclusive product;
 //  4. z[p + 1] = (num prefix before the lane) (den suffix after the lane, times NK_b Dafter_b) Q_j.
-// The scans run on waves chosen by the ticket, so the SIMDs share them; the LDS sample of the
-// searches is reused for the lane totals once every wave has searched.
+// The scans run on waves chosen by the ticket, so the SIMDs share them; the LDS tables of step 1
+// are reused for the lane totals once every wave has read its rows.
 template <class F, bool MONT>
 __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES))) void lk_zpass_kernel(
     const uint32_t* __restrict__ adv, uint64_t total_rows, const uint64_t* __restrict__ row_begin,
     uint32_t c0, uint32_t g, uint64_t usable, uint64_t nb, const Fe* __restrict__ Tx,
     const Fe* __restrict__ Ts, uint64_t* __restrict__ out, uint64_t out_rows, Chal ch,
-    const uint32_t* __restrict__ pos, const uint32_t* __restrict__ dcnt, const uint32_t* __restrict__ lp,
-    const uint32_t* __restrict__ samp, const Fe* __restrict__ NK, const Fe* __restrict__ Dnum,
+    const uint32_t* __restrict__ pos, const uint32_t* __restrict__ dcnt, const uint32_t* __restrict__ lrank,
+    const uint32_t* __restrict__ lstart, const uint32_t* __restrict__ blk, const uint32_t* __restrict__ nlr,
+    const Fe* __restrict__ NK, const Fe* __restrict__ Dnum, const Fe* __restrict__ bg,
     uint64_t* __restrict__ lbs, uint32_t* __restrict__ ticket, int* __restrict__ sticky, uint64_t lb_zero) {
-  // the search samples, then (after every wave has searched) the lane totals
+  // the row and leftover tables, then (after every wave has read its rows) the lane totals
   static_assert(ZT == 256, "the scans take 4 lane totals per lane");
-  constexpr int SMEM = 2 * SAMPLE * 4 > 2 * ZT * 32 ? 2 * SAMPLE * 4 : 2 * ZT * 32;
+  constexpr int SMEM = 2 * LB * 4 > 2 * ZT * 32 ? 2 * LB * 4 : 2 * ZT * 32;
   __shared__ uint4 smem[SMEM / 16];
-  uint32_t* sP = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* sL = sP + SAMPLE;
+  uint32_t* ent = reinterpret_cast<uint32_t*>(smem);  // per row: rank | start << 16 | (j - J0) << 17
+  uint32_t* yl = ent + LB;                             // per leftover index - ylo: its rank
   Fe* sN = reinterpret_cast<Fe*>(smem);
   Fe* sD = sN + ZT;
   __shared__ uint4 stage[4][ZSTAGE];  // per wave: the column staging
@@ -676,19 +755,15 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
   // descending block order: every circuit's last block first
   const uint32_t c = tk % g;
   const uint64_t b = nb - 1 - tk / g;
-  {
-    const uint4* sa = reinterpret_cast<const uint4*>(samp + (uint64_t)c * 2 * SAMPLE);
-    for (uint32_t i = t; i < (uint32_t)SAMPLE / 2; i += ZT) smem[i] = sa[i];
-  }
-  const Fe beta = field::to_mont<F>(field::load_words(ch.beta));
-  const Fe gamma = field::to_mont<F>(field::load_words(ch.gamma));
+  const Fe beta = bg[0], gamma = bg[1];  // Montgomery forms (lk_table_kernel): uniform loads
   const Circ k = circ(row_begin, total_rows, usable, c0 + c);
   // 32-bit row arithmetic (usable <= 2^31, b2f_lookup_columns_dev)
   const uint32_t us = (uint32_t)usable, n_in = (uint32_t)k.n_in;
   const uint32_t* a1 = adv + total_rows + k.first;  // the circuit's dense cells
   const uint32_t* P = pos + (uint64_t)c * TROWS;
   const uint32_t* D = dcnt + (uint64_t)c * TROWS;
-  const uint32_t* L = lp + (uint64_t)c * TROWS;
+  const uint32_t* LR = lrank + (uint64_t)c * TROWS;
+  const uint32_t* LS = lstart + (uint64_t)c * TROWS;
   const uint32_t n_left = us - D[TROWS - 1];  // repeated rows = leftover items
   uint64_t* o = out + (uint64_t)(c0 + c) * 5 * out_rows * 4;
   const uint32_t base = (uint32_t)b * LB, p0 = base + ZR * t, r0 = base + 64u * ZR * wv;
@@ -701,16 +776,62 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
   const uint32_t e0 = 4 * lane;                     // a scanning lane's first entry
   __syncthreads();
   LKCLK(0);
-  // 1. the searches
   uint32_t x[ZR], ra[ZR], rs[ZR];
+  // 1. the runs of the block's rows: every rank of the pos window writes its rows' entries,
+  // every compacted leftover rank of the lstart window its leftover indices' rank
+  {
+    const uint4* bt = reinterpret_cast<const uint4*>(blk + ((uint64_t)c * nb + b) * BLK_WORDS);
+    const uint4 w0 = bt[0], w1 = bt[1];
+    const uint32_t J0 = w0.z, end = us - base < (uint32_t)LB ? us : base + LB, ylo = n_left - w0.w,
+                   yhi = n_left - J0, nr = nlr[c];
+    // the first SC_U ranks of each window per thread (windows are ~LB / 2 wide): every load in
+    // flight before the first write; wider windows finish in the loops after
+    constexpr int SC_U = 4;
+    uint32_t ps0[SC_U], ps1[SC_U], pd[SC_U], ly0[SC_U], ly1[SC_U], lr[SC_U];
 #pragma unroll
-  for (int j = 0; j < ZR; j++) {
-    const uint32_t p = p0 + j;
-    x[j] = p < n_in ? (a1[p] & 0xffffu) : 0u;
-    ra[j] = rs[j] = 0;
-    if (p < us) {
-      ra[j] = last_le(P, sP, p);
-      rs[j] = P[ra[j]] == p ? ra[j] : last_le(L, sL, n_left - 1u - (p - D[ra[j]]));
+    for (int u = 0; u < SC_U; u++) {
+      const uint32_t r = w0.x + t + ZT * u, kk = w1.x + t + ZT * u;
+      ps0[u] = ps1[u] = pd[u] = 0;
+      ly0[u] = ly1[u] = lr[u] = 0;
+      if (r <= w0.y) {
+        ps0[u] = P[r];
+        ps1[u] = r + 1 < (uint32_t)TROWS ? P[r + 1] : us;
+        pd[u] = D[r];
+      }
+      if (kk <= w1.y) {
+        ly0[u] = LS[kk];
+        ly1[u] = kk + 1 < nr ? LS[kk + 1] : n_left;
+        lr[u] = LR[kk];
+      }
+    }
+    auto put_run = [&](uint32_t r, uint32_t s0, uint32_t s1, uint32_t dr) {
+      const uint32_t lo = s0 > base ? s0 : base, hi = s1 < end ? s1 : end;
+      for (uint32_t q = lo; q < hi; q++) ent[q - base] = q == s0 ? (r | 0x10000u) : (r | ((q - dr - J0) << 17));
+    };
+    auto put_left = [&](uint32_t r, uint32_t y0, uint32_t y1) {
+      const uint32_t lo = y0 > ylo ? y0 : ylo, hi = y1 < yhi ? y1 : yhi;
+      for (uint32_t y = lo; y < hi; y++) yl[y - ylo] = r;
+    };
+#pragma unroll
+    for (int u = 0; u < SC_U; u++) {
+      put_run(w0.x + t + ZT * u, ps0[u], ps1[u], pd[u]);  // empty (s0 = s1 = 0) past the window
+      put_left(lr[u], ly0[u], ly1[u]);
+    }
+    for (uint32_t r = w0.x + t + ZT * SC_U; r <= w0.y; r += ZT)
+      put_run(r, P[r], r + 1 < (uint32_t)TROWS ? P[r + 1] : us, D[r]);
+    for (uint32_t kk = w1.x + t + ZT * SC_U; kk <= w1.y; kk += ZT)
+      put_left(LR[kk], LS[kk], kk + 1 < nr ? LS[kk + 1] : n_left);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ZR; j++) {
+      const uint32_t p = p0 + j;
+      x[j] = p < n_in ? (a1[p] & 0xffffu) : 0u;
+      ra[j] = rs[j] = 0;
+      if (p < us) {
+        const uint32_t e = ent[p - base];
+        ra[j] = e & 0xffffu;
+        rs[j] = (e & 0x10000u) ? ra[j] : yl[yhi - 1u - (e >> 17) - ylo];
+      }
     }
   }
   LKCLK(1);
@@ -737,7 +858,7 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
 #pragma unroll
   for (int j = ZR - 3; j >= 0; j--) sf[j] = LKMUL(d[j + 1], sf[j + 1]);
   const Fe dl = LKMUL(d[0], sf[0]);
-  __syncthreads();  // every wave has searched: the samples' memory takes the lane totals
+  __syncthreads();  // every wave has read its rows: the tables' memory takes the lane totals
   sD[pz(t)] = dl;
   __syncthreads();
   LKCLK(2);
@@ -906,13 +1027,17 @@ struct Carve {
   uint32_t* count;  // group x TROWS
   uint32_t* pos;
   uint32_t* dcnt;
-  uint32_t* lp;
-  uint32_t* samp;  // group x 2 x SAMPLE
+  uint32_t* lrank;   // group x TROWS: the ranks with leftover items, compacted
+  uint32_t* lstart;  // group x TROWS: their first leftover index
+  uint32_t* samp;    // group x 2 x SAMPLE: pos and lstart samples
+  uint32_t* nlr;     // group: ranks with leftovers
+  uint32_t* blk;     // group x nb x BLK_WORDS: lk_block_kernel's windows
   uint32_t* part;  // group x SC_PARTS x 3 (rank-scan part totals)
   Fe* partA;  // group x nb: block num products, the A part
   Fe* partS;  // nb: the S part (every circuit's)
   Fe* NK;     // group x nb: Nbefore_b D^-1
   Fe* Dnum;   // group: D from the num side
+  Fe* bg;     // beta, gamma in Montgomery form
   uint64_t* lbs;     // group x nb x LBS_WORDS look-back state, then the ticket counter
   void* sort_tmp;
   size_t sort_bytes;
@@ -946,13 +1071,17 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   k.count = (uint32_t*)take(4ull * TROWS * group);
   k.pos = (uint32_t*)take(4ull * TROWS * group);
   k.dcnt = (uint32_t*)take(4ull * TROWS * group);
-  k.lp = (uint32_t*)take(4ull * TROWS * group);
+  k.lrank = (uint32_t*)take(4ull * TROWS * group);
+  k.lstart = (uint32_t*)take(4ull * TROWS * group);
   k.samp = (uint32_t*)take(8ull * SAMPLE * group);
-  k.part = (uint32_t*)take(12ull * SC_PARTS * group);
+  k.nlr = (uint32_t*)take(4ull * group);
+  k.blk = (uint32_t*)take(4ull * BLK_WORDS * nb * group);
+  k.part = (uint32_t*)take(16ull * SC_PARTS * group);
   k.partA = (Fe*)take(sizeof(Fe) * nb * group);
   k.partS = (Fe*)take(sizeof(Fe) * nb);
   k.NK = (Fe*)take(sizeof(Fe) * nb * group);
   k.Dnum = (Fe*)take(sizeof(Fe) * group);
+  k.bg = (Fe*)take(sizeof(Fe) * 2);
   k.lbs_bytes = 8ull * LBS_WORDS * nb * group + 64;  // + the ticket counter
   k.lbs = (uint64_t*)take(k.lbs_bytes);
   k.sort_bytes = sort_temp_bytes();
@@ -969,7 +1098,7 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   Carve k = carve(scratch, group, usable_rows);
   const uint64_t nb = n_lb(usable_rows);
   const dim3 tb(TROWS / 256);
-  hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm);
+  hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm, k.bg);
   // one radix sort by the top limb of the canonical value (< 2^63: both moduli are < 2^255),
   // then ties in the top limb ordered by the lower limbs
   uint32_t* pa = k.perm2;
@@ -1001,13 +1130,15 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
                        total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
     hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
     hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
-                       k.part, k.pos, k.dcnt, k.lp, k.samp);
+                       k.part, k.pos, k.dcnt, k.lrank, k.lstart, k.samp, k.nlr);
+    hipLaunchKernelGGL(lk_block_kernel, dim3((uint32_t)((nb + BK_T - 1) / BK_T), g), dim3(BK_T), 0, s, usable_rows,
+                       nb, k.pos, k.dcnt, k.lstart, k.samp, k.nlr, k.blk);
     if ((e = hipMemsetAsync(k.lbs, 0, 8ull * LBS_WORDS * nb * g + 64, s)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(s, side.join, 0)) != hipSuccess) return e;
     uint32_t* ticket = reinterpret_cast<uint32_t*>(k.lbs + LBS_WORDS * nb * g);
     hipLaunchKernelGGL((mont ? lk_zpass_kernel<F, true> : lk_zpass_kernel<F, false>), dim3((uint32_t)(nb * g)),
                        dim3(ZT), 0, s, d_advice, total_rows, d_row_begin, c0, g, usable_rows, nb, k.Tx, k.Ts,
-                       d_out, out_rows, ch, k.pos, k.dcnt, k.lp, k.samp, k.NK, k.Dnum, k.lbs, ticket, sticky, 0ull);
+                       d_out, out_rows, ch, k.pos, k.dcnt, k.lrank, k.lstart, k.blk, k.nlr, k.NK, k.Dnum, k.bg, k.lbs, ticket, sticky, 0ull);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;

@@ -200,7 +200,10 @@ constexpr uint32_t PM_CL = 3;  // pm_chunk_kernel's column sets: chunk_len <= 3 
 // waves per SIMD pm_chunk_kernel is compiled for: BN254 fits 4 (119 VGPRs, no scratch; 147 at
 // the default budget, 3 waves); pasta's form spills at 128, so it keeps 3
 template <class F> struct PmWaves { static constexpr int v = 3; };
-template <> struct PmWaves<field::Bn254> { static constexpr int v = 4; };
+#ifndef B2F_PM_WAVES_BN254
+#define B2F_PM_WAVES_BN254 4
+#endif
+template <> struct PmWaves<field::Bn254> { static constexpr int v = B2F_PM_WAVES_BN254; };
 // The factors fused with the grand product's chunk pass (replaces pm_factor_kernel + gp_chunk):
 // a lane per 16-row chunk walks its rows -- per row the set's num / den factors as
 // pm_factor_kernel forms them, the running num prefix Nloc written over num and the den factor
