@@ -38,7 +38,9 @@ def per_kernel(d, counter):
                 continue
             per_dispatch[r["Dispatch_Id"]] += float(r["Counter_Value"])
             names[r["Dispatch_Id"]] = kind
-            names_of[kind].add(k.split("(")[0])
+            nm = k.replace("(anonymous namespace)::", "")
+            nm = nm[5:] if nm.startswith("void ") else nm
+            names_of[kind].add(nm.split("(")[0])
         for disp, v in per_dispatch.items():
             vals[names[disp]].append(v)
     return {k: sum(v) / len(v) for k, v in vals.items() if v}
