@@ -250,3 +250,53 @@ def test_lookup_two_groups_equal_within_call(engine, trace):
     assert torch.equal(out[16, :4, :usable], out[5, :4, :usable])
     assert torch.equal(out[16, 4, :usable + 1], out[5, 4, :usable + 1])
     assert not torch.equal(out[16, 2, :usable], out[4, 2, :usable])
+
+
+def _spread16(x):
+    x = x.astype(np.uint32)
+    x = (x | (x << 8)) & np.uint32(0x00FF00FF)
+    x = (x | (x << 4)) & np.uint32(0x0F0F0F0F)
+    x = (x | (x << 2)) & np.uint32(0x33333333)
+    x = (x | (x << 1)) & np.uint32(0x55555555)
+    return x
+
+
+def test_lookup_sparse_values_wide_windows(engine):
+    """Dense-cell distributions that stretch the z pass's per-block windows (lk_block_kernel):
+    three distinct values (a block's rows then span thousands of unused table ranks in rank
+    order, the scatter's loops past their first four ranks per thread), two runs of 100,000 and
+    31,065 rows (one rank covers every row of many blocks), and every table value once followed
+    by 65,529 repeats of 65,535 (leftover items of nearly every rank, the leftover windows at
+    their widest). All five columns equal the restatement."""
+    import b2f
+    import lookup as lk
+    import torch
+
+    usable = (1 << 17) - 7
+    rng = np.random.default_rng(41)
+    xs = [rng.choice(np.array([5, 40000, 65535], dtype=np.uint32), usable, p=[0.8, 0.15, 0.05]),
+          np.where(np.arange(usable) < 100000, 7, 60000).astype(np.uint32),
+          np.concatenate([rng.permutation(65536).astype(np.uint32),
+                          np.full(usable - 65536, 65535, dtype=np.uint32)])]
+    rows = (3 * usable + 3) // 4 * 4  # a trace holds a multiple of 4 rows
+    adv = rng.integers(0, 2**32, (10, rows), dtype=np.uint64).astype(np.uint32)
+    x = np.concatenate(xs + [np.zeros(rows - 3 * usable, dtype=np.uint32)])
+    adv[0] = np.where(x < 256, 0, np.where(x < 32768, 1, 2)).astype(np.uint32)
+    adv[1] = x
+    adv[2] = _spread16(x)
+    batch = b2f.DeviceBatch(random_inputs(1, (0,), 1), device="cuda:0", total_rows=rows)
+    batch.advice.copy_(torch.from_numpy(adv.view(np.int32)))
+    theta, beta, gamma = _chal(43)
+    out, bad = batch.lookup_columns(engine, [0, usable, 2 * usable], usable, theta, beta, gamma)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    assert (bad.cpu().numpy().view(np.uint64) == np.uint64(2**64 - 1)).all()
+    for c in range(3):
+        a = adv[:3, c * usable:(c + 1) * usable]
+        ref = lk.columns(a[0], a[1], a[2], usable, theta, beta, gamma)
+        for j in range(5):
+            n = usable + 1 if j == 4 else usable
+            got = _col_ints(out[c, j, :n])
+            want = [v * R256 % lk.P for v in ref[j]]
+            if got != want:
+                i = next(i for i in range(n) if got[i] != want[i])
+                pytest.fail("circuit %d column %d differs first at row %d" % (c, j, i))

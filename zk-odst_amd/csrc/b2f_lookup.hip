@@ -940,7 +940,11 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     // word; the blocks up to the first inclusive one (fi) must all have published, then their
     // values are read and multiplied.
     Fe after = field::one<F>();
+#ifdef B2F_LK_NOWAIT  // diagnostics (wrong z): no look-back, to time what waiting for it costs
+    if (false) {
+#else
     if (b + 1 < nb) {
+#endif
       uint64_t q0 = b + 1;
       while (true) {
         const uint64_t qb = q0 + lane;
