@@ -546,25 +546,13 @@ __device__ __forceinline__ Fe lb_join(const uint64_t (&w)[6]) {
   v.w[6] = (uint32_t)L3; v.w[7] = (uint32_t)(L3 >> 32);
   return v;
 }
-#ifndef B2F_LB_MODE
-#define B2F_LB_MODE 0  // look-back state access (A/B): 0 agent-scope atomic load / store, 1 stores
-                       // as atomic exchanges, 2 loads as memory-side atomic adds of a runtime 0,
-                       // 3 an agent-scope acquire fence before every poll
-#endif
-__device__ __forceinline__ uint64_t lb_load(const uint64_t* p, uint64_t zero) {
-#if B2F_LB_MODE == 2
-  return __hip_atomic_fetch_add(const_cast<uint64_t*>(p), zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-  (void)zero;
+// (exchange stores, memory-side fetch-add loads and an acquire fence per poll were measured
+// neutral or slower, r05i-k: DESIGN.md §5)
+__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
 }
 __device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
-#if B2F_LB_MODE == 1
-  (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
 }
 // lanes 0..5 of the calling wave publish v (the same in every lane) as the aggregate (kind 1) or
 // the inclusive value (kind 2) of block state st, then lane 0 its status
@@ -573,13 +561,13 @@ __device__ __forceinline__ void lb_publish(uint64_t* st, uint32_t lane, const Fe
   if (lane == 0) lb_store(st + 15, kind);
 }
 // the value of kind `kind` of block state st; false while a piece is not yet visible
-__device__ __forceinline__ bool lb_read(const uint64_t* st, uint32_t kind, Fe& v, uint64_t zero) {
+__device__ __forceinline__ bool lb_read(const uint64_t* st, uint32_t kind, Fe& v) {
   uint64_t w[6];
   const uint64_t tag = kind == 2 ? LB_TAG_INC : LB_TAG_AGG;
   bool ok = true;
 #pragma unroll
   for (int i = 0; i < 6; i++) {
-    w[i] = lb_load(st + (kind == 2 ? 8 : 0) + i, zero);
+    w[i] = lb_load(st + (kind == 2 ? 8 : 0) + i);
     ok &= (w[i] & ~LB_M48) == tag;
   }
   v = lb_join(w);
@@ -735,7 +723,7 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     const uint32_t* __restrict__ pos, const uint32_t* __restrict__ dcnt, const uint32_t* __restrict__ lrank,
     const uint32_t* __restrict__ lstart, const uint32_t* __restrict__ blk, const uint32_t* __restrict__ nlr,
     const Fe* __restrict__ NK, const Fe* __restrict__ Dnum, const Fe* __restrict__ bg,
-    uint64_t* __restrict__ lbs, uint32_t* __restrict__ ticket, int* __restrict__ sticky, uint64_t lb_zero) {
+    uint64_t* __restrict__ lbs, uint32_t* __restrict__ ticket, int* __restrict__ sticky) {
   // the row and leftover tables, then (after every wave has read its rows) the lane totals
   static_assert(ZT == 256, "the scans take 4 lane totals per lane");
   constexpr int SMEM = 2 * LB * 4 > 2 * ZT * 32 ? 2 * LB * 4 : 2 * ZT * 32;
@@ -948,10 +936,7 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
       uint64_t q0 = b + 1;
       while (true) {
         const uint64_t qb = q0 + lane;
-#if B2F_LB_MODE == 3
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-        const uint32_t s = qb < nb ? (uint32_t)lb_load(lbs + ((uint64_t)c * nb + qb) * LBS_WORDS + 15, lb_zero) : 2u;
+        const uint32_t s = qb < nb ? (uint32_t)lb_load(lbs + ((uint64_t)c * nb + qb) * LBS_WORDS + 15) : 2u;
         const uint64_t inc = __ballot(s == 2), none = __ballot(s == 0);
         const uint32_t fi = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
         const uint64_t need = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
@@ -972,7 +957,7 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
         }
         Fe val = field::one<F>();
         bool ok = true;
-        if (lane <= fi && qb < nb) ok = lb_read(lbs + ((uint64_t)c * nb + qb) * LBS_WORDS, s, val, lb_zero);
+        if (lane <= fi && qb < nb) ok = lb_read(lbs + ((uint64_t)c * nb + qb) * LBS_WORDS, s, val);
         if (__ballot(!ok)) {
 #ifdef B2F_LK_CLOCK
           if (lane == 0) atomicAdd(&g_lk_clock[18], 1ull);  // status seen before its pieces
@@ -1142,7 +1127,7 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
     uint32_t* ticket = reinterpret_cast<uint32_t*>(k.lbs + LBS_WORDS * nb * g);
     hipLaunchKernelGGL((mont ? lk_zpass_kernel<F, true> : lk_zpass_kernel<F, false>), dim3((uint32_t)(nb * g)),
                        dim3(ZT), 0, s, d_advice, total_rows, d_row_begin, c0, g, usable_rows, nb, k.Tx, k.Ts,
-                       d_out, out_rows, ch, k.pos, k.dcnt, k.lrank, k.lstart, k.blk, k.nlr, k.NK, k.Dnum, k.bg, k.lbs, ticket, sticky, 0ull);
+                       d_out, out_rows, ch, k.pos, k.dcnt, k.lrank, k.lstart, k.blk, k.nlr, k.NK, k.Dnum, k.bg, k.lbs, ticket, sticky);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;
