@@ -15,13 +15,17 @@
 //            workgroups per circuit, a quarter of the bins each), with the row check (tag,
 //            dense, spread) in table (first failing row reported);
 //   scan:    in rank order, run starts pos[r] (exclusive prefix of counts), D[r] (runs up to
-//            and including r) and LP[r] (exclusive prefix of leftover table multiplicities), 16
-//            workgroups per circuit (part totals, then each part's scan);
-//   permute: row p of A' is Ts[r] for the run r holding p (binary search of pos); a run
-//            start gets S'[p] = Ts[r]; the j-th repeated row gets leftover item L - 1 - j
-//            (halo2 hands leftovers out in ascending order, each to the last open repeated
-//            row), found by binary search of LP;
-//   z:       the same pass forms each row's factors num = (A + beta)(S + gamma) and
+//            and including r) and the ranks with leftover table multiplicity, compacted
+//            (lrank, lstart = their first leftover index), 16 workgroups per circuit (part
+//            totals, then each part's scan);
+//   windows: per 1,024-row look-back block, the pos ranks its rows fall in and the compacted
+//            leftover ranks its repeated rows take (lk_block_kernel: LDS-sampled searches,
+//            one thread per block);
+//   z pass:  row p of A' is Ts[r] for the run r holding p; a run start gets S'[p] = Ts[r]; the
+//            j-th repeated row gets leftover item L - 1 - j (halo2 hands leftovers out in
+//            ascending order, each to the last open repeated row). The workgroup scatters its
+//            block's windows into LDS tables by row and by leftover index, so every row reads
+//            its ranks; the same pass forms each row's factors num = (A + beta)(S + gamma) and
 //            den = (A' + beta)(S' + gamma) in registers and writes the grand product z in one
 //            go: the num side's block prefix and D^-1 come from a side-stream pre-pass over the
 //            trace (D = prod num = prod den), the den side's suffix over blocks from a decoupled
