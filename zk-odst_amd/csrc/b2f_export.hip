@@ -202,8 +202,11 @@ hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint6
                             int cu_count, hipStream_t s) {
   // persistent grid: 4 workgroups per CU (halo2 column h -> a_i by kAofH)
   uint64_t tiles = (nrows + XT - 1) / XT;
-  // 122 VGPRs: 4 waves/SIMD (BN254 Montgomery, one cell per lane: 64), every workgroup resident
-  uint64_t want = (uint64_t)cu_count * 4;
+  // persistent workgroups per CU, per form (same-process A/B, profiles/r05g*_export_ab_*.txt:
+  // pasta 3 vs 4 / 2 / 5: 2.47 vs 2.49 / 2.85 / 2.79 ms; BN254 2 vs 4 / 3 / 5: 2.38 vs 2.54 /
+  // 2.50 / 2.53 at 2^25 rows): fewer concurrent tile streams write faster until the cells'
+  // compute is no longer hidden (pasta's is a few instructions, BN254's a 32-bit quotient)
+  uint64_t want = (uint64_t)cu_count * (form == B2F_FP_BN254_MONTGOMERY ? 2 : 3);
   uint32_t gx = (uint32_t)(tiles < want ? tiles : want);
   if (gx == 0) return hipSuccess;
   if (form == B2F_FP_BN254_MONTGOMERY) {
