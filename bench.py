@@ -48,14 +48,14 @@ LOOKUP_MIN_PRODUCTS_PER_ROW = 6  # num, den factors + a grand product's 4: round
 LOOKUP_EVIDENCE = {
     "history_ms_per_call": "1.16 (round 4: permute pass + gp passes) -> 1.29-1.31 (one pass, r05h) -> "
                            "1.12-1.15 (asm product, 4 rows per lane, r05m/n) -> 1.04-1.08 (block windows "
-                           "instead of row searches, r05p)",
-    "files": ["profiles/r05n_lk_clock_zr4.txt", "profiles/r05n_lookup_ab_noprod_zr4.jsonl",
-              "profiles/r05m_lookup_ab_comba_zr4.jsonl"],
+                           "instead of row searches, r05p) -> 1.00-1.02 (window loads up front, 4 waves, r05q/r)",
+    "files": ["profiles/r05r_lk_pmc.txt", "profiles/r05r_lk_clock_w4.txt", "profiles/r05q_lookup_ab_block_w4.jsonl",
+              "profiles/r05w_lookup_ab_nowait_diag.jsonl"],
 }
 PERM_EVIDENCE = {
     "history_ms_per_call": "3.05 (round 3) -> 2.58-2.60 (factors fused with the chunk pass, r04o) -> "
-                           "2.15-2.19 (sigma as keygen, divsteps inversion, r05) -> 2.13 (asm product, r05m)",
-    "files": ["profiles/r04a_pm_pmc.txt", "profiles/r05m_perm_ab_comba.jsonl"],
+                           "2.15-2.19 (sigma as keygen, divsteps inversion, r05) -> 2.07-2.13 (asm product, r05m/s)",
+    "files": ["profiles/r04a_pm_pmc.txt", "profiles/r05r_pm_pmc.txt", "profiles/r05m_perm_ab_comba.jsonl"],
 }
 # 1 in BN254 Fr Montgomery form (R mod r) as four little-endian int64 limbs
 FR_ONE_MONT = [int.from_bytes((0x0e0a77c19a07df2f666ea36f7879462e36fc76959f60cd29ac96341c4ffffffb
