@@ -9,22 +9,22 @@
 // their compressed values:
 //   table pass (once per theta): T[x] = theta^2 tag(x) + theta x + spread(x) for x < 2^16,
 //     sorted by canonical value (one radix sort by the top 64-bit limb, ties -- about 2^-33
-//     likely -- ordered by the lower limbs), giving the rank order x_of_rank[r] and
-//     Ts[r] = T[x_of_rank[r]];
+//     likely -- ordered by the lower limbs), giving the rank order x_of_rank[r];
 //   count:   histogram of the dense cell (a_1) over the circuit's rows (LDS-privatised, four
 //            workgroups per circuit, a quarter of the bins each), with the row check (tag,
 //            dense, spread) in table (first failing row reported);
 //   scan:    in rank order, run starts pos[r] (exclusive prefix of counts), D[r] (runs up to
 //            and including r) and the ranks with leftover table multiplicity, compacted
-//            (lrank, lstart = their first leftover index), 16 workgroups per circuit (part
-//            totals, then each part's scan);
+//            (lrank = their table index, lstart = their first leftover index), 16
+//            workgroups per circuit (part totals, then each part's scan);
 //   windows: per 1,024-row look-back block, the pos ranks its rows fall in and the compacted
 //            leftover ranks its repeated rows take (lk_block_kernel: LDS-sampled searches,
 //            one thread per block);
-//   z pass:  row p of A' is Ts[r] for the run r holding p; a run start gets S'[p] = Ts[r]; the
-//            j-th repeated row gets leftover item L - 1 - j (halo2 hands leftovers out in
-//            ascending order, each to the last open repeated row). The workgroup scatters its
-//            block's windows into LDS tables by row and by leftover index, so every row reads
+//   z pass:  row p of A' is T[x_of_rank[r]] for the run r holding p; a run start gets the
+//            same S'[p]; the j-th repeated row gets leftover item L - 1 - j (halo2 hands
+//            leftovers out in ascending order, each to the last open repeated row). The
+//            workgroup scatters its block's windows into LDS tables by row and by leftover
+//            index (table indices, so every gather reads T alone), so every row reads
 //            its ranks; the same pass forms each row's factors num = (A + beta)(S + gamma) and
 //            den = (A' + beta)(S' + gamma) in registers and writes the grand product z in one
 //            go: the num side's block prefix and D^-1 come from a side-stream pre-pass over the
@@ -121,13 +121,6 @@ __global__ __launch_bounds__(256) void lk_tie_fix_kernel(const uint64_t* __restr
   }
 }
 
-__global__ __launch_bounds__(256) void lk_rank_kernel(const Fe* __restrict__ Tx,
-                                                      const uint32_t* __restrict__ perm,
-                                                      Fe* __restrict__ Ts) {
-  const uint32_t r = blockIdx.x * 256 + threadIdx.x;
-  Ts[r] = Tx[perm[r]];
-}
-
 // ------------------------------------------------------------------ per-circuit passes
 struct Circ {
   uint64_t first;  // first trace row of the circuit
@@ -211,6 +204,7 @@ static_assert(SC_PER == 16, "one search sample per thread");
 // multiplicity, ranks with leftovers
 struct RankRun {
   uint32_t nv[SC_PER];
+  uint32_t xv[SC_PER];  // the table index of each rank
   int iz;
   uint32_t sc, sd, sl, sr;
 };
@@ -226,6 +220,10 @@ __device__ __forceinline__ RankRun rank_run(const uint32_t* __restrict__ perm, c
     R.nv[4 * i + 1] = cnt[x.y];
     R.nv[4 * i + 2] = cnt[x.z];
     R.nv[4 * i + 3] = cnt[x.w];
+    R.xv[4 * i] = x.x;
+    R.xv[4 * i + 1] = x.y;
+    R.xv[4 * i + 2] = x.z;
+    R.xv[4 * i + 3] = x.w;
     R.iz = x.x == 0 ? 4 * i : x.y == 0 ? 4 * i + 1 : x.z == 0 ? 4 * i + 2 : x.w == 0 ? 4 * i + 3 : R.iz;
   }
   R.sc = R.sd = R.sl = R.sr = 0;
@@ -322,7 +320,7 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
       ed += n ? 1u : 0u;
       dq[j] = ed;
       if (m) {
-        LR[er] = r0 + 4 * i + j;
+        LR[er] = R.xv[4 * i + j];  // its table index: the z pass gathers Tx only
         LS[er] = el;
         if (er % SAMP == 0) SP[SAMPLE + er / SAMP] = el;  // an lstart sample
         er++;
@@ -703,7 +701,7 @@ __global__ __launch_bounds__(BK_T) void lk_block_kernel(uint64_t usable, uint64_
 
 // The five columns of one look-back block (LB = 256 ZR rows). Lane t of the workgroup owns rows
 // base + ZR t + j:
-//  1. the runs: A' = Ts[r] for the run r holding p, S' = A' at a run start, else leftover item
+//  1. the runs: A' = T[x_of_rank[r]] for the run r holding p, S' = A' at a run start, else leftover item
 //     n_left - 1 - j for the j-th repeated row (halo2 hands leftovers out in ascending order,
 //     each to the last open repeated row). The workgroup scatters the runs of its pos window and
 //     the leftover ranks of its lstart window (lk_block_kernel) into LDS tables indexed by row
@@ -723,7 +721,7 @@ template <class F, bool MONT>
 __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES))) void lk_zpass_kernel(
     const uint32_t* __restrict__ adv, uint64_t total_rows, const uint64_t* __restrict__ row_begin,
     uint32_t c0, uint32_t g, uint64_t usable, uint64_t nb, const Fe* __restrict__ Tx,
-    const Fe* __restrict__ Ts, uint64_t* __restrict__ out, uint64_t out_rows, Chal ch,
+    const uint32_t* __restrict__ xrank, uint64_t* __restrict__ out, uint64_t out_rows, Chal ch,
     const uint32_t* __restrict__ pos, const uint32_t* __restrict__ dcnt, const uint32_t* __restrict__ lrank,
     const uint32_t* __restrict__ lstart, const uint32_t* __restrict__ blk, const uint32_t* __restrict__ nlr,
     const Fe* __restrict__ NK, const Fe* __restrict__ Dnum, const Fe* __restrict__ bg,
@@ -769,8 +767,9 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
   __syncthreads();
   LKCLK(0);
   uint32_t x[ZR], ra[ZR], rs[ZR];
-  // 1. the runs of the block's rows: every rank of the pos window writes its rows' entries,
-  // every compacted leftover rank of the lstart window its leftover indices' rank
+  // 1. the runs of the block's rows: every rank of the pos window writes its rows' entries (its
+  // table index x_of_rank, so the gathers below read Tx alone: one 2 MiB table in L2, not two),
+  // every compacted leftover rank of the lstart window its leftover indices' table index
   {
     const uint4* bt = reinterpret_cast<const uint4*>(blk + ((uint64_t)c * nb + b) * BLK_WORDS);
     const uint4 w0 = bt[0], w1 = bt[1];
@@ -779,16 +778,17 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     // the first SC_U ranks of each window per thread (windows are ~LB / 2 wide): every load in
     // flight before the first write; wider windows finish in the loops after
     constexpr int SC_U = 4;
-    uint32_t ps0[SC_U], ps1[SC_U], pd[SC_U], ly0[SC_U], ly1[SC_U], lr[SC_U];
+    uint32_t ps0[SC_U], ps1[SC_U], pd[SC_U], px[SC_U], ly0[SC_U], ly1[SC_U], lr[SC_U];
 #pragma unroll
     for (int u = 0; u < SC_U; u++) {
       const uint32_t r = w0.x + t + ZT * u, kk = w1.x + t + ZT * u;
-      ps0[u] = ps1[u] = pd[u] = 0;
+      ps0[u] = ps1[u] = pd[u] = px[u] = 0;
       ly0[u] = ly1[u] = lr[u] = 0;
       if (r <= w0.y) {
         ps0[u] = P[r];
         ps1[u] = r + 1 < (uint32_t)TROWS ? P[r + 1] : us;
         pd[u] = D[r];
+        px[u] = xrank[r];
       }
       if (kk <= w1.y) {
         ly0[u] = LS[kk];
@@ -796,9 +796,9 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
         lr[u] = LR[kk];
       }
     }
-    auto put_run = [&](uint32_t r, uint32_t s0, uint32_t s1, uint32_t dr) {
+    auto put_run = [&](uint32_t xr, uint32_t s0, uint32_t s1, uint32_t dr) {
       const uint32_t lo = s0 > base ? s0 : base, hi = s1 < end ? s1 : end;
-      for (uint32_t q = lo; q < hi; q++) ent[q - base] = q == s0 ? (r | 0x10000u) : (r | ((q - dr - J0) << 17));
+      for (uint32_t q = lo; q < hi; q++) ent[q - base] = q == s0 ? (xr | 0x10000u) : (xr | ((q - dr - J0) << 17));
     };
     auto put_left = [&](uint32_t r, uint32_t y0, uint32_t y1) {
       const uint32_t lo = y0 > ylo ? y0 : ylo, hi = y1 < yhi ? y1 : yhi;
@@ -806,11 +806,11 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     };
 #pragma unroll
     for (int u = 0; u < SC_U; u++) {
-      put_run(w0.x + t + ZT * u, ps0[u], ps1[u], pd[u]);  // empty (s0 = s1 = 0) past the window
+      put_run(px[u], ps0[u], ps1[u], pd[u]);  // empty (s0 = s1 = 0) past the window
       put_left(lr[u], ly0[u], ly1[u]);
     }
     for (uint32_t r = w0.x + t + ZT * SC_U; r <= w0.y; r += ZT)
-      put_run(r, P[r], r + 1 < (uint32_t)TROWS ? P[r + 1] : us, D[r]);
+      put_run(xrank[r], P[r], r + 1 < (uint32_t)TROWS ? P[r + 1] : us, D[r]);
     for (uint32_t kk = w1.x + t + ZT * SC_U; kk <= w1.y; kk += ZT)
       put_left(LR[kk], LS[kk], kk + 1 < nr ? LS[kk + 1] : n_left);
     __syncthreads();
@@ -830,7 +830,7 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
   // 2. the den side: A', S' -> d[j] = den_j, the in-lane suffix sf[j] = prod_{i > j} d_i, dl
   Fe a[ZR], d[ZR], v[ZR];
 #pragma unroll
-  for (int j = 0; j < ZR; j++) v[j] = Ts[ra[j]];
+  for (int j = 0; j < ZR; j++) v[j] = Tx[ra[j]];  // ra, rs: table indices (step 1)
 #pragma unroll
   for (int j = 0; j < ZR; j++) {
     d[j] = field::add<F>(v[j], beta);
@@ -838,7 +838,7 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
   }
   wave_store_zr<true>(o + 2 * out_rows * 4, st, lane, v, r0, us);
 #pragma unroll
-  for (int j = 0; j < ZR; j++) v[j] = Ts[rs[j]];
+  for (int j = 0; j < ZR; j++) v[j] = Tx[rs[j]];
 #pragma unroll
   for (int j = 0; j < ZR; j++) {
     d[j] = p0 + j < us ? LKMUL(d[j], field::add<F>(v[j], gamma)) : field::one<F>();
@@ -1012,7 +1012,6 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
 
 struct Carve {
   Fe* Tx;
-  Fe* Ts;
   uint64_t* key;   // 4 x TROWS canonical limbs
   uint64_t* kout;  // TROWS
   uint32_t* perm;  // TROWS
@@ -1020,7 +1019,7 @@ struct Carve {
   uint32_t* count;  // group x TROWS
   uint32_t* pos;
   uint32_t* dcnt;
-  uint32_t* lrank;   // group x TROWS: the ranks with leftover items, compacted
+  uint32_t* lrank;   // group x TROWS: the table indices of the ranks with leftover items, compacted
   uint32_t* lstart;  // group x TROWS: their first leftover index
   uint32_t* samp;    // group x 2 x SAMPLE: pos and lstart samples
   uint32_t* nlr;     // group: ranks with leftovers
@@ -1056,7 +1055,6 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   };
   const uint64_t nb = n_lb(usable);
   k.Tx = (Fe*)take(sizeof(Fe) * TROWS);
-  k.Ts = (Fe*)take(sizeof(Fe) * TROWS);
   k.key = (uint64_t*)take(8ull * 4 * TROWS);
   k.kout = (uint64_t*)take(8ull * TROWS);
   k.perm = (uint32_t*)take(4ull * TROWS);
@@ -1102,7 +1100,6 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(lk_tie_fix_kernel, tb, dim3(256), 0, s, k.key, k.kout, pa);
-  hipLaunchKernelGGL(lk_rank_kernel, tb, dim3(256), 0, s, k.Tx, pa, k.Ts);
   hipError_t e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s);
   if (e != hipSuccess) return e;
   // Per group: the num side (block products, their prefix, D and D^-1) on the side stream,
@@ -1130,7 +1127,7 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
     if ((e = hipStreamWaitEvent(s, side.join, 0)) != hipSuccess) return e;
     uint32_t* ticket = reinterpret_cast<uint32_t*>(k.lbs + LBS_WORDS * nb * g);
     hipLaunchKernelGGL((mont ? lk_zpass_kernel<F, true> : lk_zpass_kernel<F, false>), dim3((uint32_t)(nb * g)),
-                       dim3(ZT), 0, s, d_advice, total_rows, d_row_begin, c0, g, usable_rows, nb, k.Tx, k.Ts,
+                       dim3(ZT), 0, s, d_advice, total_rows, d_row_begin, c0, g, usable_rows, nb, k.Tx, pa,
                        d_out, out_rows, ch, k.pos, k.dcnt, k.lrank, k.lstart, k.blk, k.nlr, k.NK, k.Dnum, k.bg, k.lbs, ticket, sticky);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
