@@ -19,7 +19,9 @@ LB = 1024
 def _scan(count, usable):
     """pos, dcnt, leftover multiplicity per rank, compacted leftover ranks and their starts."""
     mult = np.ones(TROWS, dtype=np.int64)
-    mult[0] = usable - TROWS + 1  # rank 0 here stands for table row 0 (the rest of the rows)
+    # table row 0's multiplicity (it fills the rows past the table); the kernel gives it to the
+    # rank holding table row 0, here rank 0 -- the window logic does not depend on which rank
+    mult[0] = usable - TROWS + 1
     pos = np.concatenate([[0], np.cumsum(count)[:-1]])
     dcnt = np.cumsum(count > 0)
     m = mult - (count > 0)
