@@ -42,6 +42,8 @@ extern "C" {
 #define B2F_CODE_COPY 17
 #define B2F_CODE_FIXED 18   /* fixed-column cell differs from the keygen structure */
 #define B2F_CODE_LAYOUT 19  /* the row map was rejected: nothing was checked */
+#define B2F_CODE_CHECK 20   /* an internal cross-check failed (B2F_ERR_CHECK, a library defect):
+                               the verdict is not trustworthy, whatever the witness */
 #define B2F_MAX_ROUNDS (1u << 20)
 
 /* Status codes */
@@ -77,7 +79,9 @@ typedef struct {
  * constants at keygen, so a trace checked under a caller-altered fixed column is rejected even
  * when its advice is consistent with the altered selectors.
  * A rejected row map (B2F_ERR_LAYOUT) leaves rows_checked = 0 and first_failure =
- * B2F_CODE_LAYOUT: the report never reads clean for a batch that was not checked. */
+ * B2F_CODE_LAYOUT: the report never reads clean for a batch that was not checked. A failed
+ * internal cross-check (B2F_ERR_CHECK) does the same with B2F_CODE_CHECK, so a library defect
+ * never reads as a witness layout failure. */
 typedef struct {
     uint64_t gate_failures[B2F_NUM_GATES];
     uint64_t lookup_failures;
@@ -334,6 +338,11 @@ B2F_API int b2f_permutation_sigma_dev(b2f_ctx* ctx, const uint64_t* h_offsets, s
 #define B2F_KERNEL_PERM 6   /* permutation-argument prover columns (all passes of one call) */
 #define B2F_KERNEL_PERM_SIGMA 7 /* permutation keygen: the sigma columns (b2f_permutation_sigma_dev) */
 #define B2F_NUM_KERNELS 8
+/* total_ms and count must each hold b2f_num_kernels() entries (= B2F_NUM_KERNELS of the
+ * header the library was built with; it grew from 7 to 8 with B2F_KERNEL_PERM_SIGMA): a caller
+ * built against another header sizes its buffers from the query, so the library never writes
+ * past them. */
+B2F_API int b2f_num_kernels(void);
 B2F_API int b2f_set_timing(b2f_ctx* ctx, int enable);
 B2F_API int b2f_kernel_times(b2f_ctx* ctx, double* total_ms, uint32_t* count);
 

@@ -147,3 +147,17 @@ def test_status_codes_match_the_header():
     assert codes["B2F_ERR_FIELD"] == 7
     assert {v: k for k, v in _lib.STATUS_NAMES.items()} == \
         {("OK" if k == "B2F_OK" else k): v for k, v in codes.items()}
+
+
+def test_kernel_count_and_report_codes_match_the_header():
+    """b2f_kernel_times writes b2f_num_kernels() entries, which is the header's
+    B2F_NUM_KERNELS and the binding's KERNEL_NAMES; the report codes (incl. B2F_CODE_CHECK)
+    are the header's."""
+    import b2f
+    from b2f import _lib
+
+    src = open(ROOT + "/include/b2f.h").read()
+    n = int(re.search(r"#define B2F_NUM_KERNELS\s+(\d+)", src).group(1))
+    assert b2f.load().b2f_num_kernels() == n == len(_lib.KERNEL_NAMES)
+    codes = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define B2F_(CODE_\w+)\s+(\d+)", src)}
+    assert codes == {k: getattr(_lib, k) for k in codes} and codes["CODE_CHECK"] == 20

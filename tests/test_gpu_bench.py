@@ -48,3 +48,26 @@ def test_bench_line_config_is_the_headline_batch(extra, rounds_of):
     fl = line["floors"]
     assert "error" not in fl and fl["reps"] == 2 and fl["interleaved"], fl
     assert line["other_path"]["verdict_clean"]
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_spawns_two_ranks_without_launcher():
+    """`bench.py --gpus 2` with no launcher runs two ranks by itself (here
+    rehearsed on one GPU: B2F_BENCH_REHEARSE=1 puts both ranks on cuda:0 with gloo
+    collectives) and rank 0's one line says n_gpus 2 with the step's collectives timed."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["B2F_BENCH_REHEARSE"] = "1"
+    n = 64
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", str(n),
+           "--steps", "2", "--warmup", "1", "--witness-gather", "32", "--extras-timeout", "120"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 2 * n
+    assert line["config"]["parallelism"].startswith("dp2")
+    assert line["collectives"] is not None and line["collectives"]["ms_per_step"] > 0
+    assert line["witness_gather"] and line["witness_gather"].get("own_rows_in_place"), line["witness_gather"]

@@ -34,3 +34,13 @@ def test_safegcd_inverse_equals_big_integer_inverse(checker, p):
     assert len(out) == len(xs)
     for x, o in zip(xs, out):
         assert int(o, 16) == (pow(x, -1, p) if x else 0), hex(x)
+
+
+def test_safegcd_reports_no_inverse(checker):
+    """inverse() says when the divsteps did not end at a unit (no silent wrong D^-1):
+    a non-invertible x (odd composite moduli) and x = p are reported; x = 0 is the documented 0."""
+    cases = [(15, 5), (15, 3), (21, 14), (P_PALLAS, P_PALLAS), (15, 0), (15, 7)]
+    inp = "".join("%x %x\n" % c for c in cases)
+    out = subprocess.run([checker], input=inp, capture_output=True, text=True, check=True).stdout.split()
+    assert out[:4] == ["nonconverged"] * 4, out
+    assert int(out[4], 16) == 0 and int(out[5], 16) == pow(7, -1, 15)

@@ -24,4 +24,7 @@ B2F_BENCH_REHEARSE=1 timeout -k 10 300 python3 -m torch.distributed.run --nnodes
 B2F_BENCH_REHEARSE=1 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 2 --batch 16384 --config4 32768 \
   --config4-world 2 --gather-cap-gb 1 --steps 3 --warmup 1 > $OUT/rehearse_config4_skip.json 2> $OUT/rehearse_config4_skip.err || exit 6
+# bench.py --gpus 2 with no launcher: it spawns the two ranks itself
+B2F_BENCH_REHEARSE=1 timeout -k 10 300 python3 bench.py --gpus 2 --batch 16384 --steps 3 --warmup 1 \
+  > $OUT/rehearse_spawn_n2.json 2> $OUT/rehearse_spawn_n2.err || exit 7
 echo done

@@ -23,6 +23,7 @@ CODE_LOOKUP = 16
 CODE_COPY = 17
 CODE_FIXED = 18
 CODE_LAYOUT = 19
+CODE_CHECK = 20  # an internal cross-check failed (B2F_ERR_CHECK): a library defect
 MAX_ROUNDS = 1 << 20
 KERNEL_NAMES = ["record", "fill", "eval", "export", "fill_eval", "lookup", "perm",
                 "perm_sigma"]  # B2F_KERNEL_*
@@ -111,6 +112,7 @@ SIGNATURES = [
     ("b2f_sync", I32, [P, P]),
     ("b2f_fill", I32, [P, P, SIZE, P, P, P]),
     ("b2f_eval", I32, [P, P, P, P, SIZE, U64, P]),
+    ("b2f_num_kernels", I32, []),
     ("b2f_set_timing", I32, [P, I32]),
     ("b2f_kernel_times", I32, [P, P, P]),
 ]

@@ -216,7 +216,8 @@ class MockProver:
         what = (SELECTORS[code] if code < 16 else
                 {_lib.CODE_LOOKUP: "lookup", _lib.CODE_COPY: "permutation",
                  _lib.CODE_FIXED: "fixed column (differs from keygen)",
-                 _lib.CODE_LAYOUT: "row map rejected"}.get(code, "code %d" % code))
+                 _lib.CODE_LAYOUT: "row map rejected",
+                 _lib.CODE_CHECK: "internal cross-check failed"}.get(code, "code %d" % code))
         raise VerifyFailure(rep, {"row": int(row), "instance": inst,
                                   "local_row": int(row - off[inst]), "constraint": what})
 

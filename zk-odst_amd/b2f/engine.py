@@ -205,7 +205,10 @@ class Engine:
 
     def kernel_times(self):
         """{kernel: (total_ms, launches)} since set_timing(True) / the previous call."""
-        k = len(_lib.KERNEL_NAMES)
+        k = int(self.lib.b2f_num_kernels())  # the library's count sizes the buffers
+        if k != len(_lib.KERNEL_NAMES):
+            raise _lib.B2FError(_lib.ERR_ARG, "library reports %d kernel kinds, binding knows %d"
+                                % (k, len(_lib.KERNEL_NAMES)))
         tot = (ctypes.c_double * k)()
         cnt = (ctypes.c_uint32 * k)()
         self._check(self.lib.b2f_kernel_times(self.ctx, tot, cnt))

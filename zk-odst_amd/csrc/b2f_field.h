@@ -499,16 +499,17 @@ __device__ Fe inv_kaliski(const Fe& a) {
 // Montgomery-form inverse by Bernstein-Yang divsteps (b2f_safegcd.h) on the integer A = aR:
 // A^-1 = a^-1 R^-1, then one product with R^3 gives a^-1 R. About 20 steps of 30 divsteps and
 // two 2x2-matrix updates of 9-limb vectors against Kaliski's ~270 single-bit steps of 8-word
-// work (inv_kaliski, kept as a cross-check); one lane, a = 0 gives 0.
+// work (inv_kaliski, kept as a cross-check); one lane, a = 0 gives 0. `ok` is cleared when the
+// divsteps did not converge (never for a < p; the callers raise B2F_ERR_CHECK on it).
 template <class F>
-__device__ Fe inv_safegcd(const Fe& a) {
+__device__ Fe inv_safegcd(const Fe& a, bool& ok) {
   uint32_t x[8], pw[8], o[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     x[i] = a.w[i];
     pw[i] = F::P[i];
   }
-  sgcd::inverse(x, pw, o);
+  ok = sgcd::inverse(x, pw, o);
   Fe r;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.w[i] = o[i];

@@ -268,7 +268,9 @@ __global__ __launch_bounds__(64) void gp_inv(Fe* __restrict__ dt, int* __restric
 #elif defined(B2F_INV_KALISKI)  // diagnostics: Kaliski's almost-inverse (round 4's)
   dt[c] = field::inv_kaliski<F>(D);
 #else
-  dt[c] = field::inv_safegcd<F>(D);
+  bool ok;
+  dt[c] = field::inv_safegcd<F>(D, ok);
+  if (sticky && !ok) atomicOr(sticky, 1 << B2F_ERR_CHECK);
 #endif
 }
 

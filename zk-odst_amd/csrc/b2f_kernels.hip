@@ -97,7 +97,8 @@ __device__ __forceinline__ void raise_error(int* status, int* sticky, b2f_eval_r
   atomicOr(sticky, 1 << code);
   if (rep) {
     rep->rows_checked = 0;
-    atomicMin((unsigned long long*)&rep->first_failure, (unsigned long long)B2F_CODE_LAYOUT);
+    const unsigned long long why = code == B2F_ERR_CHECK ? B2F_CODE_CHECK : B2F_CODE_LAYOUT;
+    atomicMin((unsigned long long*)&rep->first_failure, why);
   }
 }
 
@@ -1168,6 +1169,8 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
 
 B2F_API const char* b2f_last_error(const b2f_ctx* ctx) { return ctx ? ctx->err : "null context"; }
 
+B2F_API int b2f_num_kernels(void) { return B2F_NUM_KERNELS; }
+
 B2F_API int b2f_set_timing(b2f_ctx* ctx, int enable) {
   if (!ctx) return B2F_ERR_ARG;
   ctx->timing = enable ? 1 : 0;
@@ -1192,6 +1195,14 @@ B2F_API int b2f_kernel_times(b2f_ctx* ctx, double* total_ms, uint32_t* count) {
 }  // extern "C"
 
 namespace {
+// Entries of the fused launch's segment list. Diagnostics build only: B2F_DIAG_SEG_CAP caps it
+// below what the batch needs, so a test sees the overflow raise B2F_ERR_CHECK.
+uint64_t seg_entries(const b2f_ctx* ctx) {
+  const uint64_t cap = ctx->seg_cap ? ctx->seg_cap - 1 : 0;
+  const int lim = diag_mode("B2F_DIAG_SEG_CAP", -1);
+  return lim >= 0 && (uint64_t)lim < cap ? (uint64_t)lim : cap;
+}
+
 // Argument checks, record scratch and the record kernel: the first part of b2f_fill_dev and
 // b2f_fill_eval_dev.
 int fill_prologue(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const uint64_t* d_offsets,
@@ -1243,7 +1254,7 @@ int fill_prologue(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const uint64_t*
   }
   hipLaunchKernelGGL(record_kernel, dim3((uint32_t)((4ull * nn + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, d_in, nn,
                      d_offsets, total_rows, ctx->rec_cap, ctx->d_rec, d_h_out, ctx->d_status,
-                     ctx->d_status + 2, d_report, lite, seg, lite ? ctx->seg_cap - 1 : 0);
+                     ctx->d_status + 2, d_report, lite, seg, lite ? seg_entries(ctx) : 0);
   HIPCHK(ctx, hipGetLastError());
   timed_end(ctx, tk, s);
   return B2F_OK;
@@ -1334,7 +1345,7 @@ B2F_API int b2f_fill_eval_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n,
   HIPCHK(ctx, launch_fill_eval(d_in, (uint32_t)n, d_offsets, total_rows, ctx->d_rec, d_advice,
                                d_fixed, ctx->d_fz, tiles, d_report, ctx->d_status,
                                ctx->inj_row, ctx->inj_col, ctx->inj_mask, fmode,
-                               ctx->cu_count, ctx->d_clock, ctx->d_seg, ctx->seg_cap ? ctx->seg_cap - 1 : 0, s));
+                               ctx->cu_count, ctx->d_clock, ctx->d_seg, seg_entries(ctx), s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }

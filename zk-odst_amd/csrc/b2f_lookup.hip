@@ -408,6 +408,13 @@ __device__ unsigned long long g_lk_clock[24];
   } while (0)
 #endif
 
+#ifdef B2F_DIAG
+// Diagnostics build only (libb2f_diag.so, B2F_DIAG_LK_CORRUPT=1 at the call): row 0's A' of every
+// circuit is read from the next table row, i.e. one wrong permuted cell, so the den-product
+// cross-check must raise B2F_ERR_CHECK (a test that sees it fire).
+__device__ uint32_t g_lk_corrupt;
+#endif
+
 __device__ __forceinline__ Fe shfl_fe(const Fe& v, int src) {
   Fe r;
 #pragma unroll
@@ -504,7 +511,9 @@ __global__ __launch_bounds__(NS_T) void lk_nscan_kernel(uint64_t nb, const Fe* _
     Dnum[c] = D;
     __builtin_amdgcn_s_setprio(3);
     if (sticky && field::is_zero(D)) atomicOr(sticky, 1 << B2F_ERR_FIELD);
-    sdinv = field::inv_safegcd<F>(D);
+    bool ok;
+    sdinv = field::inv_safegcd<F>(D, ok);
+    if (sticky && !ok) atomicOr(sticky, 1 << B2F_ERR_CHECK);
     __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
@@ -827,6 +836,9 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     }
   }
   LKCLK(1);
+#ifdef B2F_DIAG
+  if (g_lk_corrupt && b == 0 && t == 0) ra[0] = (ra[0] + 1u) & 0xffffu;
+#endif
   // 2. the den side: A', S' -> d[j] = den_j, the in-lane suffix sf[j] = prod_{i > j} d_i, dl
   Fe a[ZR], d[ZR], v[ZR];
 #pragma unroll
@@ -1088,6 +1100,13 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
                       uint32_t group, int* sticky, const gp::Side& side, hipStream_t s) {
   Carve k = carve(scratch, group, usable_rows);
   const uint64_t nb = n_lb(usable_rows);
+#ifdef B2F_DIAG
+  {
+    const uint32_t corrupt = getenv("B2F_DIAG_LK_CORRUPT") ? 1u : 0u;
+    hipError_t e0 = hipMemcpyToSymbol(HIP_SYMBOL(g_lk_corrupt), &corrupt, sizeof(corrupt));
+    if (e0 != hipSuccess) return e0;
+  }
+#endif
   const dim3 tb(TROWS / 256);
   hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm, k.bg);
   // one radix sort by the top limb of the canonical value (< 2^63: both moduli are < 2^255),

@@ -37,13 +37,7 @@ struct T2 {
 };
 constexpr uint32_t M30 = 0x3fffffffu;
 
-__host__ __device__ inline int ctz32(uint32_t x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_ctz(x);
-#else
-  return __builtin_ctz(x);
-#endif
-}
+__host__ __device__ inline int ctz32(uint32_t x) { return __builtin_ctz(x); }
 
 // 8 words little-endian (< 2^256) <-> signed-30 limbs (all limbs in [0, 2^30) but the top)
 __host__ __device__ inline S30 from_words(const uint32_t (&w)[8]) {
@@ -182,8 +176,11 @@ __host__ __device__ inline void normalize(S30& r, int32_t sign, const S30& p) {
   }
 }
 
-// x^-1 mod p (x < p, as 8 words; x = 0 gives 0), p odd < 2^256 as 8 words
-__host__ __device__ inline void inverse(const uint32_t (&x)[8], const uint32_t (&pw)[8], uint32_t (&out)[8]) {
+// x^-1 mod p (x < p, as 8 words; x = 0 gives 0), p odd < 2^256 as 8 words. Returns whether the
+// divsteps converged -- g reached 0 with f = +-1 (gcd 1; for x = 0, f = +-p and out = 0) --
+// within the 40 outer steps: ~25 suffice for 256 bits, so false means an input outside the
+// contract (x >= p, a modulus change) and `out` is not an inverse.
+__host__ __device__ inline bool inverse(const uint32_t (&x)[8], const uint32_t (&pw)[8], uint32_t (&out)[8]) {
   const S30 p = from_words(pw);
   uint32_t pinv = pw[0];  // p^-1 mod 2^32 by Newton (p odd)
   for (int i = 0; i < 5; i++) pinv *= 2u - pw[0] * pinv;
@@ -191,7 +188,8 @@ __host__ __device__ inline void inverse(const uint32_t (&x)[8], const uint32_t (
   S30 d = {{0, 0, 0, 0, 0, 0, 0, 0, 0}}, e = {{1, 0, 0, 0, 0, 0, 0, 0, 0}};
   S30 f = p, g = from_words(x);
   int32_t eta = -1;
-  for (int it = 0; it < 40; it++) {  // 25 steps suffice for 256 bits (<= 750 divsteps)
+  bool done = false;
+  for (int it = 0; it < 40 && !done; it++) {  // 25 steps suffice for 256 bits (<= 750 divsteps)
     T2 t;
     eta = divsteps_30(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
     update_de(d, e, t, p, pinv30);
@@ -199,10 +197,21 @@ __host__ __device__ inline void inverse(const uint32_t (&x)[8], const uint32_t (
     int32_t nz = 0;
 #pragma unroll
     for (int i = 0; i < 9; i++) nz |= g.v[i];
-    if (nz == 0) break;
+    done = nz == 0;
   }
+  // f = +-1 (x invertible; -1 is limbs 0..7 = 2^30 - 1, limb 8 = -1) or +-p (x = 0, d stays 0)
+  int32_t one = f.v[0] == 1 && f.v[8] == 0, mone = f.v[0] == (int32_t)M30 && f.v[8] == -1, zx = 1;
+#pragma unroll
+  for (int i = 1; i < 8; i++) {
+    one &= f.v[i] == 0;
+    mone &= f.v[i] == (int32_t)M30;
+  }
+  const int32_t unit = one | mone;
+#pragma unroll
+  for (int i = 0; i < 9; i++) zx &= d.v[i] == 0;
   normalize(d, f.v[8], p);
   to_words(d, out);
+  return done && (unit || zx);
 }
 
 }  // namespace sgcd
