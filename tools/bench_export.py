@@ -1,7 +1,9 @@
 """Fp export throughput A/B (b2f_export_fp_dev): 2^25 rows of a filled 12-round trace exported
 in pasta Montgomery and BN254 Montgomery form by each library given, interleaved rep by rep in
 one process (HIP-event kernel time). Diagnostic only:
-    python tools/bench_export.py [--libs a.so,b.so] [--rows N]"""
+    python tools/bench_export.py [--libs a.so,b.so] [--rows N] [--pads 0,256]
+--pads: output column strides of rows + pad (out_rows; the bench's [10, 2^25, 4] tensor puts the
+columns exactly 2^30 bytes apart)."""
 import argparse
 import json
 import os
@@ -17,6 +19,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1 << 25)
     ap.add_argument("--instances", type=int, default=1 << 13)
     ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--pads", default="0", help="comma-separated out_rows - rows values")
     args = ap.parse_args()
     import torch
 
@@ -31,20 +34,22 @@ def main():
     nr = min(args.rows, batch.total_rows)
     engines = [("product", prod)] + [(os.path.basename(p), b2f.Engine(0, lib_path=os.path.join(ROOT, p)))
                                      for p in args.libs.split(",") if p]
-    out = torch.empty((10, nr, 4), dtype=torch.int64, device=batch.advice.device)
+    pads = [int(p) for p in args.pads.split(",")]
+    outs = {p: torch.empty((10, nr + p, 4), dtype=torch.int64, device=batch.advice.device) for p in pads}
     res = {}
     for rep in range(args.reps):
         for name, eng in engines:
-            for form in (b2f.FP_MONTGOMERY, b2f.FP_BN254_MONTGOMERY):
-                eng.set_timing(True)
-                batch.export_fp(eng, nrows=nr, out=out, form=form, stream=s)
-                eng.sync(s)
-                tot, cnt = eng.kernel_times()["export"]
-                res.setdefault((name, form), []).append(tot / max(cnt, 1))
+            for p in pads:
+                for form in (b2f.FP_MONTGOMERY, b2f.FP_BN254_MONTGOMERY):
+                    eng.set_timing(True)
+                    batch.export_fp(eng, nrows=nr, out=outs[p], form=form, stream=s)
+                    eng.sync(s)
+                    tot, cnt = eng.kernel_times()["export"]
+                    res.setdefault((name, p, form), []).append(tot / max(cnt, 1))
     nbytes = nr * 10 * 36
-    for (name, form), v in res.items():
+    for (name, p, form), v in res.items():
         best = min(v[1:]) if len(v) > 1 else v[0]
-        print(json.dumps({"lib": name, "form": form, "ms": round(best, 4),
+        print(json.dumps({"lib": name, "pad_rows": p, "form": form, "ms": round(best, 4),
                           "GBs": round(nbytes / best / 1e6, 1), "all": [round(x, 3) for x in v]}))
 
 

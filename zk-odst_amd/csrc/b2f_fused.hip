@@ -2003,15 +2003,28 @@ edge_redo_kernel(const b2f_input* __restrict__ in, const uint64_t* __restrict__ 
 // assumes) sets `dirty`, and the exact eval kernel then evaluates the whole trace and writes the
 // report (MockProver's counters and first failing row).
 
-// half-round tile descriptors from the row map alone (the eval has no input records)
-__global__ void eval_desc_kernel(const uint64_t* __restrict__ off, uint32_t n, TileDesc* __restrict__ desc,
-                                 const int* __restrict__ status) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || *status) return;
-  const uint64_t o = off[i];
-  const uint32_t rounds = (uint32_t)((off[i + 1] - o - FIXED_ROWS) / ROUND_ROWS);
-  const uint64_t st = 2 * ((o - (uint64_t)FIXED_ROWS * i) / ROUND_ROWS) + i;
-  for (uint32_t j = 1; j <= 2 * rounds; j++) desc[st - i + j - 1].v = make_uint4(i, j, rounds, (uint32_t)st);
+// half-round tile descriptors from the row map alone (the eval has no input records): a thread
+// per tile T finds its instance -- the last i with 2 R_i <= T, R_i = (off_i - 228 i) / 416 the
+// rounds before instance i (instances without rounds own no tile) -- by a binary search over the
+// row map, so the descriptors go out as whole lines (round 5: a thread per instance wrote its
+// 2 rounds descriptors 384 bytes apart from its neighbours', 73 us per 2^18 x 12 call)
+__global__ void __launch_bounds__(256) eval_desc_kernel(const uint64_t* __restrict__ off, uint32_t n,
+                                                        TileDesc* __restrict__ desc,
+                                                        const int* __restrict__ status) {
+  const uint64_t T = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (*status) return;
+  auto R = [&](uint32_t i) { return (off[i] - (uint64_t)FIXED_ROWS * i) / ROUND_ROWS; };
+  const uint64_t tiles = 2 * R(n);
+  if (T >= tiles) return;
+  uint32_t lo = 0, hi = n;  // 2 R_lo <= T < 2 R_hi
+  while (hi - lo > 1) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (2 * R(mid) <= T) lo = mid;
+    else hi = mid;
+  }
+  const uint64_t r0 = R(lo);
+  const uint32_t rounds = (uint32_t)(R(lo + 1) - r0);
+  desc[T].v = make_uint4(lo, (uint32_t)(T - 2 * r0) + 1, rounds, (uint32_t)(2 * r0 + lo));
 }
 
 // The loads of one eval tile (see eval_hr_kernel): the tile's 11 cells of the lane's quad, the
@@ -2052,124 +2065,22 @@ __device__ __forceinline__ EvCells ev_load(const hr2::HCtx& c, uint32_t lane, ui
   return v;
 }
 
-#ifndef B2F_EVAL_WAVES_HR
-#define B2F_EVAL_WAVES_HR 3  // waves per SIMD of the eval fast pass (the prefetched tile's registers)
-#endif
-#ifndef B2F_EVAL_HR_BAND
-#define B2F_EVAL_HR_BAND 24  // consecutive half-round tiles per wave visit (1: one tile, every limb table gathered)
-#endif
-constexpr uint32_t EV_BAND = B2F_EVAL_HR_BAND;
-// LDS byte addresses (dense | spread << 16) of limb k = lane % 4 of state word lane / 4 in the staged
-// PREVIOUS half-round tile, for that tile's parity `par` (0: column G's, 1: diagonal G's): where the
-// limb table of a tile comes from when the wave has just checked the instance's previous half-round
-__device__ __forceinline__ uint32_t carry_addr(uint32_t lane, uint32_t Sb, uint32_t par) {
-  const Canon cs = canon_state(lane >> 2, 1 + par);  // rows of half-round par of round 0
-  const uint32_t ri = cs.row(lane & 3u) - INIT_ROWS - 208 * par;
-  return (Sb + 4 * (cs.dcol * HSTR + ri)) | ((Sb + 4 * (cs.scol * HSTR + ri)) << 16);
-}
+// The eval's edge tiles (one per instance: its init and final regions; then the zero rows as
+// PAD_Q-quad tiles) dealt from tile t0 with stride W, in the wave's region S: the fast checks of
+// the fused edge launch on the loaded trace. Returns whether any tile was flagged.
 template <int MODE>
-__global__ void __launch_bounds__(FW * WAVES, B2F_EVAL_WAVES_HR)
-eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fixed, uint32_t n,
-               const uint64_t* __restrict__ off, uint64_t total_rows, const TileDesc* __restrict__ desc,
-               uint32_t* __restrict__ dirty, const int* __restrict__ status) {
-  using namespace hr2;
-  __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS];
-  const int tid = threadIdx.x;
-  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
-  if (tid < 40) L[H_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
-  __syncthreads();
-  if (*status) return;  // a rejected row map: the eval kernel reports it
-  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + H_SG);
-  uint32_t* S = L + H_WAVE + wv * HW_WORDS + HPRE;
-  const Lane K = make_lane(lane, lds_byte(S));
-  const bool qlane = lane < HR_Q;
-  const uint32_t lq = qlane ? lane : 0;
-  const uint32_t m32 = lane & 31u, mg = m32 >> 3, mwh = (m32 >> 2) & 1u, mk = m32 & 3u;
-  const uint64_t used_rows = off[n];
-  const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
-  const uint64_t W = (uint64_t)gridDim.x * WAVES;
-  // bands of EV_BAND consecutive tiles per wave visit, dealt like single tiles (first_tile)
-  uint64_t b = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
-  uint64_t t = b * EV_BAND;
-  uint32_t j = 0;
-  const uint32_t cA0 = carry_addr(lane, lds_byte(S), 0), cA1 = carry_addr(lane, lds_byte(S), 1);
-  auto raw_desc = [&](uint64_t tt) -> uint4 { return desc[tt].v; };
-  // per tile: its cells (lane = quad), its limb-table entry (the canonical dense / spread cell of
-  // state word lane / 4, limb lane % 4, as the half-round starts: gathered at a band's first tile
-  // and at an instance's first half-round, otherwise read from the previous tile's staging) and its
-  // message-copy source (message word SIGMA[..] limb, a_1 of its INW block), loaded one tile ahead
-  HCtx c = hctx(raw_desc(t < n_hr ? t : 0));
-  EvCells cur = ev_load(c, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg, true);
-  while (t < n_hr) {
-    uint64_t tn = t + 1, bn = b;
-    uint32_t jn = j + 1;
-    if (jn == EV_BAND || tn >= n_hr) {
-      bn = b + W;
-      tn = bn * EV_BAND;
-      jn = 0;
-    }
-    const HCtx cn = hctx(raw_desc(tn < n_hr ? tn : 0));
-    const EvCells nxt = ev_load(cn, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg, jn == 0 || cn.hr == 0);
-    uint32_t ltd = cur.d, lts = cur.sp;
-    if (j != 0 && c.hr != 0) {  // the staging holds half-round hr - 1 of this instance
-      const uint32_t a = ((c.hr - 1) & 1u) ? cA1 : cA0;
-      ltd = ld32(a & 0xffffu);
-      lts = ld32(a >> 16);
-    }
-    asm volatile("" ::: "memory");  // read before the tile's cells overwrite the staging
-    if (qlane) {
-      uint4* q = reinterpret_cast<uint4*>(S + 4 * lane);
-      q[0 * HSTR / 4] = cur.c0;
-      q[1 * HSTR / 4] = cur.c1;
-      q[2 * HSTR / 4] = cur.c2;
-      q[3 * HSTR / 4] = cur.c3;
-      q[4 * HSTR / 4] = cur.c4;
-      q[5 * HSTR / 4] = cur.c5;
-      q[6 * HSTR / 4] = cur.c6;
-      q[7 * HSTR / 4] = cur.c7;
-      q[8 * HSTR / 4] = cur.c8;
-      q[9 * HSTR / 4] = cur.c9;
-      q[10 * HSTR / 4] = cur.c10;
-    }
-    S[H_LT + lane] = ltd;
-    S[H_LT + 64 + lane] = lts;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t mc = cur.mc;
-    const uint32_t acc = hr_fast_checks<MODE>(K, c.hr, [&] { return mc; });
-    if (__builtin_amdgcn_ballot_w64(acc != 0) && lane == 0) *dirty = 1u;
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    c = cn;
-    cur = nxt;
-    t = tn;
-    j = jn;
-    b = bn;
-  }
-}
-
-template <int MODE>
-__global__ void __launch_bounds__(FW * WAVES, 3)
-eval_edge_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fixed, uint32_t n,
-                 const uint64_t* __restrict__ off, uint64_t total_rows, uint32_t* __restrict__ dirty,
-                 const int* __restrict__ status) {
+__device__ __forceinline__ bool eval_edge_walk(uint32_t* S, uint32_t lane, uint64_t t0, uint64_t W,
+                                               const uint64_t* IV, const uint32_t* __restrict__ adv,
+                                               const uint32_t* __restrict__ fixed, uint32_t n,
+                                               const uint64_t* __restrict__ off, uint64_t total_rows) {
   using namespace hr2;
   using namespace edge2;
-  __shared__ __attribute__((aligned(16))) uint32_t L[E_WORDS];
-  const int tid = threadIdx.x;
-  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
-  if (tid < 16) L[E_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
-  __syncthreads();
-  if (*status) return;
-  const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + E_IV);
-  uint32_t* S = L + E_WAVE + wv * EW_WORDS;
   const ELane E = make_elane(lane, lds_byte(S), IV);
   const uint64_t used_rows = off[n];
   const uint64_t n_pad = ((total_rows - used_rows) / 4 + PAD_Q - 1) / PAD_Q;
   const uint64_t t_all = (uint64_t)n + n_pad;
-  const uint64_t W = (uint64_t)gridDim.x * WAVES;
   bool bad = false;
-  for (uint64_t t = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x); t < t_all; t += W) {
+  for (uint64_t t = t0; t < t_all; t += W) {
     if (t < n) {
       const uint32_t i = (uint32_t)t;
       const uint64_t o = off[i];
@@ -2211,6 +2122,161 @@ eval_edge_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ 
       }
     }
   }
+  return bad;
+}
+
+#ifndef B2F_EVAL_WAVES_HR
+#define B2F_EVAL_WAVES_HR 3  // waves per SIMD of the eval fast pass (the prefetched tile's registers)
+#endif
+#ifndef B2F_EVAL_ILV
+#define B2F_EVAL_ILV 0
+#endif
+#ifndef B2F_EVAL_HR_BAND
+#define B2F_EVAL_HR_BAND 24  // consecutive half-round tiles per wave visit (1: one tile, every limb table gathered)
+#endif
+constexpr uint32_t EV_BAND = B2F_EVAL_HR_BAND;
+// LDS byte addresses (dense | spread << 16) of limb k = lane % 4 of state word lane / 4 in the staged
+// PREVIOUS half-round tile, for that tile's parity `par` (0: column G's, 1: diagonal G's): where the
+// limb table of a tile comes from when the wave has just checked the instance's previous half-round
+__device__ __forceinline__ uint32_t carry_addr(uint32_t lane, uint32_t Sb, uint32_t par) {
+  const Canon cs = canon_state(lane >> 2, 1 + par);  // rows of half-round par of round 0
+  const uint32_t ri = cs.row(lane & 3u) - INIT_ROWS - 208 * par;
+  return (Sb + 4 * (cs.dcol * HSTR + ri)) | ((Sb + 4 * (cs.scol * HSTR + ri)) << 16);
+}
+template <int MODE>
+__global__ void __launch_bounds__(FW * WAVES, B2F_EVAL_WAVES_HR)
+eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fixed, uint32_t n,
+               const uint64_t* __restrict__ off, uint64_t total_rows, const TileDesc* __restrict__ desc,
+               uint32_t* __restrict__ dirty, const int* __restrict__ status) {
+  using namespace hr2;
+  __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS];
+  const int tid = threadIdx.x;
+  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
+  if (tid < 40) L[H_SG + tid] = reinterpret_cast<const uint32_t*>(c_sigma)[tid];
+  if (tid < 16) L[H_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
+  __syncthreads();
+  if (*status) return;  // a rejected row map: the eval kernel reports it
+  const uint8_t* Sg = reinterpret_cast<const uint8_t*>(L + H_SG);
+  uint32_t* S = L + H_WAVE + wv * HW_WORDS + HPRE;
+  const Lane K = make_lane(lane, lds_byte(S));
+  const bool qlane = lane < HR_Q;
+  const uint32_t lq = qlane ? lane : 0;
+  const uint32_t m32 = lane & 31u, mg = m32 >> 3, mwh = (m32 >> 2) & 1u, mk = m32 & 3u;
+  const uint64_t used_rows = off[n];
+  const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
+  const uint64_t W = (uint64_t)gridDim.x * WAVES;
+#if B2F_EVAL_ILV
+  // (variant) a workgroup's 4 waves walk ONE band of 4 EV_BAND consecutive tiles interleaved --
+  // wave w takes tiles 4 m + w -- so the workgroup reads 4 adjacent tiles (3.3 KB per column) at a
+  // time; every limb table is gathered (the previous tile is another wave's)
+  const uint64_t WB = gridDim.x, EVB = (uint64_t)EV_BAND * WAVES;
+  uint64_t b = first_tile(blockIdx.x, 0, gridDim.x) / WAVES;
+  uint64_t t = b * EVB + wv;
+  uint32_t j = 0;
+#else
+  // bands of EV_BAND consecutive tiles per wave visit, dealt like single tiles (first_tile)
+  uint64_t b = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
+  uint64_t t = b * EV_BAND;
+  uint32_t j = 0;
+#endif
+  const uint32_t cA0 = carry_addr(lane, lds_byte(S), 0), cA1 = carry_addr(lane, lds_byte(S), 1);
+  auto raw_desc = [&](uint64_t tt) -> uint4 { return desc[tt].v; };
+  // per tile: its cells (lane = quad), its limb-table entry (the canonical dense / spread cell of
+  // state word lane / 4, limb lane % 4, as the half-round starts: gathered at a band's first tile
+  // and at an instance's first half-round, otherwise read from the previous tile's staging) and its
+  // message-copy source (message word SIGMA[..] limb, a_1 of its INW block), loaded one tile ahead
+  HCtx c = hctx(raw_desc(t < n_hr ? t : 0));
+  EvCells cur = ev_load(c, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg, true);
+  while (t < n_hr) {
+#if B2F_EVAL_ILV
+    uint64_t tn = t + WAVES, bn = b;
+    uint32_t jn = j + 1;
+    if (jn == EV_BAND || tn >= n_hr) {
+      bn = b + WB;
+      tn = bn * EVB + wv;
+      jn = 0;
+    }
+    const HCtx cn = hctx(raw_desc(tn < n_hr ? tn : 0));
+    const EvCells nxt = ev_load(cn, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg, true);
+    uint32_t ltd = cur.d, lts = cur.sp;
+    if (false) {
+#else
+    uint64_t tn = t + 1, bn = b;
+    uint32_t jn = j + 1;
+    if (jn == EV_BAND || tn >= n_hr) {
+      bn = b + W;
+      tn = bn * EV_BAND;
+      jn = 0;
+    }
+    const HCtx cn = hctx(raw_desc(tn < n_hr ? tn : 0));
+    const EvCells nxt = ev_load(cn, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg, jn == 0 || cn.hr == 0);
+    uint32_t ltd = cur.d, lts = cur.sp;
+    if (j != 0 && c.hr != 0) {  // the staging holds half-round hr - 1 of this instance
+#endif
+      const uint32_t a = ((c.hr - 1) & 1u) ? cA1 : cA0;
+      ltd = ld32(a & 0xffffu);
+      lts = ld32(a >> 16);
+    }
+    asm volatile("" ::: "memory");  // read before the tile's cells overwrite the staging
+    if (qlane) {
+      uint4* q = reinterpret_cast<uint4*>(S + 4 * lane);
+      q[0 * HSTR / 4] = cur.c0;
+      q[1 * HSTR / 4] = cur.c1;
+      q[2 * HSTR / 4] = cur.c2;
+      q[3 * HSTR / 4] = cur.c3;
+      q[4 * HSTR / 4] = cur.c4;
+      q[5 * HSTR / 4] = cur.c5;
+      q[6 * HSTR / 4] = cur.c6;
+      q[7 * HSTR / 4] = cur.c7;
+      q[8 * HSTR / 4] = cur.c8;
+      q[9 * HSTR / 4] = cur.c9;
+      q[10 * HSTR / 4] = cur.c10;
+    }
+    S[H_LT + lane] = ltd;
+    S[H_LT + 64 + lane] = lts;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t mc = cur.mc;
+    const uint32_t acc = hr_fast_checks<MODE>(K, c.hr, [&] { return mc; });
+    if (__builtin_amdgcn_ballot_w64(acc != 0) && lane == 0) *dirty = 1u;
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    c = cn;
+    cur = nxt;
+    t = tn;
+    j = jn;
+    b = bn;
+  }
+  // then the edge tiles, in the wave's whole region (as the fused launch
+  // does since round 4, the edge work fills this launch's tail instead of a launch after it)
+  if (!B2F_EDGE_SEPARATE) {
+    const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + H_IV);
+    const bool bad = eval_edge_walk<MODE>(L + H_WAVE + wv * HW_WORDS, lane,
+                                          first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x),
+                                          W, IV, adv, fixed, n, off, total_rows);
+    if (__builtin_amdgcn_ballot_w64(bad) && lane == 0) *dirty = 1u;
+  }
+}
+
+// The edge walk as its own launch after the half-round pass (diagnostics: B2F_EDGE_SEPARATE = 1
+// builds this form; the product runs the walk as eval_hr_kernel's last phase)
+template <int MODE>
+__global__ void __launch_bounds__(FW * WAVES, 3)
+eval_edge_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fixed, uint32_t n,
+                 const uint64_t* __restrict__ off, uint64_t total_rows, uint32_t* __restrict__ dirty,
+                 const int* __restrict__ status) {
+  using namespace hr2;
+  using namespace edge2;
+  __shared__ __attribute__((aligned(16))) uint32_t L[E_WORDS];
+  const int tid = threadIdx.x;
+  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
+  if (tid < 16) L[E_IV + tid] = reinterpret_cast<const uint32_t*>(c_iv)[tid];
+  __syncthreads();
+  if (*status) return;
+  const uint64_t* IV = reinterpret_cast<const uint64_t*>(L + E_IV);
+  const bool bad = eval_edge_walk<MODE>(L + E_WAVE + wv * EW_WORDS, lane,
+                                        first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x),
+                                        (uint64_t)gridDim.x * WAVES, IV, adv, fixed, n, off, total_rows);
   if (__builtin_amdgcn_ballot_w64(bad) && lane == 0) *dirty = 1u;
 }
 
@@ -2262,7 +2328,8 @@ hipError_t launch_eval_fast(const uint32_t* d_adv, const uint32_t* d_fixed, cons
   uint32_t* dirty = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + fused_scratch_bytes(tiles) - 8);
   hipError_t e = hipMemsetAsync(dirty, 0, 4, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(eval_desc_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d_off, n, desc, d_status);
+  // tiles (an upper bound on the half-round tiles) >= 2 sum(rounds): every tile has its thread
+  hipLaunchKernelGGL(eval_desc_kernel, dim3((uint32_t)((tiles + 255) / 256)), dim3(256), 0, s, d_off, n, desc, d_status);
   static int per_cu[2] = {0, 0};
   if (!per_cu[0]) {
     int nb = 0;
@@ -2289,8 +2356,9 @@ hipError_t launch_eval_fast(const uint32_t* d_adv, const uint32_t* d_fixed, cons
   case M:                                                                                          \
     hipLaunchKernelGGL(eval_hr_kernel<M>, dim3(cu_count * ev_per_cu), dim3(FW * WAVES), 0, s, d_adv, d_fixed, n, \
                        d_off, total_rows, desc, dirty, d_status);                                  \
-    hipLaunchKernelGGL(eval_edge_kernel<M>, dim3(grid_e), dim3(FW * WAVES), 0, s, d_adv, d_fixed, n, d_off, \
-                       total_rows, dirty, d_status);                                               \
+    if (B2F_EDGE_SEPARATE)                                                                         \
+      hipLaunchKernelGGL(eval_edge_kernel<M>, dim3(grid_e), dim3(FW * WAVES), 0, s, d_adv, d_fixed, n, d_off, \
+                         total_rows, dirty, d_status);                                             \
     break;
 #ifdef B2F_DIAG
     B2F_EVFAST(0) B2F_EVFAST(1) B2F_EVFAST(8) B2F_EVFAST(16)
