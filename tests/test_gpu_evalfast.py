@@ -76,3 +76,34 @@ def test_fast_pass_clean_and_carried_faults(engine, orc, rounds_choices, n, seed
     # the batch restored: clean again, fast pass only
     path, rep = _dev_eval(engine, batch, adv, fixed)
     assert path == 0 and rep["first_failure"] == NONE
+
+
+def test_fast_pass_tile_map_across_zero_round_runs(engine, orc):
+    """The fast pass's tile descriptors (eval_desc_kernel: a wave searches the row map for its
+    first tile, its lanes then search the next 64 instances and fall back to their own search
+    past them) on a batch with runs of 0-round instances -- which own no half-round tile -- of
+    1, 63, 64, 65 and 300 instances between 1-, 2- and 12-round ones: clean, then a fault in a
+    half-round cell of the instance right after each run is handed to the exact kernel and
+    reported where the oracle reports it."""
+    import b2f
+
+    x = random_inputs(1200, (1, 2, 12), 44)
+    runs = [(10, 1), (40, 63), (200, 64), (400, 65), (700, 300)]
+    for a, k in runs:
+        x["rounds"][a:a + k] = 0
+    batch = b2f.DeviceBatch(x)
+    batch.fill(engine)
+    engine.sync(0)
+    adv, fixed = batch.host_trace()
+    adv, fixed = adv.copy(), fixed.copy()
+    off = batch.offsets_host.astype(np.uint64)
+    path, rep = _dev_eval(engine, batch, adv, fixed)
+    assert path == 0 and rep["first_failure"] == NONE and rep["rows_checked"] == int(off[-1])
+    for a, k in runs:
+        i = a + k  # the first instance after the run
+        r = int(off[i]) + INIT_ROWS + 30  # a cell of its first half-round tile
+        a2 = adv.copy()
+        a2[4, r] ^= np.uint32(1 << 3)
+        path, g = _dev_eval(engine, batch, a2, fixed)
+        o = orc.evaluate(a2, fixed, off)
+        assert o["first_failure"] != NONE and g == o and path == 1, (a, k)

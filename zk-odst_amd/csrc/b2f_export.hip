@@ -200,7 +200,7 @@ hipError_t launch_spread_table(uint64_t usable_rows, uint32_t form, uint64_t* d_
 hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
                             uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
                             int cu_count, hipStream_t s) {
-  // persistent grid: 4 workgroups per CU (halo2 column h -> a_i by kAofH)
+  // persistent grid, workgroups per CU by form (below; halo2 column h -> a_i by kAofH)
   uint64_t tiles = (nrows + XT - 1) / XT;
   // persistent workgroups per CU, per form (same-process A/B, profiles/r05g*_export_ab_*.txt:
   // pasta 3 vs 4 / 2 / 5: 2.47 vs 2.49 / 2.85 / 2.79 ms; BN254 2 vs 4 / 3 / 5: 2.38 vs 2.54 /

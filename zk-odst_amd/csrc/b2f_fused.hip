@@ -2004,27 +2004,80 @@ edge_redo_kernel(const b2f_input* __restrict__ in, const uint64_t* __restrict__ 
 // report (MockProver's counters and first failing row).
 
 // half-round tile descriptors from the row map alone (the eval has no input records): a thread
-// per tile T finds its instance -- the last i with 2 R_i <= T, R_i = (off_i - 228 i) / 416 the
-// rounds before instance i (instances without rounds own no tile) -- by a binary search over the
-// row map, so the descriptors go out as whole lines (round 5: a thread per instance wrote its
-// 2 rounds descriptors 384 bytes apart from its neighbours', 73 us per 2^18 x 12 call)
+// per tile T, whose instance is the last i with 2 R_i <= T (R_i = (off_i - 228 i) / 416, the
+// rounds before instance i; instances without rounds own no tile). One search over the row map
+// per wave (its first tile), then the wave loads 2 R of the next 64 instances (one
+// coalesced load) and each lane finds its instance among them by a 6-step shuffle search; a lane
+// whose tile lies past them (possible only after runs of zero-round instances) searches the row
+// map itself. The descriptors go out as whole lines. (Round 5: a thread per instance wrote its
+// 2 rounds descriptors 384 bytes apart from its neighbours', 73 us per 2^18 x 12 call; a thread
+// per tile with its own 18-step search over the row map, 96 us; the per-wave search starts from the
+// interpolated instance, so a uniform batch needs two row-map loads per wave.)
 __global__ void __launch_bounds__(256) eval_desc_kernel(const uint64_t* __restrict__ off, uint32_t n,
                                                         TileDesc* __restrict__ desc,
                                                         const int* __restrict__ status) {
-  const uint64_t T = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t T = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, T0 = T - lane;
   if (*status) return;
-  auto R = [&](uint32_t i) { return (off[i] - (uint64_t)FIXED_ROWS * i) / ROUND_ROWS; };
-  const uint64_t tiles = 2 * R(n);
-  if (T >= tiles) return;
-  uint32_t lo = 0, hi = n;  // 2 R_lo <= T < 2 R_hi
-  while (hi - lo > 1) {
-    const uint32_t mid = lo + (hi - lo) / 2;
-    if (2 * R(mid) <= T) lo = mid;
-    else hi = mid;
+  auto R2 = [&](uint32_t i) { return 2 * ((off[i] - (uint64_t)FIXED_ROWS * i) / ROUND_ROWS); };
+  const uint64_t tiles = R2(n);
+  if (T0 >= tiles) return;
+  auto search = [&](uint64_t t) {  // last i < n with R2(i) <= t (R2(0) = 0 <= t < R2(n))
+    // the bracket [lo, hi) around the interpolated guess t n / tiles (exact for uniform rounds),
+    // widened by doubling steps, then bisected
+    uint32_t g = (uint32_t)((double)t / (double)tiles * (double)n);
+    g = g < n ? g : n - 1;
+    uint32_t lo, hi;
+    if (R2(g) <= t) {
+      lo = g;
+      uint32_t step = 1;
+      hi = g + 1;
+      while (hi < n && R2(hi) <= t) {
+        lo = hi;
+        hi = n - hi > step ? hi + step : n;
+        step *= 2;
+      }
+    } else {
+      hi = g;
+      uint32_t step = 1;
+      lo = g > step ? g - step : 0;
+      while (lo > 0 && R2(lo) > t) {
+        hi = lo;
+        step *= 2;
+        lo = lo > step ? lo - step : 0;
+      }
+    }
+    while (hi - lo > 1) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (R2(mid) <= t) lo = mid;
+      else hi = mid;
+    }
+    return lo;
+  };
+  const uint32_t i0 = __builtin_amdgcn_readfirstlane(search(T0));
+  const uint32_t il = i0 + lane;
+  const uint64_t r2 = il <= n ? R2(il) : ~0ull;  // nondecreasing over the lanes
+  uint32_t k = 0;
+#pragma unroll
+  for (uint32_t step = 32; step > 0; step >>= 1) {
+    const uint64_t v = ((uint64_t)(uint32_t)__shfl((int)(r2 >> 32), (int)(k + step) & 63, 64) << 32) |
+                       (uint32_t)__shfl((int)(uint32_t)r2, (int)(k + step) & 63, 64);
+    if (k + step < 64 && v <= T) k += step;
   }
-  const uint64_t r0 = R(lo);
-  const uint32_t rounds = (uint32_t)(R(lo + 1) - r0);
-  desc[T].v = make_uint4(lo, (uint32_t)(T - 2 * r0) + 1, rounds, (uint32_t)(2 * r0 + lo));
+  const uint64_t rn_sh = ((uint64_t)(uint32_t)__shfl((int)(r2 >> 32), (int)(k + 1) & 63, 64) << 32) |
+                         (uint32_t)__shfl((int)(uint32_t)r2, (int)(k + 1) & 63, 64);
+  if (T >= tiles) return;
+  uint32_t i = i0 + k;
+  uint64_t r0, r1;
+  if (k < 63) {  // instance i0 + k and the next one are among the wave's 64
+    r0 = ((uint64_t)(uint32_t)__shfl((int)(r2 >> 32), (int)k, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)r2, (int)k, 64);
+    r1 = rn_sh;
+  } else {  // past them
+    i = search(T);
+    r0 = R2(i);
+    r1 = R2(i + 1);
+  }
+  desc[T].v = make_uint4(i, (uint32_t)(T - r0) + 1, (uint32_t)((r1 - r0) / 2), (uint32_t)(r0 + i));
 }
 
 // The loads of one eval tile (see eval_hr_kernel): the tile's 11 cells of the lane's quad, the

@@ -374,7 +374,12 @@ __global__ __launch_bounds__(SC_THREADS) void lk_scan_write(const uint32_t* __re
 #endif
 constexpr int ZR = B2F_ZR;       // rows per lane
 static_assert(ZR == 2 || ZR == 4, "rows per lane");
-constexpr int ZT = 256;          // lanes per look-back block (lk_zpass workgroup)
+#ifndef B2F_ZT
+#define B2F_ZT 256
+#endif
+constexpr int ZT = B2F_ZT;       // lanes per look-back block (lk_zpass workgroup)
+constexpr int ZW = ZT / 64;      // its waves; a scanning lane takes ZW of the ZT lane totals
+static_assert(ZT == 128 || ZT == 256, "2 or 4 waves per look-back block");
 constexpr int LB = ZT * ZR;      // rows per look-back block
 __host__ __device__ inline uint64_t n_lb(uint64_t usable) { return (usable + LB - 1) / LB; }
 
@@ -708,7 +713,7 @@ __global__ __launch_bounds__(BK_T) void lk_block_kernel(uint64_t usable, uint64_
   }
 }
 
-// The five columns of one look-back block (LB = 256 ZR rows). Lane t of the workgroup owns rows
+// The five columns of one look-back block (LB = ZT ZR rows). Lane t of the workgroup owns rows
 // base + ZR t + j:
 //  1. the runs: A' = T[x_of_rank[r]] for the run r holding p, S' = A' at a run start, else leftover item
 //     n_left - 1 - j for the j-th repeated row (halo2 hands leftovers out in ascending order,
@@ -736,14 +741,13 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     const Fe* __restrict__ NK, const Fe* __restrict__ Dnum, const Fe* __restrict__ bg,
     uint64_t* __restrict__ lbs, uint32_t* __restrict__ ticket, int* __restrict__ sticky) {
   // the row and leftover tables, then (after every wave has read its rows) the lane totals
-  static_assert(ZT == 256, "the scans take 4 lane totals per lane");
   constexpr int SMEM = 2 * LB * 4 > 2 * ZT * 32 ? 2 * LB * 4 : 2 * ZT * 32;
   __shared__ uint4 smem[SMEM / 16];
   uint32_t* ent = reinterpret_cast<uint32_t*>(smem);  // per row: rank | start << 16 | (j - J0) << 17
   uint32_t* yl = ent + LB;                             // per leftover index - ylo: its rank
   Fe* sN = reinterpret_cast<Fe*>(smem);
   Fe* sD = sN + ZT;
-  __shared__ uint4 stage[4][ZSTAGE];  // per wave: the column staging
+  __shared__ uint4 stage[ZW][ZSTAGE];  // per wave: the column staging
   __shared__ Fe sX[64], sDb;          // the den wave's exclusive values and block product, parked
   __shared__ uint32_t s_tk;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
@@ -767,12 +771,12 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
   uint64_t* o = out + (uint64_t)(c0 + c) * 5 * out_rows * 4;
   const uint32_t base = (uint32_t)b * LB, p0 = base + ZR * t, r0 = base + 64u * ZR * wv;
   uint4* st = stage[wv];
-  // lane totals sit transposed (entry i at (i % 4) 64 + i / 4): a scanning lane's 4 entries are
+  // lane totals sit transposed (entry i at (i % ZW) 64 + i / ZW): a scanning lane's ZW entries are
   // 64 elements apart and its neighbours' adjacent (4-entry rows put lanes 128 B apart on the
   // same banks)
-  auto pz = [](uint32_t i) { return (i & 3u) * 64u + (i >> 2); };
-  const uint32_t wn = tk & 3u, wd = (tk + 1) & 3u;  // the num-scan and den-scan waves
-  const uint32_t e0 = 4 * lane;                     // a scanning lane's first entry
+  auto pz = [](uint32_t i) { return (i % ZW) * 64u + i / ZW; };
+  const uint32_t wn = tk % ZW, wd = (tk + 1) % ZW;  // the num-scan and den-scan waves
+  const uint32_t e0 = ZW * lane;                    // a scanning lane's first entry
   __syncthreads();
   LKCLK(0);
   uint32_t x[ZR], ra[ZR], rs[ZR];
@@ -869,16 +873,22 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
   // the den wave: its in-lane scan (suffix order: entry i of the scan is lane total 255 - i) and
   // the 6-level scan across its lanes; the block's product goes out as the aggregate at once
   uint64_t* my = lbs + ((uint64_t)c * nb + b) * LBS_WORDS;
-  auto atd = [&](uint32_t i) { return pz(255u - i); };
+  auto atd = [&](uint32_t i) { return pz((uint32_t)ZT - 1u - i); };
   if (wv == wd) {
     Fe Pd = sD[atd(e0)];
     sD[atd(e0)] = field::one<F>();
+#ifdef B2F_LK_NOSCAN  // diagnostics (wrong z): the block scans' products left out, to bound what they cost
+    if (false)
+#endif
 #pragma unroll 1
-    for (uint32_t k2 = 1; k2 < 4; k2++) {
+    for (uint32_t k2 = 1; k2 < (uint32_t)ZW; k2++) {
       const Fe e = sD[atd(e0 + k2)];
       sD[atd(e0 + k2)] = Pd;
       Pd = LKMUL(Pd, e);
     }
+#ifdef B2F_LK_NOSCAN
+    if (false)
+#endif
 #pragma unroll 1
     for (int off = 1; off < 64; off <<= 1) {
       const Fe y = shfl_fe(Pd, (int)lane - off);
@@ -922,12 +932,18 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     // the num wave: the exclusive prefix of the 256 num totals, in place
     Fe Pn = sN[pz(e0)];
     sN[pz(e0)] = field::one<F>();
+#ifdef B2F_LK_NOSCAN
+    if (false)
+#endif
 #pragma unroll 1
-    for (uint32_t k2 = 1; k2 < 4; k2++) {
+    for (uint32_t k2 = 1; k2 < (uint32_t)ZW; k2++) {
       const Fe e = sN[pz(e0 + k2)];
       sN[pz(e0 + k2)] = Pn;
       Pn = LKMUL(Pn, e);
     }
+#ifdef B2F_LK_NOSCAN
+    if (false)
+#endif
 #pragma unroll 1
     for (int off = 1; off < 64; off <<= 1) {
       const Fe y = shfl_fe(Pn, (int)lane - off);
@@ -937,8 +953,11 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     Fe Xn = shfl_fe(Pn, (int)lane - 1);
     if (lane == 0) Xn = field::one<F>();
     sN[pz(e0)] = Xn;
+#ifdef B2F_LK_NOSCAN
+    if (false)
+#endif
 #pragma unroll 1
-    for (uint32_t k2 = 1; k2 < 4; k2++) sN[pz(e0 + k2)] = LKMUL(Xn, sN[pz(e0 + k2)]);
+    for (uint32_t k2 = 1; k2 < (uint32_t)ZW; k2++) sN[pz(e0 + k2)] = LKMUL(Xn, sN[pz(e0 + k2)]);
   } else if (wv == wd) {
     // the den wave: the look-back over the blocks after b. Lane i watches block q0 + i's status
     // word; the blocks up to the first inclusive one (fi) must all have published, then their
@@ -1008,8 +1027,11 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(B2F_ZP_WAVES
     // exclusive values, so a lane's K is one product: (num prefix) (den suffix)
     const Fe X = LKMUL(sX[lane], LKMUL(NK[(uint64_t)c * nb + b], after));
     sD[atd(e0)] = X;
+#ifdef B2F_LK_NOSCAN
+    if (false)
+#endif
 #pragma unroll 1
-    for (uint32_t k2 = 1; k2 < 4; k2++) sD[atd(e0 + k2)] = LKMUL(X, sD[atd(e0 + k2)]);
+    for (uint32_t k2 = 1; k2 < (uint32_t)ZW; k2++) sD[atd(e0 + k2)] = LKMUL(X, sD[atd(e0 + k2)]);
   }
   __syncthreads();
   LKCLK(5);
