@@ -439,3 +439,41 @@ def test_fused_injection_at_segment_starts(engine, orc):
                 adv, fixed = batch.host_trace()
                 assert got == orc.evaluate(adv, fixed, off), (i, r, col)
                 cases += 1
+
+
+def test_max_rounds_instance(engine, orc):
+    """An instance at B2F_MAX_ROUNDS (2^20 rounds: 436 M rows, 19 GB of trace, 87,381 listed
+    segments of the fused launch) among 12-round ones: h' equals the oracle's compression
+    (oracle.compress, the same rounds), the fused and split traces are equal column by column,
+    both verdicts are clean, and a fault near the instance's end is reported at the same row by
+    the fused pass and by b2f_eval_dev (the eval's exact kernel then runs over 436 M rows)."""
+    import torch
+
+    import b2f
+
+    x = random_inputs(8, (12,), 95)
+    i = 5
+    x["rounds"][i] = b2f._lib.MAX_ROUNDS
+    fused = _fused(engine, x)
+    rep = fused.report_dict()
+    assert rep["first_failure"] == NONE and rep["rows_checked"] >= fused.used_rows
+    want = orc.compress(int(x["rounds"][i]), x["h"][i], x["m"][i], x["t"][i], int(x["f"][i]))
+    assert np.array_equal(fused.host_h_out()[i], np.asarray(want, dtype=np.uint64))
+    split = b2f.DeviceBatch(x)
+    split.fill(engine)
+    split.evaluate(engine)
+    engine.sync(_stream())
+    assert split.report_dict() == rep
+    for c in range(10):
+        assert torch.equal(fused.advice[c], split.advice[c]), "a_%d" % c
+    assert torch.equal(fused.fixed, split.fixed) and torch.equal(fused.h_out, split.h_out)
+    del split
+    torch.cuda.empty_cache()
+    # a fault in the instance's last half-round: fused verdict == split eval's
+    r = int(fused.offsets_host[i + 1]) - 64 - 100
+    bad = _fused(engine, x, inject=(r, 3, 1 << 5))
+    got = bad.report_dict()
+    assert got["first_failure"] != NONE and (got["first_failure"] >> 8) <= r + 2
+    bad.evaluate(engine)
+    engine.sync(_stream())
+    assert bad.report_dict() == got

@@ -23,6 +23,7 @@
 // l >> 1 of the span's 32 cells), non-temporal.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/b2f.h"
 #include "b2f_field.h"
@@ -50,6 +51,30 @@ __device__ __forceinline__ u64x2 bn254_half(uint32_t x, uint32_t half) {
 #pragma unroll
   for (int i = 0; i < 4; i++) o[i] = half ? m.w[4 + i] : m.w[i];  // no dynamic index (scratch)
   return u64x2{(uint64_t)o[0] | ((uint64_t)o[1] << 32), (uint64_t)o[2] | ((uint64_t)o[3] << 32)};
+}
+
+// the whole pasta Montgomery element of cell value x (the closed form of fp_half below)
+__device__ __forceinline__ field::Fe pasta_mont(uint32_t x) {
+  field::Fe r;
+  uint64_t v[4] = {0, 0, 0, 0};
+  if (x != 0) {
+    const uint64_t y = 4ull * x - 1;
+    const uint64_t z0 = y * kD0, h0 = __umul64hi(y, kD0), l1 = y * kD1;
+    uint64_t z2 = __umul64hi(y, kD1);
+    const uint64_t z1 = h0 + l1;
+    z2 += (z1 < h0);
+    const uint64_t b0 = (z0 != 0), b1 = (z1 != 0) | b0, b2 = (z2 != 0) | b1;
+    v[0] = 0 - z0;
+    v[1] = 0 - z1 - b0;
+    v[2] = 0 - z2 - b1;
+    v[3] = (1ull << 62) - b2;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    r.w[2 * i] = (uint32_t)v[i];
+    r.w[2 * i + 1] = (uint32_t)(v[i] >> 32);
+  }
+  return r;
 }
 
 // limbs (2*half, 2*half+1) of the field element for cell value x: canonical (either field),
@@ -95,6 +120,9 @@ __device__ __forceinline__ u64x2 fp_half(uint32_t x, uint32_t half) {
 // reads the ten 2 KiB column slices (all loads issued first) and writes the ten 16 KiB output
 // slices; every store instruction of a wave covers 1 KiB contiguous.
 constexpr int XT = 512;
+#ifndef B2F_EXPORT_PAIR_PASTA
+#define B2F_EXPORT_PAIR_PASTA 0  // 1 (variant): pasta cells formed once per store pair, as BN254's
+#endif
 constexpr int XSUB = XT / CELLS_PER_ITER;  // 4 store passes per column per tile
 constexpr int kAofH[10] = {5, 3, 4, 6, 7, 8, 9, 0, 1, 2};
 
@@ -118,7 +146,7 @@ __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
 #pragma unroll
     for (int h = 0; h < 10; h++) {
       u64x2* dst = reinterpret_cast<u64x2*>(out + (uint64_t)h * out_rows * 4);
-      if (FORM == 3) {
+      if (FORM == 3 || (FORM == 1 && B2F_EXPORT_PAIR_PASTA)) {
         // BN254's per-cell product is the cost, and both lanes of a store pair need the same
         // cell: each lane forms one whole cell of two consecutive passes instead (even lane:
         // pass i's, odd lane: pass i + 1's), and the pair swaps the half the other one stores
@@ -126,7 +154,8 @@ __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
         for (int i = 0; i < XSUB; i += 2) {
           // a bitwise select: `half ? x[h][i + 1] : x[h][i]` became a dynamic index (x in scratch)
           const uint32_t xa = x[h][i], xb = x[h][i + 1];
-          const field::Fe m = field::from_u32<field::Bn254>(xa ^ ((xa ^ xb) & (0u - half)));
+          const uint32_t xs = xa ^ ((xa ^ xb) & (0u - half));
+          const field::Fe m = FORM == 3 ? field::from_u32<field::Bn254>(xs) : pasta_mont(xs);
           uint32_t own[4], give[4];
 #pragma unroll
           for (int w = 0; w < 4; w++) {
@@ -206,7 +235,14 @@ hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint6
   // pasta 3 vs 4 / 2 / 5: 2.47 vs 2.49 / 2.85 / 2.79 ms; BN254 2 vs 4 / 3 / 5: 2.38 vs 2.54 /
   // 2.50 / 2.53 at 2^25 rows): fewer concurrent tile streams write faster until the cells'
   // compute is no longer hidden (pasta's is a few instructions, BN254's a 32-bit quotient)
-  uint64_t want = (uint64_t)cu_count * (form == B2F_FP_BN254_MONTGOMERY ? 2 : 3);
+  int per_cu = form == B2F_FP_BN254_MONTGOMERY ? 2 : 3;
+#ifdef B2F_DIAG  // diagnostics: B2F_EXPORT_PERCU overrides the workgroups per CU
+  if (const char* v = getenv("B2F_EXPORT_PERCU")) {
+    const int k = atoi(v);
+    if (k >= 1 && k <= 8) per_cu = k;
+  }
+#endif
+  uint64_t want = (uint64_t)cu_count * per_cu;
   uint32_t gx = (uint32_t)(tiles < want ? tiles : want);
   if (gx == 0) return hipSuccess;
   if (form == B2F_FP_BN254_MONTGOMERY) {
