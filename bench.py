@@ -229,35 +229,54 @@ def spawn_ranks(n, argv, script=None, grace_s=30.0, poll_s=0.2):
     script = script or os.path.abspath(__file__)
     port = free_port()
     procs = []
-    for k in range(n):
-        env = dict(os.environ)
-        env.update({"RANK": str(k), "LOCAL_RANK": str(k), "WORLD_SIZE": str(n),
-                    "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
-                    "MASTER_PORT": str(port)})
-        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        t_kill = time.monotonic() + 10
+        for p in procs:
+            try:
+                p.wait(max(0.1, t_kill - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    class Stopped(Exception):
+        pass
+
+    def on_signal(signum, frame):
+        raise Stopped(signum)
+
+    # the parent stopped (a launcher's time limit, ^C): its ranks stop with it
+    old = {sg: signal.signal(sg, on_signal) for sg in (signal.SIGTERM, signal.SIGINT)}
     first_bad, deadline = None, None
-    while True:
-        codes = [p.poll() for p in procs]
-        for c in codes:
-            if c is not None and c != 0 and first_bad is None:
-                first_bad = 128 - c if c < 0 else c
-                deadline = time.monotonic() + grace_s
-                log("bench: a rank exited with status %d; the others get %g s" % (first_bad, grace_s))
-        if all(c is not None for c in codes):
-            break
-        if deadline is not None and time.monotonic() > deadline:
-            for p in procs:
-                if p.poll() is None:
-                    p.send_signal(signal.SIGTERM)
-            t_kill = time.monotonic() + 10
-            for p in procs:
-                try:
-                    p.wait(max(0.1, t_kill - time.monotonic()))
-                except subprocess.TimeoutExpired:
-                    p.kill()
-                    p.wait()
-            break
-        time.sleep(poll_s)
+    try:
+        for k in range(n):
+            env = dict(os.environ)
+            env.update({"RANK": str(k), "LOCAL_RANK": str(k), "WORLD_SIZE": str(n),
+                        "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                        "MASTER_PORT": str(port)})
+            procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+        while True:
+            codes = [p.poll() for p in procs]
+            for c in codes:
+                if c is not None and c != 0 and first_bad is None:
+                    first_bad = 128 - c if c < 0 else c
+                    deadline = time.monotonic() + grace_s
+                    log("bench: a rank exited with status %d; the others get %g s" % (first_bad, grace_s))
+            if all(c is not None for c in codes):
+                break
+            if deadline is not None and time.monotonic() > deadline:
+                stop_all()
+                break
+            time.sleep(poll_s)
+    except Stopped as e:
+        stop_all()
+        first_bad = first_bad or 128 + int(e.args[0])
+    finally:
+        for sg, h in old.items():
+            signal.signal(sg, h)
     return first_bad or 0
 
 

@@ -135,3 +135,38 @@ def test_bench_spawns_ranks_without_launcher(tmp_path, capfd):
     t0 = time.monotonic()
     assert bench.spawn_ranks(2, ["hang"], script=str(child), grace_s=1.0) == 5
     assert time.monotonic() - t0 < 60
+
+
+def test_bench_spawned_ranks_stop_with_the_parent(tmp_path):
+    """A launcher that stops `bench.py --gpus N` (SIGTERM to the parent) stops its ranks too:
+    no rank outlives the parent, and the parent's status says it was terminated."""
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    child = tmp_path / "child.py"
+    child.write_text("import os, time\nopen(os.environ['PIDDIR'] + '/' + os.environ['RANK'], 'w').write(str(os.getpid()))\ntime.sleep(600)\n")
+    code = ("import sys; sys.path.insert(0, %r); import bench; "
+            "sys.exit(bench.spawn_ranks(2, [], script=%r))" % (root, str(child)))
+    env = dict(os.environ, PIDDIR=str(tmp_path))
+    parent = subprocess.Popen([sys.executable, "-c", code], env=env)
+    pids = []
+    for _ in range(300):
+        pids = [p for p in ("0", "1") if (tmp_path / p).exists() and (tmp_path / p).read_text()]
+        if len(pids) == 2:
+            break
+        time.sleep(0.1)
+    assert len(pids) == 2
+    parent.send_signal(signal.SIGTERM)
+    assert parent.wait(30) == 128 + signal.SIGTERM
+    for p in pids:
+        pid = int((tmp_path / p).read_text())
+        try:
+            os.kill(pid, 0)
+            alive = True
+        except ProcessLookupError:
+            alive = False
+        assert not alive, "rank %s outlived the parent" % p
