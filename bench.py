@@ -707,34 +707,23 @@ def main():
     fp_export_bn254 = None
     if args.export_rows > 0 and world == 1:
         nr = min(args.export_rows, batch.total_rows)
-        # the output columns nr + COLUMN_PAD_ROWS rows apart (the layout b2f.engine allocates:
-        # a 2^30-byte column stride aliases in the HBM interleave); the bare nr-row stride is
-        # timed beside it
-        out = torch.empty((10, nr + b2f.COLUMN_PAD_ROWS, 4), dtype=torch.int64, device=batch.advice.device)
-        bare = torch.empty((10, nr, 4), dtype=torch.int64, device=batch.advice.device)
+        out = torch.empty((10, nr, 4), dtype=torch.int64, device=batch.advice.device)
         res = {}
-
-        def export_ms(form, o, reps):
-            batch.export_fp(eng, nrows=nr, out=o, form=form, stream=stream)
-            eng.sync(stream)
-            eng.set_timing(True)
-            for _ in range(reps):
-                batch.export_fp(eng, nrows=nr, out=o, form=form, stream=stream)
-            tot, cnt = eng.kernel_times()["export"]
-            return tot / max(cnt, 1)
-
         for form, name in ((b2f.FP_MONTGOMERY, "pasta Fp montgomery"),
                            (b2f.FP_BN254_MONTGOMERY, "bn254 Fr montgomery")):
-            avg = export_ms(form, out, 5)
+            batch.export_fp(eng, nrows=nr, out=out, form=form, stream=stream)
+            eng.sync(stream)
+            eng.set_timing(True)
+            reps = 5
+            for _ in range(reps):
+                batch.export_fp(eng, nrows=nr, out=out, form=form, stream=stream)
+            tot, cnt = eng.kernel_times()["export"]
+            avg = tot / max(cnt, 1)
             nbytes = nr * 10 * (4 + 32)
             res[form] = {"rows": nr, "form": name, "avg_ms": round(avg, 4),
                          "bytes_per_launch": nbytes,
                          "achieved_GBs": round(nbytes / (avg * 1e-3) / 1e9, 1),
-                         "frac": round(nbytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "column_stride_bytes": out.shape[1] * 32,
-                         "bare_stride_avg_ms": round(export_ms(form, bare, 3), 4),
-                         "bare_stride_bytes": nr * 32}
-        del bare
+                         "frac": round(nbytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         fp_export, fp_export_bn254 = res[b2f.FP_MONTGOMERY], res[b2f.FP_BN254_MONTGOMERY]
         del out
 

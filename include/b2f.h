@@ -222,10 +222,7 @@ B2F_API int b2f_chain_inputs_dev(b2f_ctx* ctx, const uint64_t* d_h_prev, const u
  * order (b2f_halo2_column_index): element of a_i at row row_begin + r goes to
  * d_out[(h * out_rows + r) * 4 + limb], h = b2f_halo2_column_index(i), 4 little-endian u64
  * limbs. out_rows >= nrows is the column stride (rows past nrows are not written; a prover
- * zero-fills to 2^k). Layout advice (this and every other call writing field-element columns
- * side by side): a column stride of a large power of two (2^k rows x 32 B) aliases in the HBM
- * channel interleave and writes ~12 % slower; 1,024 rows more than 2^k do not (the Python host
- * allocates so, b2f.engine.COLUMN_PAD_ROWS). `form`:
+ * zero-fills to 2^k). `form`:
  *   B2F_FP_MONTGOMERY        x * 2^256 mod p (the in-memory Fp of pasta_curves)
  *   B2F_FP_CANONICAL         x as a 32-byte little-endian integer (PrimeField::to_repr)
  *   B2F_FP_BN254_MONTGOMERY  x * 2^256 mod r (the in-memory bn256::Fr of halo2curves)

@@ -34,22 +34,23 @@ def main():
     nr = min(args.rows, batch.total_rows)
     engines = [("product", prod)] + [(os.path.basename(p), b2f.Engine(0, lib_path=os.path.join(ROOT, p)))
                                      for p in args.libs.split(",") if p]
-    pads = [int(p) for p in args.pads.split(",")]
-    outs = {p: torch.empty((10, nr + p, 4), dtype=torch.int64, device=batch.advice.device) for p in pads}
+    pads = [int(p) for p in args.pads.split(",")]  # a pad may repeat: allocations in this order
+    outs = [torch.empty((10, nr + p, 4), dtype=torch.int64, device=batch.advice.device) for p in pads]
     res = {}
     for rep in range(args.reps):
         for name, eng in engines:
-            for p in pads:
+            for ip, p in enumerate(pads):
                 for form in (b2f.FP_MONTGOMERY, b2f.FP_BN254_MONTGOMERY):
                     eng.set_timing(True)
-                    batch.export_fp(eng, nrows=nr, out=outs[p], form=form, stream=s)
+                    batch.export_fp(eng, nrows=nr, out=outs[ip], form=form, stream=s)
                     eng.sync(s)
                     tot, cnt = eng.kernel_times()["export"]
-                    res.setdefault((name, p, form), []).append(tot / max(cnt, 1))
+                    res.setdefault((name, ip, p, form), []).append(tot / max(cnt, 1))
     nbytes = nr * 10 * 36
-    for (name, p, form), v in res.items():
+    for (name, ip, p, form), v in res.items():
         best = min(v[1:]) if len(v) > 1 else v[0]
-        print(json.dumps({"lib": name, "pad_rows": p, "form": form, "ms": round(best, 4),
+        print(json.dumps({"lib": name, "alloc": ip, "base_mod_1GiB": outs[ip].data_ptr() % (1 << 30),
+                          "pad_rows": p, "form": form, "ms": round(best, 4),
                           "GBs": round(nbytes / best / 1e6, 1), "all": [round(x, 3) for x in v]}))
 
 

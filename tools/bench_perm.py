@@ -18,7 +18,6 @@ def main():
     ap.add_argument("--forms", default="1,3")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--lib", default=None, help="a variant library (A/B), default the product")
-    ap.add_argument("--pad", type=int, default=None, help="output column pad rows (default: the engine's)")
     args = ap.parse_args()
     import torch
 
@@ -34,22 +33,21 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     eng.sync(s)
     for form in [int(f) for f in args.forms.split(",")]:
-        batch.permutation_columns(eng, args.k, usable, 3, 5, chunk_len=args.chunk, form=form, sigma=False,
-                                  pad_rows=args.pad)
-        sig = batch.permutation_sigma(eng, args.k, form=form, pad_rows=args.pad)
+        batch.permutation_columns(eng, args.k, usable, 3, 5, chunk_len=args.chunk, form=form, sigma=False)
+        sig = batch.permutation_sigma(eng, args.k, form=form)
         eng.sync(s)
         eng.set_timing(True)
         for _ in range(args.reps):
             _, z = batch.permutation_columns(eng, args.k, usable, 3, 5, chunk_len=args.chunk,
-                                             form=form, sigma=False, pad_rows=args.pad)
-            sig = batch.permutation_sigma(eng, args.k, form=form, pad_rows=args.pad)
+                                             form=form, sigma=False)
+            sig = batch.permutation_sigma(eng, args.k, form=form)
         eng.sync(s)
         kt = eng.kernel_times()
         ms, cnt = kt["perm"]
         sms, scnt = kt["perm_sigma"]
         per, sper = ms / cnt, sms / scnt
         sets = (8 + args.chunk - 1) // args.chunk
-        print(json.dumps({"lib": args.lib or "product", "pad": args.pad, "k": args.k, "instances": n_inst, "form": form,
+        print(json.dumps({"lib": args.lib or "product", "k": args.k, "instances": n_inst, "form": form,
                           "chunk_len": args.chunk, "z_ms_per_call": round(per, 3),
                           "sigma_ms_per_call": round(sper, 3), "rows_per_s": round(n_rows / per * 1e3),
                           "z_written_GBps": round(usable * 32 * sets / per / 1e6, 1)}))

@@ -7,5 +7,5 @@ from ._lib import (FP_BN254_CANONICAL, FP_BN254_MONTGOMERY, FP_CANONICAL, FP_MON
                    B2FError, EvalReport, load)
 from .layout import (INPUT_DTYPE, SELECTORS, as_inputs, halo2_column_index, offsets,  # noqa: F401
                      parse_eip152, rows, split_fixed)
-from .engine import COLUMN_PAD_ROWS, DeviceBatch, Engine, copy_constraints, permutation_mapping  # noqa: F401
+from .engine import DeviceBatch, Engine, copy_constraints, permutation_mapping  # noqa: F401
 from . import field  # noqa: F401

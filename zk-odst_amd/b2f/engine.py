@@ -11,13 +11,6 @@ import numpy as np
 from . import _lib
 from .layout import INPUT_DTYPE, as_inputs, offsets as layout_offsets
 
-# Column stride of the field-element outputs this module allocates: rows + COLUMN_PAD_ROWS
-# (32 KiB more). A stride of a large power of two (2^k rows x 32 B: 2^27 .. 2^30 bytes) makes the
-# columns alias in the HBM channel interleave, and the kernels write the columns side by side:
-# the Fp export of 2^25 rows ran 2.46 / 2.40 ms (pasta / BN254) at a 2^30-byte stride and
-# 2.19 / 2.11 with 1,024 rows more (profiles/r06b_export_pads.txt); 64 rows more did not help.
-COLUMN_PAD_ROWS = 1024
-
 
 def _vp(x):
     return ctypes.c_void_p(int(x))
@@ -294,18 +287,16 @@ class DeviceBatch:
         preallocated tensor of that shape (out_rows >= nrows)."""
         torch = self.torch
         nrows = self.total_rows - row_begin if nrows is None else int(nrows)
-        view = None
-        if out is None:  # columns COLUMN_PAD_ROWS rows further apart than nrows (returned as a view)
-            out = torch.empty((_lib.NUM_ADVICE, nrows + COLUMN_PAD_ROWS, 4), dtype=torch.int64,
+        if out is None:
+            out = torch.empty((_lib.NUM_ADVICE, nrows, 4), dtype=torch.int64,
                               device=self.advice.device)
-            view = nrows
         if out.dim() != 3 or out.shape[0] != _lib.NUM_ADVICE or out.shape[2] != 4 \
                 or out.dtype != torch.int64 or not out.is_contiguous():
             raise _lib.B2FError(_lib.ERR_ARG, "export_fp: out must be contiguous int64 [10, rows, 4]")
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
         eng.export_fp_dev(self.advice.data_ptr(), self.total_rows, row_begin, nrows, form,
                           out.data_ptr(), out.shape[1], s)
-        return out if view is None else out[:, :view]
+        return out
 
     def lookup_columns(self, eng, row_begin, usable_rows, theta, beta, gamma,
                        form=_lib.FP_MONTGOMERY, stream=None):
@@ -325,13 +316,11 @@ class DeviceBatch:
         return out, bad
 
     def permutation_columns(self, eng, k, usable_rows, beta, gamma, chunk_len=3,
-                            form=_lib.FP_MONTGOMERY, instances=None, sigma=True, stream=None,
-                            pad_rows=None):
+                            form=_lib.FP_MONTGOMERY, instances=None, sigma=True, stream=None):
         """Permutation-argument prover columns of the circuit holding instances
         [i0, i1) = `instances` (default: all) in a 2^k-row domain: (sigma int64 [8, 2^k, 4] or
         None, z int64 [sets, 2^k, 4] with rows 0..usable_rows written) -- see
-        b2f_permutation_columns_dev. omega and delta come from the field of `form`. The columns
-        are views of buffers 2^k + pad_rows rows apart (COLUMN_PAD_ROWS by default)."""
+        b2f_permutation_columns_dev. omega and delta come from the field of `form`."""
         from . import field
 
         torch = self.torch
@@ -340,19 +329,17 @@ class DeviceBatch:
         off = self.offsets_host[i0:i1 + 1]
         f = field.of_form(form)
         n_rows = 1 << int(k)
-        stride = n_rows + (COLUMN_PAD_ROWS if pad_rows is None else int(pad_rows))
         sets = (8 + chunk_len - 1) // chunk_len
-        sig = torch.empty((8, stride, 4), dtype=torch.int64, device=dev) if sigma else None
-        z = torch.empty((sets, stride, 4), dtype=torch.int64, device=dev)
+        sig = torch.empty((8, n_rows, 4), dtype=torch.int64, device=dev) if sigma else None
+        z = torch.empty((sets, n_rows, 4), dtype=torch.int64, device=dev)
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
         eng.permutation_columns_dev(self.advice.data_ptr(), self.total_rows, off, k, usable_rows,
                                     field.omega(f, int(k)), field.delta(f), beta, gamma,
                                     chunk_len, form, sig.data_ptr() if sigma else 0,
-                                    z.data_ptr(), stride, s)
-        return (sig[:, :n_rows] if sigma else None), z[:, :n_rows]
+                                    z.data_ptr(), n_rows, s)
+        return sig, z
 
-    def permutation_sigma(self, eng, k, form=_lib.FP_MONTGOMERY, instances=None, stream=None,
-                          pad_rows=None):
+    def permutation_sigma(self, eng, k, form=_lib.FP_MONTGOMERY, instances=None, stream=None):
         """Keygen's sigma columns (int64 [8, 2^k, 4]) of the circuit holding instances
         [i0, i1) = `instances` (default: all): b2f_permutation_sigma_dev, the same columns
         permutation_columns returns, without a witness."""
@@ -363,12 +350,11 @@ class DeviceBatch:
         off = self.offsets_host[i0:i1 + 1]
         f = field.of_form(form)
         n_rows = 1 << int(k)
-        stride = n_rows + (COLUMN_PAD_ROWS if pad_rows is None else int(pad_rows))
-        sig = torch.empty((8, stride, 4), dtype=torch.int64, device=self.advice.device)
+        sig = torch.empty((8, n_rows, 4), dtype=torch.int64, device=self.advice.device)
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
         eng.permutation_sigma_dev(off, k, field.omega(f, int(k)), field.delta(f), form, sig.data_ptr(),
-                                  stride, s)
-        return sig[:, :n_rows]
+                                  n_rows, s)
+        return sig
 
     def report_dict(self):
         raw = self.report.cpu().numpy().view(np.uint64)

@@ -53,30 +53,6 @@ __device__ __forceinline__ u64x2 bn254_half(uint32_t x, uint32_t half) {
   return u64x2{(uint64_t)o[0] | ((uint64_t)o[1] << 32), (uint64_t)o[2] | ((uint64_t)o[3] << 32)};
 }
 
-// the whole pasta Montgomery element of cell value x (the closed form of fp_half below)
-__device__ __forceinline__ field::Fe pasta_mont(uint32_t x) {
-  field::Fe r;
-  uint64_t v[4] = {0, 0, 0, 0};
-  if (x != 0) {
-    const uint64_t y = 4ull * x - 1;
-    const uint64_t z0 = y * kD0, h0 = __umul64hi(y, kD0), l1 = y * kD1;
-    uint64_t z2 = __umul64hi(y, kD1);
-    const uint64_t z1 = h0 + l1;
-    z2 += (z1 < h0);
-    const uint64_t b0 = (z0 != 0), b1 = (z1 != 0) | b0, b2 = (z2 != 0) | b1;
-    v[0] = 0 - z0;
-    v[1] = 0 - z1 - b0;
-    v[2] = 0 - z2 - b1;
-    v[3] = (1ull << 62) - b2;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    r.w[2 * i] = (uint32_t)v[i];
-    r.w[2 * i + 1] = (uint32_t)(v[i] >> 32);
-  }
-  return r;
-}
-
 // limbs (2*half, 2*half+1) of the field element for cell value x: canonical (either field),
 // pasta Montgomery (the closed form above) or BN254 Montgomery (FORM 3)
 template <int FORM>
@@ -120,8 +96,8 @@ __device__ __forceinline__ u64x2 fp_half(uint32_t x, uint32_t half) {
 // reads the ten 2 KiB column slices (all loads issued first) and writes the ten 16 KiB output
 // slices; every store instruction of a wave covers 1 KiB contiguous.
 constexpr int XT = 512;
-#ifndef B2F_EXPORT_PAIR_PASTA
-#define B2F_EXPORT_PAIR_PASTA 0  // 1 (variant): pasta cells formed once per store pair, as BN254's
+#ifndef B2F_EXPORT_STAGGER
+#define B2F_EXPORT_STAGGER 0
 #endif
 constexpr int XSUB = XT / CELLS_PER_ITER;  // 4 store passes per column per tile
 constexpr int kAofH[10] = {5, 3, 4, 6, 7, 8, 9, 0, 1, 2};
@@ -133,6 +109,11 @@ __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
   const uint32_t t = threadIdx.x;
   const uint32_t half = t & 1;
   const uint64_t n_tiles = (nrows + XT - 1) / XT;
+  // the output column of the tile's h-th store pass: h itself, or (variant B2F_EXPORT_STAGGER)
+  // h + blockIdx mod 10, so the chip's concurrent stores spread over all ten columns instead of
+  // sweeping one column at a time (x[h] then holds that column's cells: registers stay static)
+  const int h0 = B2F_EXPORT_STAGGER ? (int)(blockIdx.x % 10u) : 0;
+  auto col_of = [&](int h) { return h + h0 >= 10 ? h + h0 - 10 : h + h0; };
   for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const uint64_t r0 = tile * XT;
     uint32_t x[10][XSUB];
@@ -141,12 +122,13 @@ __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
 #pragma unroll
       for (int i = 0; i < XSUB; i++) {
         uint64_t cell = r0 + i * CELLS_PER_ITER + (t >> 1);
-        x[h][i] = cell < nrows ? advice[(uint64_t)kAofH[h] * total_rows + row_begin + cell] : 0u;
+        x[h][i] = cell < nrows ? advice[(uint64_t)kAofH[col_of(h)] * total_rows + row_begin + cell] : 0u;
       }
 #pragma unroll
     for (int h = 0; h < 10; h++) {
-      u64x2* dst = reinterpret_cast<u64x2*>(out + (uint64_t)h * out_rows * 4);
-      if (FORM == 3 || (FORM == 1 && B2F_EXPORT_PAIR_PASTA)) {
+      const int hs = col_of(h);
+      u64x2* dst = reinterpret_cast<u64x2*>(out + (uint64_t)hs * out_rows * 4);
+      if (FORM == 3) {
         // BN254's per-cell product is the cost, and both lanes of a store pair need the same
         // cell: each lane forms one whole cell of two consecutive passes instead (even lane:
         // pass i's, odd lane: pass i + 1's), and the pair swaps the half the other one stores
@@ -154,8 +136,7 @@ __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
         for (int i = 0; i < XSUB; i += 2) {
           // a bitwise select: `half ? x[h][i + 1] : x[h][i]` became a dynamic index (x in scratch)
           const uint32_t xa = x[h][i], xb = x[h][i + 1];
-          const uint32_t xs = xa ^ ((xa ^ xb) & (0u - half));
-          const field::Fe m = FORM == 3 ? field::from_u32<field::Bn254>(xs) : pasta_mont(xs);
+          const field::Fe m = field::from_u32<field::Bn254>(xa ^ ((xa ^ xb) & (0u - half)));
           uint32_t own[4], give[4];
 #pragma unroll
           for (int w = 0; w < 4; w++) {

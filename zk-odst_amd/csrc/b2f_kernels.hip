@@ -39,7 +39,8 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
                          void* scratch, uint32_t group, int* sticky, hipStream_t s2,
-                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s);
+                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s3, hipEvent_t ev_tab,
+                         hipEvent_t ev_sorted, hipStream_t s);
 hipError_t launch_spread_table(uint64_t usable_rows, uint32_t form, uint64_t* d_out,
                                uint64_t out_rows, hipStream_t s);
 size_t perm_scratch_bytes(uint32_t k, uint64_t usable_rows, size_t n_inst, uint32_t chunk_len);
@@ -884,6 +885,8 @@ struct b2f_ctx {
   // down-sweep (b2f_gprod.h), forked from and joined back to the caller's stream
   hipStream_t s2;
   hipEvent_t ev_fork, ev_join;
+  hipStream_t s3;                // the lookup's table pass and sort (beside the count pass)
+  hipEvent_t ev_tab, ev_sorted;
 };
 
 namespace {
@@ -950,6 +953,9 @@ int ensure_side(b2f_ctx* ctx) {
   if (!ctx->s2) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
   if (!ctx->ev_fork) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
   if (!ctx->ev_join) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+  if (!ctx->s3) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->s3, hipStreamNonBlocking));
+  if (!ctx->ev_tab) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_tab, hipEventDisableTiming));
+  if (!ctx->ev_sorted) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_sorted, hipEventDisableTiming));
   return B2F_OK;
 }
 
@@ -1162,6 +1168,9 @@ B2F_API void b2f_destroy(b2f_ctx* ctx) {
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   if (ctx->s2) (void)hipStreamDestroy(ctx->s2);
+  if (ctx->ev_tab) (void)hipEventDestroy(ctx->ev_tab);
+  if (ctx->ev_sorted) (void)hipEventDestroy(ctx->ev_sorted);
+  if (ctx->s3) (void)hipStreamDestroy(ctx->s3);
   (void)hipHostFree(ctx->h_pm_inst);
   for (hipEvent_t e : ctx->pool) (void)hipEventDestroy(e);
   delete ctx;
@@ -1539,7 +1548,8 @@ B2F_API int b2f_lookup_columns_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint6
   int tk = timed_begin(ctx, B2F_KERNEL_LOOKUP, s);
   HIPCHK(ctx, launch_lookup(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, theta, beta,
                             gamma, form, d_out, out_rows, d_first_bad, ctx->d_lk, group,
-                            ctx->d_status + 2, ctx->s2, ctx->ev_fork, ctx->ev_join, s));
+                            ctx->d_status + 2, ctx->s2, ctx->ev_fork, ctx->ev_join, ctx->s3,
+                            ctx->ev_tab, ctx->ev_sorted, s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }

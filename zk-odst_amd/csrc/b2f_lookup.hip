@@ -47,7 +47,8 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
                          void* scratch, uint32_t group, int* sticky, hipStream_t s2,
-                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s);
+                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s3, hipEvent_t ev_tab,
+                         hipEvent_t ev_sorted, hipStream_t s);
 
 namespace {
 
@@ -1115,11 +1116,20 @@ Carve carve(void* base, uint32_t group, uint64_t usable) {
   return k;
 }
 
+#ifndef B2F_LK_SORT_SIDE
+#define B2F_LK_SORT_SIDE 1  // 0 (variant): table pass + sort on the main stream before the count pass
+#endif
+// A third stream for the table pass and its sort (run_lookup)
+struct SortSide {
+  hipStream_t s3;
+  hipEvent_t tab, sorted;
+};
+
 template <class F>
 hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint64_t* d_row_begin,
                       uint32_t n_circuits, uint64_t usable_rows, const Chal& ch, bool mont,
                       uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad, void* scratch,
-                      uint32_t group, int* sticky, const gp::Side& side, hipStream_t s) {
+                      uint32_t group, int* sticky, const gp::Side& side, const SortSide& ss, hipStream_t s) {
   Carve k = carve(scratch, group, usable_rows);
   const uint64_t nb = n_lb(usable_rows);
 #ifdef B2F_DIAG
@@ -1130,27 +1140,43 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   }
 #endif
   const dim3 tb(TROWS / 256);
-  hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, s, ch, k.Tx, k.key, k.perm, k.bg);
-  // one radix sort by the top limb of the canonical value (< 2^63: both moduli are < 2^255),
-  // then ties in the top limb ordered by the lower limbs
+  hipError_t e;
+  // The table values, their rank order (a radix sort by the top limb, then ties ordered by the
+  // lower limbs) and the per-circuit count pass are independent: the table pass and the sort run
+  // on a third stream beside the count pass (the sort is six small rocprim launches, ~60 us of
+  // latency on the main stream before round 6), and the num side's block products start as soon
+  // as the table values exist, beside both (profiles/r06d_lookup_timeline.txt).
+  hipStream_t st = B2F_LK_SORT_SIDE ? ss.s3 : s;
+  if (B2F_LK_SORT_SIDE) {
+    if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(st, side.fork, 0)) != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, st, ch, k.Tx, k.key, k.perm, k.bg);
+  if ((e = hipEventRecord(ss.tab, st)) != hipSuccess) return e;
   uint32_t* pa = k.perm2;
   {
     size_t bytes = k.sort_bytes;
-    hipError_t e = rocprim::radix_sort_pairs(k.sort_tmp, bytes, k.key + 3ull * TROWS, k.kout, k.perm, pa,
-                                             (size_t)TROWS, 0, 63, s);
+    e = rocprim::radix_sort_pairs(k.sort_tmp, bytes, k.key + 3ull * TROWS, k.kout, k.perm, pa,
+                                  (size_t)TROWS, 0, 63, st);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(lk_tie_fix_kernel, tb, dim3(256), 0, s, k.key, k.kout, pa);
-  hipError_t e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s);
-  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(lk_tie_fix_kernel, tb, dim3(256), 0, st, k.key, k.kout, pa);
+  if ((e = hipEventRecord(ss.sorted, st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s)) != hipSuccess) return e;
   // Per group: the num side (block products, their prefix, D and D^-1) on the side stream,
   // forked at the group's start (after the previous group's z pass, which read the same NK
-  // slots), beside the count and rank-scan passes; then the z pass over all the group's circuits
-  // (a workgroup count that fills the chip).
+  // slots; the first group's after the table pass), beside the count and rank-scan passes; then
+  // the z pass over all the group's circuits (a workgroup count that fills the chip).
   for (uint32_t c0 = 0; c0 < n_circuits; c0 += group) {
     const uint32_t g = n_circuits - c0 < group ? n_circuits - c0 : group;
-    if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
+    if (c0 == 0) {
+      if (!B2F_LK_SORT_SIDE && (e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(side.s2, ss.tab, 0)) != hipSuccess) return e;
+    } else {
+      if ((e = hipEventRecord(side.fork, s)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(side.s2, side.fork, 0)) != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(lk_npart_kernel<F>, dim3((uint32_t)((nb + 4 * NP_BPW - 1) / (4 * NP_BPW)), g + (c0 == 0 ? 1 : 0)), dim3(256), 0,
                        side.s2, d_advice, total_rows, d_row_begin, c0, g, usable_rows, nb, k.Tx, ch, k.partA,
                        k.partS);
@@ -1159,6 +1185,7 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
     if ((e = hipEventRecord(side.join, side.s2)) != hipSuccess) return e;
     hipLaunchKernelGGL(lk_count_kernel, dim3(CNT_SPLIT, g), dim3(CNT_THREADS), 0, s, d_advice,
                        total_rows, d_row_begin, c0, usable_rows, k.count, d_first_bad);
+    if (c0 == 0 && B2F_LK_SORT_SIDE && (e = hipStreamWaitEvent(s, ss.sorted, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(lk_scan_sums, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows, k.part);
     hipLaunchKernelGGL(lk_scan_write, dim3(SC_PARTS, g), dim3(SC_THREADS), 0, s, pa, k.count, usable_rows,
                        k.part, k.pos, k.dcnt, k.lrank, k.lstart, k.samp, k.nlr);
@@ -1195,8 +1222,10 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
                          const uint64_t* theta, const uint64_t* beta, const uint64_t* gamma,
                          uint32_t form, uint64_t* d_out, uint64_t out_rows, uint64_t* d_first_bad,
                          void* scratch, uint32_t group, int* sticky, hipStream_t s2,
-                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s) {
+                         hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s3, hipEvent_t ev_tab,
+                         hipEvent_t ev_sorted, hipStream_t s) {
   const gp::Side side{s2, ev_fork, ev_join};
+  const SortSide ss{s3, ev_tab, ev_sorted};
   Chal ch;
   for (int i = 0; i < 4; i++) {
     ch.theta[i] = theta[i];
@@ -1206,9 +1235,9 @@ hipError_t launch_lookup(const uint32_t* d_advice, uint64_t total_rows,
   const bool mont = (form & 1u) != 0;
   if (form >> 1)
     return run_lookup<field::Bn254>(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, ch,
-                                    mont, d_out, out_rows, d_first_bad, scratch, group, sticky, side, s);
+                                    mont, d_out, out_rows, d_first_bad, scratch, group, sticky, side, ss, s);
   return run_lookup<field::Pallas>(d_advice, total_rows, d_row_begin, n_circuits, usable_rows, ch,
-                                   mont, d_out, out_rows, d_first_bad, scratch, group, sticky, side, s);
+                                   mont, d_out, out_rows, d_first_bad, scratch, group, sticky, side, ss, s);
 }
 
 }  // namespace b2f
