@@ -96,9 +96,6 @@ __device__ __forceinline__ u64x2 fp_half(uint32_t x, uint32_t half) {
 // reads the ten 2 KiB column slices (all loads issued first) and writes the ten 16 KiB output
 // slices; every store instruction of a wave covers 1 KiB contiguous.
 constexpr int XT = 512;
-#ifndef B2F_EXPORT_STAGGER
-#define B2F_EXPORT_STAGGER 0
-#endif
 constexpr int XSUB = XT / CELLS_PER_ITER;  // 4 store passes per column per tile
 constexpr int kAofH[10] = {5, 3, 4, 6, 7, 8, 9, 0, 1, 2};
 
@@ -109,11 +106,6 @@ __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
   const uint32_t t = threadIdx.x;
   const uint32_t half = t & 1;
   const uint64_t n_tiles = (nrows + XT - 1) / XT;
-  // the output column of the tile's h-th store pass: h itself, or (variant B2F_EXPORT_STAGGER)
-  // h + blockIdx mod 10, so the chip's concurrent stores spread over all ten columns instead of
-  // sweeping one column at a time (x[h] then holds that column's cells: registers stay static)
-  const int h0 = B2F_EXPORT_STAGGER ? (int)(blockIdx.x % 10u) : 0;
-  auto col_of = [&](int h) { return h + h0 >= 10 ? h + h0 - 10 : h + h0; };
   for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const uint64_t r0 = tile * XT;
     uint32_t x[10][XSUB];
@@ -122,12 +114,11 @@ __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
 #pragma unroll
       for (int i = 0; i < XSUB; i++) {
         uint64_t cell = r0 + i * CELLS_PER_ITER + (t >> 1);
-        x[h][i] = cell < nrows ? advice[(uint64_t)kAofH[col_of(h)] * total_rows + row_begin + cell] : 0u;
+        x[h][i] = cell < nrows ? advice[(uint64_t)kAofH[h] * total_rows + row_begin + cell] : 0u;
       }
 #pragma unroll
     for (int h = 0; h < 10; h++) {
-      const int hs = col_of(h);
-      u64x2* dst = reinterpret_cast<u64x2*>(out + (uint64_t)hs * out_rows * 4);
+      u64x2* dst = reinterpret_cast<u64x2*>(out + (uint64_t)h * out_rows * 4);
       if (FORM == 3) {
         // BN254's per-cell product is the cost, and both lanes of a store pair need the same
         // cell: each lane forms one whole cell of two consecutive passes instead (even lane:
