@@ -356,10 +356,14 @@ def main():
     # rehearsal of the N > 1 code path on a one-GPU box (never for measurements): every rank
     # on cuda:0, collectives over gloo
     rehearse = os.environ.get("B2F_BENCH_REHEARSE") == "1"
+    # the N > 1 code path (process group, collectives, witness gather) at any world size, here
+    # for a one-rank RCCL run on a one-GPU box: the collectives are real RCCL calls on the device
+    dist_on = world > 1 or os.environ.get("B2F_BENCH_FORCE_DIST") == "1"
+    solo = not dist_on  # the one-GPU legs beside the headline
     if rehearse:
         local = 0
     torch.cuda.set_device(local)
-    if world > 1:
+    if dist_on:
         if rehearse:
             dist.init_process_group("gloo")
         else:
@@ -399,7 +403,7 @@ def main():
         """Warm-up, then `steps` timed steps between barriers; returns (elapsed max over
         ranks, kernel times, verdict dict, h' gather buffer)."""
         gathered = verdict = None
-        if world > 1:
+        if dist_on:
             width = max(hi - lo for lo, hi in info["shards"]) if info["shards"] else info["n_local"]
             gathered = torch.empty((world * width, 8), dtype=torch.int64, device=device)
             hpad = torch.zeros((width, 8), dtype=torch.int64, device=device)
@@ -407,7 +411,7 @@ def main():
         def step():
             run_path(batch, path)
             nonlocal verdict
-            if world > 1:
+            if dist_on:
                 verdict = bdist.all_reduce_verdict(
                     bdist.verdict_words(batch.report, info["base"], torch), dist)
                 hsrc = batch.h_out
@@ -423,20 +427,20 @@ def main():
         if rep["first_failure"] != 2**64 - 1:
             raise SystemExit("eval flagged the trace: %s" % rep)
         eng.set_timing(True)
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         ktimes = eng.kernel_times()
         eng.sync(stream)
         rep = batch.report_dict()
-        if world > 1:
+        if dist_on:
             t = torch.tensor([elapsed], dtype=torch.float64, device=device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
@@ -599,11 +603,11 @@ def main():
     # N > 1: the legs after the headline use collectives; one that hangs (a rank failing where
     # the others wait) must not cost the headline line, so a watchdog prints it and ends every
     # rank once the extras run past --extras-timeout (ExtrasWatchdog)
-    watchdog = ExtrasWatchdog(args.extras_timeout if world > 1 else 0, rank, headline)
+    watchdog = ExtrasWatchdog(args.extras_timeout if dist_on else 0, rank, headline)
 
     collectives = None
     witness = None
-    if world > 1:
+    if dist_on:
         collectives = collectives_alone(batch, info, args.steps)
         if global_n:
             witness = witness_gather(batch.advice, batch.fixed, info["rows"],
@@ -633,7 +637,7 @@ def main():
     # (fill floor, fused pass, split fill, eval floor, split eval), so drifts in the box's
     # store rate hit both sides alike; min and median over the reps are reported.
     floors = None
-    if world == 1 and args.floor_reps > 0:
+    if solo and args.floor_reps > 0:
         try:
             deng = b2f.Engine(local, diag=True)
             samples = {"fill_floor": [], "stream_floor": [], "fill_eval": [], "fill": [],
@@ -684,7 +688,7 @@ def main():
     # the other path, timed the same way (reported beside the headline, not part of it)
     aux = None
     other = "fused" if args.path == "split" else "split"
-    if args.aux_steps > 0 and world == 1:
+    if args.aux_steps > 0 and solo:
         run_path(batch, other)
         eng.sync(stream)
         eng.set_timing(True)
@@ -705,7 +709,7 @@ def main():
     # Montgomery pallas limbs for a chunk of the resident trace (4 B read, 32 B written/cell)
     fp_export = None
     fp_export_bn254 = None
-    if args.export_rows > 0 and world == 1:
+    if args.export_rows > 0 and solo:
         nr = min(args.export_rows, batch.total_rows)
         out = torch.empty((10, nr, 4), dtype=torch.int64, device=batch.advice.device)
         res = {}
@@ -730,7 +734,7 @@ def main():
     # Lookup-argument prover columns for circuits cut from the resident
     # trace, and the multi-block hasher (row 3): reported beside the headline, not part of it
     lookup = None
-    if world == 1 and args.lookup_circuits > 0:
+    if solo and args.lookup_circuits > 0:
         try:
             usable = (1 << 17) - 7
             nc = min(args.lookup_circuits, batch.total_rows // usable)
@@ -775,7 +779,7 @@ def main():
     # Permutation-argument prover columns of a 2^k-row circuit cut from
     # the resident trace: sigma (8 columns) + the grand products of ceil(8 / 3) column sets
     perm = None
-    if world == 1 and args.perm_k > 0:
+    if solo and args.perm_k > 0:
         try:
             k = args.perm_k
             usable = (1 << k) - 7
@@ -840,7 +844,7 @@ def main():
         except Exception as e:  # reported, never masks the headline
             perm = {"error": repr(e)}
     hasher_aux = None
-    if world == 1 and args.hasher_messages > 0:
+    if solo and args.hasher_messages > 0:
         try:
             import hashlib
 
@@ -875,7 +879,7 @@ def main():
     # the ranks, fill + eval timed the same way, then the whole witness table gathered
     # (--config4-world 2 --config4 32768 rehearses the same code on a one-GPU box)
     config4 = None
-    if world > 1 and world == args.config4_world and not global_n and args.config4 > 0:
+    if dist_on and world == args.config4_world and not global_n and args.config4 > 0:
         try:
             del batch
             torch.cuda.empty_cache()
@@ -895,7 +899,7 @@ def main():
             config4["hbm_free_after_gb"] = round(torch.cuda.mem_get_info(local)[0] / 1e9, 1)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and solo and not args.no_cpu:
         cpu = cpu_baseline(args.rounds, mix, args.cpu_seconds, args.cpu_threads)
 
     out = headline()
@@ -909,7 +913,7 @@ def main():
         return  # the watchdog printed the line and is ending the process
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -71,3 +71,28 @@ def test_bench_gpus2_spawns_two_ranks_without_launcher():
     assert line["config"]["parallelism"].startswith("dp2")
     assert line["collectives"] is not None and line["collectives"]["ms_per_step"] > 0
     assert line["witness_gather"] and line["witness_gather"].get("own_rows_in_place"), line["witness_gather"]
+
+
+@pytest.mark.gpu
+def test_bench_rccl_code_path_one_rank():
+    """The N > 1 path of bench.py over real RCCL on the one GPU (B2F_BENCH_FORCE_DIST=1, one
+    nccl rank): the step's verdict all-reduce and h' all-gather, the collectives timed alone, the
+    per-column witness all-gather (RCCL's coalesced group) and the config-4 leg with its own
+    sharded batch and full gather -- the calls an 8-GPU run makes, made on the device."""
+    env = dict(os.environ)
+    env.update({"B2F_BENCH_FORCE_DIST": "1", "RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1",
+                "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29533"})
+    env.pop("B2F_BENCH_REHEARSE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--batch", "4096", "--steps", "2",
+           "--warmup", "1", "--witness-gather", "64", "--config4", "16384", "--config4-world", "1",
+           "--extras-timeout", "200"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and line["collectives"]["ms_per_step"] > 0
+    assert line["witness_gather"]["own_rows_in_place"], line["witness_gather"]
+    c4 = line["config4"]
+    assert "error" not in c4, c4
+    assert c4["global_batch"] == 16384 and c4["witness_gather"]["own_rows_in_place"], c4
