@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--modes", default="27", help="B2F_DIAG_FUSED modes to time per variant")
     ap.add_argument("--batch", type=int, default=1 << 18)
     ap.add_argument("--rounds", type=int, default=12)
+    ap.add_argument("--mix", action="store_true", help="rounds uniform in {1,4,12} (config 5)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--eval", action="store_true", help="also time each variant's eval kernel")
     ap.add_argument("--fill", action="store_true", help="also time each variant's split fill")
@@ -26,7 +27,7 @@ def main():
     import b2f
     from b2f import synth
 
-    x = synth.batch(args.batch, rounds=args.rounds)
+    x = synth.batch(args.batch, rounds=args.rounds, rounds_mix=[1, 4, 12] if args.mix else None)
     batch = b2f.DeviceBatch(x)
     s = torch.cuda.current_stream().cuda_stream
     prod = b2f.Engine(0)

@@ -1065,6 +1065,9 @@ __device__ __forceinline__ uint32_t hr_fast_checks(const hr2::Lane& K, uint32_t 
 #ifndef B2F_EDGE_SEPARATE
 #define B2F_EDGE_SEPARATE 0  // 1 (diagnostics): the edge tiles in their own launch after this one
 #endif
+#ifndef B2F_FUSED_DYN
+#define B2F_FUSED_DYN 1  // 0 (variant): instances dealt statically to the waves (round 5)
+#endif
 template <int MODE>
 __device__ __forceinline__ void edge_walk(uint32_t* S, uint32_t lane, uint64_t t_first, uint64_t W,
                                           const uint64_t* IV, const uint8_t* Sg, EvalAcc& A,
@@ -1078,7 +1081,7 @@ template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES, B2F_FUSED_WAVES)
 fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
                 uint64_t total_rows, const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
-                uint32_t* __restrict__ fixed, const TileDesc* __restrict__ desc,
+                uint32_t* __restrict__ fixed, unsigned* __restrict__ ictr,
                 b2f_eval_report* __restrict__ rep, const int* __restrict__ status, Inject inj,
                 uint64_t* __restrict__ defer, uint32_t defer_cap, unsigned long long* __restrict__ clk,
                 const uint64_t* __restrict__ seg, uint64_t seg_cap, uint32_t* __restrict__ redo) {
@@ -1121,6 +1124,25 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
       const uint64_t* x = reinterpret_cast<const uint64_t*>(in + (i < n ? i : 0));
       return x[lane < 27 ? lane : 26];
     };
+#if B2F_FUSED_DYN
+    // Instances are claimed from the launch's counter (a wave holds the one it walks and the next
+    // one, whose record it loads ahead): the waves finish within one instance of each other
+    // whatever the rounds mix. Dealt statically (wave w: instances w, w + W, ...) a {1,4,12}
+    // batch gave each wave 85 instances of 2 / 8 / 24 half-round tiles at random, i.e. per-wave
+    // work spread by +-9 % and the launch ended with its slowest wave (round 6, config 5).
+    auto next_inst = [&](uint32_t) -> uint32_t {
+      uint32_t i;
+      do {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(ictr, 1u);
+        i = __builtin_amdgcn_readfirstlane(v);
+      } while (i < n && in[i].rounds == 0);
+      return i < n ? i : n;
+    };
+    const uint64_t w0 = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
+    uint32_t inst = next_inst(0);
+#else
+    (void)ictr;
     // the instance after `i` in this wave's sequence that has half-rounds (scalar loads)
     auto next_inst = [&](uint32_t i) -> uint32_t {
       uint64_t j = (uint64_t)i + W;
@@ -1129,6 +1151,7 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
     };
     const uint64_t w0 = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
     uint32_t inst = w0 < n ? (in[w0].rounds ? (uint32_t)w0 : next_inst((uint32_t)w0)) : n;
+#endif
     uint64_t Pi = rec_word(inst);  // the current instance's record word
     // settled before the loop: otherwise the compiler cannot prove at the loop header that Pi is
     // never pending and waits for vmcnt(0) -- every store in flight -- at its first use
@@ -2439,7 +2462,12 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   TileDesc* desc = reinterpret_cast<TileDesc*>(scratch);
   uint64_t* defer = reinterpret_cast<uint64_t*>(desc + tiles);
   uint32_t* redo = reinterpret_cast<uint32_t*>(defer + 1 + DEFER_CAP);
+  // the half-round launch's instance counter: the first word of the tile-descriptor area (only
+  // the eval's fast pass uses descriptors)
+  unsigned* ictr = reinterpret_cast<unsigned*>(desc);
   hipError_t e = hipMemsetAsync(defer, 0, 8, s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(ictr, 0, 4, s);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(redo, 0, 4, s);
   if (e != hipSuccess) return e;
@@ -2491,7 +2519,7 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
 #define B2F_FUSED(M)                                                                               \
   case M:                                                                                          \
     hipLaunchKernelGGL(fused_hr_kernel<M>, dim3(grid), dim3(FW * WAVES), 0, s, d_in, n, d_off,     \
-                       total_rows, rec, d_adv, d_fixed, desc, d_rep, d_status, inj, defer, DEFER_CAP, \
+                       total_rows, rec, d_adv, d_fixed, ictr, d_rep, d_status, inj, defer, DEFER_CAP, \
                        clk, seg, seg_cap, redo);                                                   \
     if (B2F_EDGE_SEPARATE)                                                                         \
       hipLaunchKernelGGL(fused_edge_kernel<M>, dim3(grid_e), dim3(FW * WAVES), 0, s, d_in, n, d_off, \
