@@ -32,7 +32,7 @@ namespace b2f {
 
 hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
                             uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
-                            int cu_count, hipStream_t s);
+                            int cu_count, unsigned* tctr, hipStream_t s);
 hipError_t launch_spread_table(uint64_t usable_rows, uint32_t form, uint64_t* d_out,
                                uint64_t out_rows, hipStream_t s);
 
@@ -99,14 +99,34 @@ constexpr int XT = 512;
 constexpr int XSUB = XT / CELLS_PER_ITER;  // 4 store passes per column per tile
 constexpr int kAofH[10] = {5, 3, 4, 6, 7, 8, 9, 0, 1, 2};
 
+#ifndef B2F_EXPORT_DYN
+#define B2F_EXPORT_DYN 1  // 0 (variant): tiles dealt round-robin to the workgroups (round 5)
+#endif
 template <int FORM>
 __global__ __launch_bounds__(EXPORT_BLOCK) void export_fp_kernel(
     const uint32_t* __restrict__ advice, uint64_t total_rows, uint64_t row_begin,
-    uint64_t nrows, uint64_t* __restrict__ out, uint64_t out_rows) {
+    uint64_t nrows, uint64_t* __restrict__ out, uint64_t out_rows, unsigned* __restrict__ tctr) {
   const uint32_t t = threadIdx.x;
   const uint32_t half = t & 1;
   const uint64_t n_tiles = (nrows + XT - 1) / XT;
+#if B2F_EXPORT_DYN
+  // tiles claimed from the launch's counter (a barrier per tile shares the claim), so the
+  // workgroups finish within a tile of each other: 2.20 -> 1.87 ms pasta, 2.12 -> 1.81 BN254 at
+  // 2^25 rows (profiles/r06k_placement_export_dyn.jsonl; 65,536 claims of 184 KB each)
+  __shared__ uint32_t s_tile[2];
+  uint32_t slot = 0;
+  auto claim = [&]() -> uint64_t {
+    if (t == 0) s_tile[slot] = atomicAdd(tctr, 1u);
+    __syncthreads();
+    const uint64_t v = __builtin_amdgcn_readfirstlane(s_tile[slot]);
+    slot ^= 1u;
+    return v;
+  };
+  for (uint64_t tile = claim(); tile < n_tiles; tile = claim()) {
+#else
+  (void)tctr;
   for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+#endif
     const uint64_t r0 = tile * XT;
     uint32_t x[10][XSUB];
 #pragma unroll
@@ -200,7 +220,7 @@ hipError_t launch_spread_table(uint64_t usable_rows, uint32_t form, uint64_t* d_
 
 hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
                             uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
-                            int cu_count, hipStream_t s) {
+                            int cu_count, unsigned* tctr, hipStream_t s) {
   // persistent grid, workgroups per CU by form (below; halo2 column h -> a_i by kAofH)
   uint64_t tiles = (nrows + XT - 1) / XT;
   // persistent workgroups per CU, per form (same-process A/B, profiles/r05g*_export_ab_*.txt:
@@ -217,15 +237,17 @@ hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint6
   uint64_t want = (uint64_t)cu_count * per_cu;
   uint32_t gx = (uint32_t)(tiles < want ? tiles : want);
   if (gx == 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(tctr, 0, sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
   if (form == B2F_FP_BN254_MONTGOMERY) {
     hipLaunchKernelGGL(export_fp_kernel<3>, dim3(gx), dim3(EXPORT_BLOCK), 0, s, d_advice,
-                       total_rows, row_begin, nrows, d_out, out_rows);
+                       total_rows, row_begin, nrows, d_out, out_rows, tctr);
   } else if (form & 1u) {
     hipLaunchKernelGGL(export_fp_kernel<1>, dim3(gx), dim3(EXPORT_BLOCK), 0, s, d_advice,
-                       total_rows, row_begin, nrows, d_out, out_rows);
+                       total_rows, row_begin, nrows, d_out, out_rows, tctr);
   } else {
     hipLaunchKernelGGL(export_fp_kernel<0>, dim3(gx), dim3(EXPORT_BLOCK), 0, s, d_advice,
-                       total_rows, row_begin, nrows, d_out, out_rows);
+                       total_rows, row_begin, nrows, d_out, out_rows, tctr);
   }
   return hipGetLastError();
 }

@@ -1068,6 +1068,12 @@ __device__ __forceinline__ uint32_t hr_fast_checks(const hr2::Lane& K, uint32_t 
 #ifndef B2F_FUSED_DYN
 #define B2F_FUSED_DYN 1  // 0 (variant): instances dealt statically to the waves (round 5)
 #endif
+#ifndef B2F_FUSED_EDGE_DYN
+// 1 (variant): the edge tiles claimed from a counter too -- 11.62 vs 9.38 ms (2^18 x 12) and 8.53
+// vs 6.62 ({1,4,12}), profiles/r06k_ab_dyn_*.txt: an edge tile is 9 KB of work, and 2^18 claims
+// within the launch's last half-millisecond serialise on the one counter
+#define B2F_FUSED_EDGE_DYN 0
+#endif
 template <int MODE>
 __device__ __forceinline__ void edge_walk(uint32_t* S, uint32_t lane, uint64_t t_first, uint64_t W,
                                           const uint64_t* IV, const uint8_t* Sg, EvalAcc& A,
@@ -1076,7 +1082,7 @@ __device__ __forceinline__ void edge_walk(uint32_t* S, uint32_t lane, uint64_t t
                                           const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
                                           uint32_t* __restrict__ fixed, uint32_t* __restrict__ redo,
                                           const Inject& inj, uint64_t* __restrict__ defer,
-                                          uint32_t defer_cap);
+                                          uint32_t defer_cap, unsigned* __restrict__ ectr);
 template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES, B2F_FUSED_WAVES)
 fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __restrict__ off,
@@ -1479,7 +1485,8 @@ fused_hr_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* __
     }
     if (!B2F_EDGE_SEPARATE)  // then the edge tiles, in the wave's whole region
       edge_walk<MODE>(L + H_WAVE + wv * HW_WORDS, lane, w0, W, IV, Sg, A, in, n, off, total_rows, rec,
-                      adv, fixed, redo, inj, defer, defer_cap);
+                      adv, fixed, redo, inj, defer, defer_cap,
+                      B2F_FUSED_DYN && B2F_FUSED_EDGE_DYN ? ictr + 1 : nullptr);
   }
   if ((MODE & FZ_CLOCK) && lane == 0) {
 #pragma unroll
@@ -1731,7 +1738,7 @@ __device__ __forceinline__ void edge_walk(uint32_t* S, uint32_t lane, uint64_t t
                                           const uint64_t* __restrict__ rec, uint32_t* __restrict__ adv,
                                           uint32_t* __restrict__ fixed, uint32_t* __restrict__ redo,
                                           const Inject& inj, uint64_t* __restrict__ defer,
-                                          uint32_t defer_cap) {
+                                          uint32_t defer_cap, unsigned* __restrict__ ectr) {
   using namespace hr2;
   using namespace edge2;
   const uint32_t Sb = lds_byte(S);
@@ -1748,7 +1755,15 @@ __device__ __forceinline__ void edge_walk(uint32_t* S, uint32_t lane, uint64_t t
     const uint64_t used_rows = off[n];
     const uint64_t n_pad = ((total_rows - used_rows) / 4 + PAD_Q - 1) / PAD_Q;
     const uint64_t t_all = (uint64_t)n + n_pad;
-    uint64_t t = t_first;
+    // edge tiles t, t + W, ... from t_first, or (ectr) claimed from the launch's counter: a wave
+    // holds the tile it works on and the next two, whose context it loads ahead
+    auto claim = [&]() -> uint64_t {
+      uint32_t v = 0;
+      if (lane == 0) v = atomicAdd(ectr, 1u);
+      return __builtin_amdgcn_readfirstlane(v);
+    };
+    uint64_t t = ectr ? claim() : t_first;
+    uint64_t t1 = ectr ? claim() : t + W;
     auto ectx = [&](uint64_t tt) {
       ECtx c;
       const uint32_t i = tt < n ? (uint32_t)tt : 0u;
@@ -1802,9 +1817,10 @@ __device__ __forceinline__ void edge_walk(uint32_t* S, uint32_t lane, uint64_t t
     ECtx c = ectx(t);
     Ops P = words(c);  // past the instances: instance 0's words (harmless, unused)
     settle(P);
-    ECtx cn = ectx(t + W);
-    for (; t < t_all; t += W) {
-      const ECtx cnn = ectx(t + 2 * W);  // scalar loads, two tiles ahead
+    ECtx cn = ectx(t1);
+    while (t < t_all) {
+      const uint64_t t2 = ectr ? claim() : t1 + W;
+      const ECtx cnn = ectx(t2);  // scalar loads, two tiles ahead
       const Ops Pn = words(cn);         // unconditional: the compiler counts vmcnt exactly
       if (t < n) {
         // ---- one instance's init + final regions
@@ -1930,6 +1946,8 @@ __device__ __forceinline__ void edge_walk(uint32_t* S, uint32_t lane, uint64_t t
       c = cn;
       cn = cnn;
       P = Pn;
+      t = t1;
+      t1 = t2;
     }
     }
 }
@@ -1963,7 +1981,7 @@ fused_edge_kernel(const b2f_input* __restrict__ in, uint32_t n, const uint64_t* 
   if (*status == 0)
     edge_walk<MODE>(S, lane, first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x),
                     (uint64_t)gridDim.x * WAVES, IV, Sg, A, in, n, off, total_rows, rec, adv, fixed,
-                    redo, inj, defer, defer_cap);
+                    redo, inj, defer, defer_cap, nullptr);
   __syncthreads();
   flush_report(A, rep, tid);
 }
@@ -2204,8 +2222,10 @@ __device__ __forceinline__ bool eval_edge_walk(uint32_t* S, uint32_t lane, uint6
 #ifndef B2F_EVAL_WAVES_HR
 #define B2F_EVAL_WAVES_HR 3  // waves per SIMD of the eval fast pass (the prefetched tile's registers)
 #endif
-#ifndef B2F_EVAL_ILV
-#define B2F_EVAL_ILV 0
+#ifndef B2F_EVAL_DYN
+// 1 (variant): bands claimed from a counter -- 9.77 vs 9.64 ms (2^18 x 12), 5.26 vs 5.17 (mix),
+// profiles/r06k_ab_dyn_*.txt: the load-bound pass balances itself
+#define B2F_EVAL_DYN 0
 #endif
 #ifndef B2F_EVAL_HR_BAND
 #define B2F_EVAL_HR_BAND 24  // consecutive half-round tiles per wave visit (1: one tile, every limb table gathered)
@@ -2223,7 +2243,7 @@ template <int MODE>
 __global__ void __launch_bounds__(FW * WAVES, B2F_EVAL_WAVES_HR)
 eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fixed, uint32_t n,
                const uint64_t* __restrict__ off, uint64_t total_rows, const TileDesc* __restrict__ desc,
-               uint32_t* __restrict__ dirty, const int* __restrict__ status) {
+               uint32_t* __restrict__ dirty, unsigned* __restrict__ bctr, const int* __restrict__ status) {
   using namespace hr2;
   __shared__ __attribute__((aligned(16))) uint32_t L[H_WORDS];
   const int tid = threadIdx.x;
@@ -2241,20 +2261,22 @@ eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fi
   const uint64_t used_rows = off[n];
   const uint64_t n_hr = (used_rows - (uint64_t)FIXED_ROWS * n) / 208;
   const uint64_t W = (uint64_t)gridDim.x * WAVES;
-#if B2F_EVAL_ILV
-  // (variant) a workgroup's 4 waves walk ONE band of 4 EV_BAND consecutive tiles interleaved --
-  // wave w takes tiles 4 m + w -- so the workgroup reads 4 adjacent tiles (3.3 KB per column) at a
-  // time; every limb table is gathered (the previous tile is another wave's)
-  const uint64_t WB = gridDim.x, EVB = (uint64_t)EV_BAND * WAVES;
-  uint64_t b = first_tile(blockIdx.x, 0, gridDim.x) / WAVES;
-  uint64_t t = b * EVB + wv;
-  uint32_t j = 0;
+#if B2F_EVAL_DYN
+  // (variant) bands of EV_BAND consecutive tiles per wave visit, claimed from the launch's counter
+  // (one band ahead, when the band's last tile prefetches the next one's first)
+  auto claim = [&]() -> uint64_t {
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(bctr, 1u);
+    return __builtin_amdgcn_readfirstlane(v);
+  };
+  uint64_t b = claim();
 #else
+  (void)bctr;
   // bands of EV_BAND consecutive tiles per wave visit, dealt like single tiles (first_tile)
   uint64_t b = first_tile(blockIdx.x, __builtin_amdgcn_readfirstlane(wv), gridDim.x);
+#endif
   uint64_t t = b * EV_BAND;
   uint32_t j = 0;
-#endif
   const uint32_t cA0 = carry_addr(lane, lds_byte(S), 0), cA1 = carry_addr(lane, lds_byte(S), 1);
   auto raw_desc = [&](uint64_t tt) -> uint4 { return desc[tt].v; };
   // per tile: its cells (lane = quad), its limb-table entry (the canonical dense / spread cell of
@@ -2264,23 +2286,14 @@ eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fi
   HCtx c = hctx(raw_desc(t < n_hr ? t : 0));
   EvCells cur = ev_load(c, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg, true);
   while (t < n_hr) {
-#if B2F_EVAL_ILV
-    uint64_t tn = t + WAVES, bn = b;
-    uint32_t jn = j + 1;
-    if (jn == EV_BAND || tn >= n_hr) {
-      bn = b + WB;
-      tn = bn * EVB + wv;
-      jn = 0;
-    }
-    const HCtx cn = hctx(raw_desc(tn < n_hr ? tn : 0));
-    const EvCells nxt = ev_load(cn, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg, true);
-    uint32_t ltd = cur.d, lts = cur.sp;
-    if (false) {
-#else
     uint64_t tn = t + 1, bn = b;
     uint32_t jn = j + 1;
     if (jn == EV_BAND || tn >= n_hr) {
+#if B2F_EVAL_DYN
+      bn = claim();
+#else
       bn = b + W;
+#endif
       tn = bn * EV_BAND;
       jn = 0;
     }
@@ -2288,7 +2301,6 @@ eval_hr_kernel(const uint32_t* __restrict__ adv, const uint32_t* __restrict__ fi
     const EvCells nxt = ev_load(cn, lane, lq, mg, mwh, mk, adv, fixed, total_rows, Sg, jn == 0 || cn.hr == 0);
     uint32_t ltd = cur.d, lts = cur.sp;
     if (j != 0 && c.hr != 0) {  // the staging holds half-round hr - 1 of this instance
-#endif
       const uint32_t a = ((c.hr - 1) & 1u) ? cA1 : cA0;
       ltd = ld32(a & 0xffffu);
       lts = ld32(a >> 16);
@@ -2389,7 +2401,8 @@ namespace b2f {
 // list (count + DEFER_CAP rows).
 // + the edge launch's redo list (count + one slot per instance; tiles >= instances)
 size_t fused_scratch_bytes(uint64_t tiles) {
-  return tiles * sizeof(TileDesc) + 8 * (1 + DEFER_CAP) + 4 * (2 + tiles) + 8;  // + the eval's dirty word
+  // + the eval's band counter and dirty word
+  return tiles * sizeof(TileDesc) + 8 * (1 + DEFER_CAP) + 4 * (2 + tiles) + 16;
 }
 
 // The eval's fast clean-check pass (see eval_hr_kernel) into the fused scratch; returns the
@@ -2402,7 +2415,8 @@ hipError_t launch_eval_fast(const uint32_t* d_adv, const uint32_t* d_fixed, cons
 #endif
   TileDesc* desc = reinterpret_cast<TileDesc*>(scratch);
   uint32_t* dirty = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + fused_scratch_bytes(tiles) - 8);
-  hipError_t e = hipMemsetAsync(dirty, 0, 4, s);
+  unsigned* bctr = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(scratch) + fused_scratch_bytes(tiles) - 16);
+  hipError_t e = hipMemsetAsync(bctr, 0, 16, s);  // the band counter and the dirty word
   if (e != hipSuccess) return e;
   // tiles (an upper bound on the half-round tiles) >= 2 sum(rounds): every tile has its thread
   hipLaunchKernelGGL(eval_desc_kernel, dim3((uint32_t)((tiles + 255) / 256)), dim3(256), 0, s, d_off, n, desc, d_status);
@@ -2431,7 +2445,7 @@ hipError_t launch_eval_fast(const uint32_t* d_adv, const uint32_t* d_fixed, cons
 #define B2F_EVFAST(M)                                                                              \
   case M:                                                                                          \
     hipLaunchKernelGGL(eval_hr_kernel<M>, dim3(cu_count * ev_per_cu), dim3(FW * WAVES), 0, s, d_adv, d_fixed, n, \
-                       d_off, total_rows, desc, dirty, d_status);                                  \
+                       d_off, total_rows, desc, dirty, bctr, d_status);                            \
     if (B2F_EDGE_SEPARATE)                                                                         \
       hipLaunchKernelGGL(eval_edge_kernel<M>, dim3(grid_e), dim3(FW * WAVES), 0, s, d_adv, d_fixed, n, d_off, \
                          total_rows, dirty, d_status);                                             \
@@ -2462,12 +2476,12 @@ hipError_t launch_fill_eval(const b2f_input* d_in, uint32_t n, const uint64_t* d
   TileDesc* desc = reinterpret_cast<TileDesc*>(scratch);
   uint64_t* defer = reinterpret_cast<uint64_t*>(desc + tiles);
   uint32_t* redo = reinterpret_cast<uint32_t*>(defer + 1 + DEFER_CAP);
-  // the half-round launch's instance counter: the first word of the tile-descriptor area (only
-  // the eval's fast pass uses descriptors)
+  // the half-round launch's instance and edge-tile counters: the first two words of the
+  // tile-descriptor area (only the eval's fast pass uses descriptors)
   unsigned* ictr = reinterpret_cast<unsigned*>(desc);
   hipError_t e = hipMemsetAsync(defer, 0, 8, s);
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(ictr, 0, 4, s);
+  e = hipMemsetAsync(ictr, 0, 8, s);  // the instance and the edge-tile counters
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(redo, 0, 4, s);
   if (e != hipSuccess) return e;

@@ -57,7 +57,7 @@ hipError_t launch_permutation(const uint32_t* d_advice, uint64_t total_rows, uin
                               hipEvent_t ev_fork, hipEvent_t ev_join, hipStream_t s);
 hipError_t launch_export_fp(const uint32_t* d_advice, uint64_t total_rows, uint64_t row_begin,
                             uint64_t nrows, uint32_t form, uint64_t* d_out, uint64_t out_rows,
-                            int cu_count, hipStream_t s);  // b2f_export.hip
+                            int cu_count, unsigned* tctr, hipStream_t s);  // b2f_export.hip
 size_t fused_scratch_bytes(uint64_t tiles);
 uint64_t fused_instance_tiles(uint64_t total_rows, uint64_t n);
 hipError_t launch_eval_fast(const uint32_t* d_adv, const uint32_t* d_fixed, const uint64_t* d_off, uint32_t n,
@@ -274,6 +274,11 @@ enum { FILL_COMPUTE = 1, FILL_NT = 2, FILL_FULL = 3, FILL_CLOCK = 8 };
 #ifndef B2F_FILL_WAVES
 #define B2F_FILL_WAVES 1  // minimum waves per SIMD the fill is compiled for (register bound)
 #endif
+#ifndef B2F_FILL_DYN
+// 1 (variant): tiles claimed from a counter, a barrier per tile sharing the claim -- 15.21 vs
+// 10.13 ms (2^18 x 12), profiles/r06k_ab_dyn_*.txt: 1.3 M claims of 45 KB each, and the barrier
+#define B2F_FILL_DYN 0
+#endif
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_input* __restrict__ in,
                                                     uint32_t n,
@@ -285,8 +290,10 @@ __global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_i
                                                     const int* __restrict__ status,
                                                     const TileInfo* __restrict__ tinfo,
                                                     uint64_t n_tiles,
-                                                    unsigned long long* __restrict__ clk) {
+                                                    unsigned long long* __restrict__ clk,
+                                                    unsigned* __restrict__ tctr) {
   __shared__ uint32_t rows[ROW_TABLE_WORDS];
+  __shared__ uint32_t s_tile[2];  // B2F_FILL_DYN: the workgroup's claimed tiles (double-buffered)
   uint64_t ck[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
   auto tick = [&](int k) {
     if (MODE & FILL_CLOCK) {
@@ -317,15 +324,36 @@ __global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_i
       quad_ops_ti(R, 4 * (tt * BLOCK + tid), ti, n, used_rows, in, rec, Sg);
     }
   };
+#if B2F_FILL_DYN
+  // (variant) tiles claimed from the launch's counter one tile ahead (a barrier per tile shares
+  // the claim)
+  uint32_t slot = 0;
+  auto claim = [&]() -> uint64_t {
+    if (tid == 0) s_tile[slot] = atomicAdd(tctr, 1u);
+    __syncthreads();
+    const uint64_t v = __builtin_amdgcn_readfirstlane(s_tile[slot]);
+    slot ^= 1u;
+    return v;
+  };
+  (void)G;
+  uint64_t t = claim();
+#else
+  (void)tctr;
   uint64_t t = blockIdx.x;
+#endif
   QuadOps P;
   tick(-1);
   if (t < n_tiles) ops(P, t);
   tick(0);
-  for (; t < n_tiles; t += G) {
+  while (t < n_tiles) {
+#if B2F_FILL_DYN
+    const uint64_t tn = claim();
+#else
+    const uint64_t tn = t + G;
+#endif
     QuadOps Pn;
     Pn.rounds = ~0u;
-    if (t + G < n_tiles) ops(Pn, t + G);
+    if (tn < n_tiles) ops(Pn, tn);
     tick(0);
     const uint64_t gq = t * BLOCK + tid;
     if (gq < total_quads) {
@@ -357,6 +385,7 @@ __global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_i
     }
     tick(2);
     P = Pn;
+    t = tn;
     tick(3);
   }
   if (MODE & FILL_CLOCK) {
@@ -849,7 +878,8 @@ __global__ void report_init_kernel(b2f_eval_report* rep, uint64_t total_rows) {
 struct b2f_ctx {
   int device;
   char err[512];
-  int* d_status;       // [0] fill call, [1] eval call, [2] sticky (cleared by b2f_sync only)
+  int* d_status;       // [0] fill call, [1] eval call, [2] sticky (cleared by b2f_sync only), [3] fill tile counter,
+                       // [4] export tile counter
   uint64_t* d_rec;     // half-round states
   uint64_t rec_cap;    // in states (16 x u64 each)
   uint64_t* d_seg;     // the fused launch's segment list (count, entries: instance << 32 | m)
@@ -1144,9 +1174,9 @@ B2F_API b2f_ctx* b2f_create(int device) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete ctx; return nullptr; }
   ctx->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-  if (hipMalloc(&ctx->d_status, 4 * sizeof(int)) != hipSuccess) { delete ctx; return nullptr; }
+  if (hipMalloc(&ctx->d_status, 8 * sizeof(int)) != hipSuccess) { delete ctx; return nullptr; }
   // the sticky word must read 0 before the first call: a blocking memset on the null stream
-  if (hipMemset(ctx->d_status, 0, 4 * sizeof(int)) != hipSuccess) { delete ctx; return nullptr; }
+  if (hipMemset(ctx->d_status, 0, 8 * sizeof(int)) != hipSuccess) { delete ctx; return nullptr; }
   return ctx;
 }
 
@@ -1299,12 +1329,15 @@ B2F_API int b2f_fill_dev(b2f_ctx* ctx, const b2f_input* d_in, size_t n, const ui
     HIPCHK(ctx, hipMalloc(&ctx->d_clock, 32 * sizeof(unsigned long long)));
     HIPCHK(ctx, hipMemset(ctx->d_clock, 0, 32 * sizeof(unsigned long long)));
   }
+  // the tile counter of B2F_FILL_DYN: the fourth status word
+  unsigned* tctr = reinterpret_cast<unsigned*>(ctx->d_status + 3);
+  HIPCHK(ctx, hipMemsetAsync(tctr, 0, sizeof(unsigned), s));
   switch (fmode) {
 #define B2F_FILL(M)                                                                            \
   case M:                                                                                      \
     hipLaunchKernelGGL(fill_kernel<M>, dim3(wgs), dim3(BLOCK), 0, s, d_in, nn, d_offsets,      \
                        total_rows, ctx->d_rec, d_advice, d_fixed, ctx->d_status, ctx->d_tiles, \
-                       nt, ctx->d_clock);                                                      \
+                       nt, ctx->d_clock, tctr);                                                \
     break;
 #ifdef B2F_DIAG
     B2F_FILL(0) B2F_FILL(1) B2F_FILL(2) B2F_FILL(FILL_FULL | FILL_CLOCK)
@@ -1493,7 +1526,7 @@ B2F_API int b2f_export_fp_dev(b2f_ctx* ctx, const uint32_t* d_advice, uint64_t t
   HIPCHK(ctx, hipSetDevice(ctx->device));
   int tk = timed_begin(ctx, B2F_KERNEL_EXPORT, s);
   HIPCHK(ctx, launch_export_fp(d_advice, total_rows, row_begin, nrows, form, d_out, out_rows,
-                               ctx->cu_count, s));
+                               ctx->cu_count, reinterpret_cast<unsigned*>(ctx->d_status + 4), s));
   timed_end(ctx, tk, s);
   return B2F_OK;
 }
