@@ -1069,10 +1069,16 @@ __device__ __forceinline__ uint32_t hr_fast_checks(const hr2::Lane& K, uint32_t 
 #define B2F_FUSED_DYN 1  // 0 (variant): instances dealt statically to the waves (round 5)
 #endif
 #ifndef B2F_FUSED_EDGE_DYN
-// 1 (variant): the edge tiles claimed from a counter too -- 11.62 vs 9.38 ms (2^18 x 12) and 8.53
-// vs 6.62 ({1,4,12}), profiles/r06k_ab_dyn_*.txt: an edge tile is 9 KB of work, and 2^18 claims
-// within the launch's last half-millisecond serialise on the one counter
-#define B2F_FUSED_EDGE_DYN 0
+// 1: the edge tiles claimed from a counter too, B2F_FUSED_EDGE_CHUNK consecutive tiles per claim.
+// One tile per claim was 11.62 vs 9.38 ms (2^18 x 12) and 8.53 vs 6.62 ({1,4,12},
+// profiles/r06k_ab_dyn_*.txt): an edge tile is 9 KB of work, and 2^18 claims within the launch's
+// last half-millisecond serialise on the one counter. 16 per claim: 9.49 vs 9.56 dealt, 5.25 vs
+// 5.33; 64 per claim 9.56 / 5.32 (profiles/r06m_ab_edge_*.txt); another box, 8 / 16 / 32 per claim
+// and dealt: 9.77 / 9.79 / 9.80 / 9.84 ms and 4.96 / 4.98 / 4.99 / 5.07 (profiles/r06n_ab_*.txt)
+#define B2F_FUSED_EDGE_DYN 1
+#endif
+#ifndef B2F_FUSED_EDGE_CHUNK
+#define B2F_FUSED_EDGE_CHUNK 8
 #endif
 template <int MODE>
 __device__ __forceinline__ void edge_walk(uint32_t* S, uint32_t lane, uint64_t t_first, uint64_t W,
@@ -1757,10 +1763,18 @@ __device__ __forceinline__ void edge_walk(uint32_t* S, uint32_t lane, uint64_t t
     const uint64_t t_all = (uint64_t)n + n_pad;
     // edge tiles t, t + W, ... from t_first, or (ectr) claimed from the launch's counter: a wave
     // holds the tile it works on and the next two, whose context it loads ahead
+    // (B2F_FUSED_EDGE_CHUNK consecutive tiles per claim)
+    uint32_t cleft = 0;
+    uint64_t cbase = 0;
     auto claim = [&]() -> uint64_t {
-      uint32_t v = 0;
-      if (lane == 0) v = atomicAdd(ectr, 1u);
-      return __builtin_amdgcn_readfirstlane(v);
+      if (cleft == 0) {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(ectr, (unsigned)B2F_FUSED_EDGE_CHUNK);
+        cbase = __builtin_amdgcn_readfirstlane(v);
+        cleft = B2F_FUSED_EDGE_CHUNK;
+      }
+      cleft--;
+      return cbase++;
     };
     uint64_t t = ectr ? claim() : t_first;
     uint64_t t1 = ectr ? claim() : t + W;

@@ -275,10 +275,17 @@ enum { FILL_COMPUTE = 1, FILL_NT = 2, FILL_FULL = 3, FILL_CLOCK = 8 };
 #define B2F_FILL_WAVES 1  // minimum waves per SIMD the fill is compiled for (register bound)
 #endif
 #ifndef B2F_FILL_DYN
-// 1 (variant): tiles claimed from a counter, a barrier per tile sharing the claim -- 15.21 vs
-// 10.13 ms (2^18 x 12), profiles/r06k_ab_dyn_*.txt: 1.3 M claims of 45 KB each, and the barrier
-#define B2F_FILL_DYN 0
+// 1: tiles claimed from a counter in chunks of FILL_CHUNK. One tile per claim was 15.21 vs 10.13
+// ms (2^18 x 12, profiles/r06k_ab_dyn_*.txt): 1.3 M claims in 10 ms on one address serialise.
+// Per claim 4 / 8 / 16 tiles: 9.02 / 9.07 / 9.14 ms against 10.01 dealt round-robin; {1,4,12}:
+// 4.68 / 4.71 / 4.77 against 5.16 (profiles/r06l_ab_fill_*.txt, r06m_ab_fill_*.txt); 2 against 4
+// on another box: 9.25 vs 9.36, 4.45 vs 4.47 (profiles/r06n_ab_*.txt)
+#define B2F_FILL_DYN 1
 #endif
+#ifndef B2F_FILL_CHUNK
+#define B2F_FILL_CHUNK 2
+#endif
+constexpr uint32_t FILL_CHUNK = B2F_FILL_CHUNK;
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_input* __restrict__ in,
                                                     uint32_t n,
@@ -325,15 +332,20 @@ __global__ void __launch_bounds__(BLOCK, B2F_FILL_WAVES) fill_kernel(const b2f_i
     }
   };
 #if B2F_FILL_DYN
-  // (variant) tiles claimed from the launch's counter one tile ahead (a barrier per tile shares
-  // the claim)
-  uint32_t slot = 0;
+  // tiles claimed from the launch's counter in chunks of FILL_CHUNK consecutive tiles (a barrier
+  // per chunk shares the claim), one tile ahead: the workgroups finish within a chunk of each other
+  uint32_t slot = 0, cleft = 0;
+  uint64_t cbase = 0;
   auto claim = [&]() -> uint64_t {
-    if (tid == 0) s_tile[slot] = atomicAdd(tctr, 1u);
-    __syncthreads();
-    const uint64_t v = __builtin_amdgcn_readfirstlane(s_tile[slot]);
-    slot ^= 1u;
-    return v;
+    if (cleft == 0) {  // workgroup-uniform
+      if (tid == 0) s_tile[slot] = atomicAdd(tctr, (unsigned)FILL_CHUNK);
+      __syncthreads();
+      cbase = __builtin_amdgcn_readfirstlane(s_tile[slot]);
+      slot ^= 1u;
+      cleft = FILL_CHUNK;
+    }
+    cleft--;
+    return cbase++;
   };
   (void)G;
   uint64_t t = claim();
