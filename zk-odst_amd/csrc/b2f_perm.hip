@@ -288,8 +288,16 @@ __global__ __launch_bounds__(gp::BLK) __attribute__((amdgpu_waves_per_eu(PmWaves
         const bool ident_enc = (mm & 0x1fffffffu) == 0x1fffffffu;
         const uint32_t c2 = ident_enc ? j : mm >> ROW_BITS;
         const uint64_t r2 = ident_enc ? r : cur_lo + (mm & ((1u << ROW_BITS) - 1));
+#ifdef B2F_PM_NOIDENT  // diagnostics (results wrong): no identity coset product
+        const Fe fn = vg;
+#else
         const Fe fn = field::add<F>(vg, dw<F>(BL, OH, j, r));
+#endif
+#ifdef B2F_PM_NOSIGMA  // diagnostics (results wrong): no sigma product, as if sigma were loaded
+        const Fe fd = (c2 == j && r2 == r) ? fn : vg;
+#else
         const Fe fd = (c2 == j && r2 == r) ? fn : field::add<F>(vg, dw<F>(BL, OH, c2, r2));
+#endif
         n = jj == 0 ? fn : field::mul<F>(n, fn);
         d = jj == 0 ? fd : field::mul<F>(d, fd);
       }
