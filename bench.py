@@ -631,8 +631,10 @@ def main():
 
     # same-box floors, from the diagnostics library (libb2f_diag.so; the product library has
     # no diagnostic variants): the fill with its stores but no cell computation
-    # (B2F_DIAG_FILL=2) and the eval with its loads, staging and lookups but no gates or copies
-    # (B2F_DIAG_EVAL=1). Boxes differ by up to ~40 % in store rate, so the achieved/floor ratio
+    # (B2F_DIAG_FILL=2), a plain store stream over the same columns (B2F_DIAG_FILL=4), the eval
+    # with its loads, staging and lookups but no gates or copies (B2F_DIAG_EVAL=1; it fetches only
+    # 0.86x the trace's bytes, so it is not a read floor) and a plain read stream over the same
+    # columns (B2F_DIAG_EVAL=32, load_stream_kernel: the eval's read floor). Boxes differ by up to ~40 % in store rate, so the achieved/floor ratio
     # is the comparable number. Each rep launches floor and product kernels back to back
     # (fill floor, fused pass, split fill, eval floor, split eval), so drifts in the box's
     # store rate hit both sides alike; min and median over the reps are reported.
@@ -641,7 +643,7 @@ def main():
         try:
             deng = b2f.Engine(local, diag=True)
             samples = {"fill_floor": [], "stream_floor": [], "fill_eval": [], "fill": [],
-                       "eval_floor": [], "eval": []}
+                       "eval_floor": [], "read_stream_floor": [], "eval": []}
 
             def one(e, fn, kname, var=None, val=None):
                 if var:
@@ -661,6 +663,7 @@ def main():
                 samples["fill_eval"].append(one(eng, batch.fill_evaluate, "fill_eval"))
                 samples["fill"].append(one(eng, batch.fill, "fill"))
                 samples["eval_floor"].append(one(deng, batch.evaluate, "eval", "B2F_DIAG_EVAL", "1"))
+                samples["read_stream_floor"].append(one(deng, batch.evaluate, "eval", "B2F_DIAG_EVAL", "32"))
                 samples["eval"].append(one(eng, batch.evaluate, "eval"))
             deng.sync(stream)
             deng.close()
@@ -676,6 +679,8 @@ def main():
                       "eval_floor_ms": round(med["eval_floor"], 4),
                       "fill_over_floor": round(med["fill"] / med["fill_floor"], 4),
                       "eval_over_floor": round(med["eval"] / med["eval_floor"], 4),
+                      "read_stream_floor_ms": round(med["read_stream_floor"], 4),
+                      "eval_over_read_stream_floor": round(med["eval"] / med["read_stream_floor"], 4),
                       "fill_eval_over_fill_floor": round(med["fill_eval"] / med["fill_floor"], 4),
                       "fill_eval_over_fill_floor_min": round(mn["fill_eval"] / mn["fill_floor"], 4),
                       "stream_floor_ms": round(med["stream_floor"], 4),

@@ -429,6 +429,37 @@ __global__ void __launch_bounds__(BLOCK) store_stream_kernel(uint32_t* __restric
 }
 #endif
 
+// Diagnostics (B2F_DIAG_EVAL=32 in the diagnostics library): the read counterpart of
+// store_stream_kernel -- every 16-byte quad of the same 11 columns loaded once in address order
+// (grid-stride, 4 loads in flight per thread), XOR-folded so no load is dead (the fold lands in
+// the spare status word only if it equals a constant): the box's read rate for these bytes with
+// no tile structure, the eval's load floor. (eval_kernel<1>, the floor before round 6, does not
+// count as one: its FETCH_SIZE is 0.86x the trace's bytes, profiles/r06z3_eval_floor_fetch.json.)
+#ifdef B2F_DIAG
+__global__ void __launch_bounds__(BLOCK) load_stream_kernel(const uint32_t* __restrict__ adv,
+                                                           const uint32_t* __restrict__ fixed,
+                                                           uint64_t total_rows, int* __restrict__ sink) {
+  const uint64_t per_col = total_rows >> 2, chunks = 11 * per_col;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  auto at = [&](uint64_t j) -> const u32x4* {
+    const uint64_t c = j / per_col, q = j - c * per_col;
+    return reinterpret_cast<const u32x4*>((c < 10 ? adv + c * total_rows : fixed) + 4 * q);
+  };
+  uint32_t acc = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < chunks; j += 4 * stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint64_t jk = j + k * stride;
+      v[k] = jk < chunks ? *at(jk) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) acc ^= v[k][0] ^ v[k][1] ^ v[k][2] ^ v[k][3];
+  }
+  if (acc == 0x9e3779b9u) sink[0] = 1;
+}
+#endif
+
 // --------------------------------------------------------------------------- eval kernel
 //
 // Software-pipelined over 1024-row tiles dealt round-robin to persistent workgroups (3 per
@@ -514,7 +545,8 @@ constexpr GTCarve kEvalGT{GS_QM, GS_NG, GS_GT, L_IC, L_W, WSTRIDE, BLOCK / 4, BL
 
 // MODE (diagnostics; the product uses EVAL_FULL): which checks run on a staged tile.
 enum { EVAL_LOOKUP = 1, EVAL_GATES = 2, EVAL_COPIES = 4, EVAL_FULL = 7, EVAL_TOUCH = 8,
-       EVAL_CLOCK = 16 };  // EVAL_CLOCK: per-phase s_memtime totals per wave (diagnostics)
+       EVAL_CLOCK = 16,    // EVAL_CLOCK: per-phase s_memtime totals per wave (diagnostics)
+       EVAL_STREAM = 32 };  // (diagnostics) load_stream_kernel alone: the read floor
 
 // Tiles per band: a workgroup checks EVAL_BAND consecutive tiles, then jumps a grid's worth of
 // bands (XCD-aware over bands). Inside a band the history window of a tile is the previous
@@ -1476,6 +1508,15 @@ B2F_API int b2f_eval_dev(b2f_ctx* ctx, const uint32_t* d_advice, const uint32_t*
     if (rc) return rc;
   }
   int tk = timed_begin(ctx, B2F_KERNEL_EVAL, s);
+#ifdef B2F_DIAG
+  if (emode == EVAL_STREAM) {  // the read floor alone (the spare eighth status word as its sink)
+    hipLaunchKernelGGL(load_stream_kernel, dim3(ctx->cu_count * 8), dim3(BLOCK), 0, s, d_advice, d_fixed,
+                       total_rows, ctx->d_status + 7);
+    HIPCHK(ctx, hipGetLastError());
+    timed_end(ctx, tk, s);
+    return B2F_OK;
+  }
+#endif
   if (fast)
     HIPCHK(ctx, launch_eval_fast(d_advice, d_fixed, d_offsets, (uint32_t)n, total_rows, ctx->d_fz,
                                  fused_instance_tiles(total_rows, n), ctx->d_status + 1, ctx->cu_count, s, &gate,
