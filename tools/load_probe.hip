@@ -68,6 +68,50 @@ __global__ void __launch_bounds__(256) probe(const uint32_t* __restrict__ a, uin
   if (acc == 0x12345678u) out[0] = acc;  // keeps the loads
 }
 
+// the eval kernel's floor shape: a workgroup per 1,024-row tile (wave k reads rows 256k..256k+255
+// of it: 4 KB of every column per workgroup), tiles dealt to workgroups in bands of B with the
+// XCD-aware deal of eval_kernel (b2f_kernels.hip)
+__global__ void __launch_bounds__(256) probe_wg(const uint32_t* __restrict__ a, uint64_t rows, uint32_t band,
+                                               uint32_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t G = gridDim.x;
+  const uint64_t b0 = (G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+  const uint64_t n = rows / 1024;
+  auto seq = [&](uint64_t k) { return (b0 + (k / band) * G) * band + k % band; };
+  uint32_t acc = 0;
+  uint64_t i = 0, t = seq(0);
+  Chunk cur = load_chunk(a, rows, (t < n ? t : 0) * 1024 + 256 * wv, lane);
+  while (t < n) {
+    const uint64_t tn = seq(i + 1);
+    const Chunk nxt = load_chunk(a, rows, (tn < n ? tn : 0) * 1024 + 256 * wv, lane);
+#pragma unroll
+    for (int k = 0; k < NCOL; k++) acc ^= cur.v[k].x ^ cur.v[k].y ^ cur.v[k].z ^ cur.v[k].w;
+    cur = nxt;
+    t = tn;
+    i++;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+float run_wg(const uint32_t* a, uint64_t rows, uint32_t band, uint32_t* out, int wgs_per_cu, int cus) {
+  hipEvent_t e0, e1;
+  CHK(hipEventCreate(&e0));
+  CHK(hipEventCreate(&e1));
+  float best = 1e30f;
+  for (int rep = 0; rep < 4; rep++) {
+    CHK(hipEventRecord(e0));
+    hipLaunchKernelGGL(probe_wg, dim3(cus * wgs_per_cu), dim3(256), 0, 0, a, rows, band, out);
+    CHK(hipEventRecord(e1));
+    CHK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHK(hipEventElapsedTime(&ms, e0, e1));
+    if (rep > 0 && ms < best) best = ms;
+  }
+  CHK(hipEventDestroy(e0));
+  CHK(hipEventDestroy(e1));
+  return best;
+}
+
 template <int C, bool BAND>
 float run(const uint32_t* a, uint64_t rows, uint32_t band, uint32_t* out, int wgs_per_cu, int cus) {
   hipEvent_t e0, e1;
@@ -112,6 +156,10 @@ int main(int argc, char** argv) {
     printf("wg/CU %d  C=256 band 24   %7.3f ms  %6.0f GB/s\n", wpc, t, gb / t * 1e3);
     t = run<256, true>(a, rows, 4, out, wpc, cus);
     printf("wg/CU %d  C=256 band 4    %7.3f ms  %6.0f GB/s\n", wpc, t, gb / t * 1e3);
+    t = run_wg(a, rows, 4, out, wpc, cus);
+    printf("wg/CU %d  wg tile band 4 %7.3f ms  %6.0f GB/s\n", wpc, t, gb / t * 1e3);
+    t = run_wg(a, rows, 1, out, wpc, cus);
+    printf("wg/CU %d  wg tile rr     %7.3f ms  %6.0f GB/s\n", wpc, t, gb / t * 1e3);
   }
   CHK(hipFree(a));
   CHK(hipFree(out));
