@@ -20,6 +20,8 @@ names_of = collections.defaultdict(set)  # kind -> the kernel names aggregated i
 
 
 def per_kernel(d, counter):
+    """Per kind: the sum over its kernels of each kernel's average per dispatch (a call of the
+    kind launches each of its kernels once)."""
     vals = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         per_dispatch = collections.defaultdict(float)
@@ -37,13 +39,17 @@ def per_kernel(d, counter):
             if kind is None:
                 continue
             per_dispatch[r["Dispatch_Id"]] += float(r["Counter_Value"])
-            names[r["Dispatch_Id"]] = kind
             nm = k.replace("(anonymous namespace)::", "")
-            nm = nm[5:] if nm.startswith("void ") else nm
-            names_of[kind].add(nm.split("(")[0])
+            nm = (nm[5:] if nm.startswith("void ") else nm).split("(")[0]
+            names[r["Dispatch_Id"]] = (kind, nm)
+            names_of[kind].add(nm)
         for disp, v in per_dispatch.items():
             vals[names[disp]].append(v)
-    return {k: sum(v) / len(v) for k, v in vals.items() if v}
+    out = collections.defaultdict(float)
+    for (kind, _), v in vals.items():
+        if v:
+            out[kind] += sum(v) / len(v)
+    return dict(out)
 
 
 def main():
@@ -57,8 +63,8 @@ def main():
     for d in (fetch, write):
         if "fill_eval_edge" in d:
             d["fill_eval"] = d.get("fill_eval", 0.0) + d.pop("fill_eval_edge")
-        if "eval_part" in d:  # per launch; two launches (half-round, edge) per eval call
-            d["eval"] = d.get("eval", 0.0) + 2 * d.pop("eval_part")
+        if "eval_part" in d:  # the fast pass (its edge walk inside the half-round launch since
+            d["eval"] = d.get("eval", 0.0) + d.pop("eval_part")  # round 6) + the gated exact kernel
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "zk-odst_amd"))
     from b2f import _lib
 

@@ -2164,12 +2164,23 @@ __device__ __forceinline__ EvCells ev_load(const hr2::HCtx& c, uint32_t lane, ui
   v.c10 = ev_ld(fixed + c.row0 + 4 * lq);
   // the limb-table gather only when the previous half-round's tile is not the wave's previous tile
   // (otherwise a read of the tile's own first cells: lines this wave loads anyway, value unused)
+#ifdef B2F_EV_NOGATHER  // diagnostics (verdict wrong): no limb-table or message gathers, to bound their traffic
+  (void)gath;
+  (void)Sg;
+  (void)mg;
+  (void)mwh;
+  (void)mk;
+  v.d = v.c0.x;
+  v.sp = v.c1.y;
+  v.mc = v.c2.z;
+#else
   const Canon cs = canon_state(lane >> 2, c.hr);
   const uint64_t r = gath ? c.off + cs.row(lane & 3u) : c.row0 + 4 * lq;
   v.d = adv[(uint64_t)(gath ? cs.dcol : (uint32_t)A1) * total_rows + r];
   v.sp = adv[(uint64_t)(gath ? cs.scol : (uint32_t)A2) * total_rows + r];
   const uint32_t j = Sg[16 * ((c.hr >> 1) % 10) + 2 * (mg + 4 * (c.hr & 1u)) + mwh];
   v.mc = adv[(uint64_t)A1 * total_rows + c.off + 32 + 4 * j + mk];
+#endif
   return v;
 }
 
