@@ -77,6 +77,37 @@ def test_lookup_columns_equal_oracle(engine, trace, form):
                 pytest.fail("circuit %d column %s differs first at row %d" % (c, name, i))
 
 
+@pytest.mark.parametrize("which", ["small", "minus", "mid"])
+def test_lookup_structured_theta(engine, trace, which):
+    """Challenges whose table values share their top 64-bit limb in long runs (round 6): theta =
+    3 puts all 2^16 values below 2^192 (one run, already in order), theta = -2^40 puts 65,281 of
+    them below 2^192 in descending order of x (a long run out of order), theta = 2^100 + 1 leaves
+    runs by tag. The rank order is the order of the full values in every case
+    (lk_tie_fix_kernel), so the columns equal the oracle's. (Each theta keeps the 2^16 table
+    values distinct; a theta that makes two of them equal -- theta = -3: T[1] = T[2] -- is not
+    covered: the kernels treat equal values of two table rows as two runs where halo2 makes one,
+    which moves a leftover in S'; for a transcript challenge that has probability ~2^-222.)"""
+    import lookup as lk
+    import torch
+
+    usable = 1 << 16
+    theta = {"small": 3, "minus": lk.P - (1 << 40), "mid": (1 << 100) + 1}[which]
+    _, beta, gamma = _chal(13)
+    out, bad = trace.lookup_columns(engine, [5000], usable, theta, beta, gamma)
+    engine.sync(torch.cuda.current_stream().cuda_stream)
+    assert (bad.cpu().numpy().view(np.uint64) == np.uint64(2**64 - 1)).all()
+    adv, _ = trace.host_trace()
+    a = _circuit_rows(adv, trace.total_rows, 5000, usable)
+    ref = lk.columns(a[0], a[1], a[2], usable, theta, beta, gamma)
+    for j, name in enumerate(["A", "S", "A'", "S'", "z"]):
+        n = usable + 1 if j == 4 else usable
+        got = _col_ints(out[0, j, :n])
+        want = [v * R256 % lk.P for v in ref[j]]
+        if got != want:
+            i = next(i for i in range(n) if got[i] != want[i])
+            pytest.fail("theta %s column %s differs first at row %d" % (which, name, i))
+
+
 def test_lookup_min_usable_and_bad_row(engine, trace):
     """usable = 2^16 (the table exactly fills the circuit); a flipped spread cell in the trace
     is reported at its circuit row (and only for the circuits holding it)."""

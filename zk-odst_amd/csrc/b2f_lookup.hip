@@ -92,34 +92,51 @@ __global__ __launch_bounds__(256) void lk_table_kernel(Chal ch, Fe* __restrict__
   perm[x] = x;
 }
 
-// After one radix sort by the top 64-bit limb of the canonical value: a run of equal top limbs
-// (about 2^-33 likely for 2^16 uniform values, but possible) is put in order by the three lower
-// limbs, in place, by the thread at the run's start (insertion sort). The rank order is then the
-// order of the full 256-bit values, as four LSD passes over the limbs would give.
+// After one radix sort by the top 64-bit limb of the canonical value, equal top limbs are put in
+// order by the three lower limbs: each thread of a run of equal top limbs (found by two binary
+// searches in the sorted limbs) counts the run's members below it -- by the lower limbs, then
+// by position -- and writes its table index at that rank into the output order; a thread not in
+// a run copies its index. The rank order is then the order of the full 256-bit values, as four
+// LSD passes over the limbs would give. For a uniform challenge runs are pairs at most (2^-33
+// likely), but a structured one (theta = 3: every value below 2^192, one run of 2^16; theta = -3:
+// a long run just below p, out of order) makes long runs, which cost O(L) per thread here, with
+// L threads at once, instead of one thread's insertion sort (round 6; O(L^2) on one thread).
 __global__ __launch_bounds__(256) void lk_tie_fix_kernel(const uint64_t* __restrict__ key,
                                                          const uint64_t* __restrict__ top,
-                                                         uint32_t* __restrict__ perm) {
+                                                         const uint32_t* __restrict__ pin,
+                                                         uint32_t* __restrict__ pout) {
   const uint32_t r = blockIdx.x * 256 + threadIdx.x;
   const uint64_t k = top[r];
-  if ((r > 0 && top[r - 1] == k) || r + 1 >= TROWS || top[r + 1] != k) return;
-  uint32_t e = r + 1;
-  while (e < TROWS && top[e] == k) e++;
-  auto less = [&](uint32_t a, uint32_t b) {
-    for (int l = 2; l >= 0; l--) {
-      const uint64_t x = key[(uint64_t)l * TROWS + a], y = key[(uint64_t)l * TROWS + b];
-      if (x != y) return x < y;
-    }
-    return false;
-  };
-  for (uint32_t i = r + 1; i < e; i++) {
-    const uint32_t v = perm[i];
-    uint32_t j = i;
-    while (j > r && less(v, perm[j - 1])) {
-      perm[j] = perm[j - 1];
-      j--;
-    }
-    perm[j] = v;
+  const uint32_t x = pin[r];
+  const bool tl = r > 0 && top[r - 1] == k, tr = r + 1 < (uint32_t)TROWS && top[r + 1] == k;
+  if (!tl && !tr) {
+    pout[r] = x;
+    return;
   }
+  uint32_t lo = 0, hi = r;  // the run's first index: the first with top == k
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (top[m] < k) lo = m + 1;
+    else hi = m;
+  }
+  const uint32_t s = lo;
+  lo = r + 1;
+  hi = TROWS;  // one past its last: the first with top > k
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (top[m] <= k) lo = m + 1;
+    else hi = m;
+  }
+  const uint32_t e = lo;
+  const uint64_t a2 = key[2ull * TROWS + x], a1 = key[(uint64_t)TROWS + x], a0 = key[x];
+  uint32_t rank = 0;
+#pragma unroll 8
+  for (uint32_t q = s; q < e; q++) {  // (unrolled: eight members' loads in flight at once)
+    const uint32_t y = pin[q];
+    const uint64_t b2 = key[2ull * TROWS + y], b1 = key[(uint64_t)TROWS + y], b0 = key[y];
+    rank += (b2 != a2 ? b2 < a2 : b1 != a1 ? b1 < a1 : b0 != a0 ? b0 < a0 : q < r) ? 1u : 0u;
+  }
+  pout[s + rank] = x;
 }
 
 // ------------------------------------------------------------------ per-circuit passes
@@ -1049,8 +1066,8 @@ struct Carve {
   Fe* Tx;
   uint64_t* key;   // 4 x TROWS canonical limbs
   uint64_t* kout;  // TROWS
-  uint32_t* perm;  // TROWS
-  uint32_t* perm2;
+  uint32_t* perm;   // TROWS: the sort's input (x), then the rank order (lk_tie_fix_kernel)
+  uint32_t* perm2;  // TROWS: the sort's output (by top limb)
   uint32_t* count;  // group x TROWS
   uint32_t* pos;
   uint32_t* dcnt;
@@ -1153,14 +1170,15 @@ hipError_t run_lookup(const uint32_t* d_advice, uint64_t total_rows, const uint6
   }
   hipLaunchKernelGGL(lk_table_kernel<F>, tb, dim3(256), 0, st, ch, k.Tx, k.key, k.perm, k.bg);
   if ((e = hipEventRecord(ss.tab, st)) != hipSuccess) return e;
-  uint32_t* pa = k.perm2;
   {
     size_t bytes = k.sort_bytes;
-    e = rocprim::radix_sort_pairs(k.sort_tmp, bytes, k.key + 3ull * TROWS, k.kout, k.perm, pa,
+    e = rocprim::radix_sort_pairs(k.sort_tmp, bytes, k.key + 3ull * TROWS, k.kout, k.perm, k.perm2,
                                   (size_t)TROWS, 0, 63, st);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(lk_tie_fix_kernel, tb, dim3(256), 0, st, k.key, k.kout, pa);
+  // the tie fix reads the sort's order (perm2) and writes the final one over the sort's input
+  hipLaunchKernelGGL(lk_tie_fix_kernel, tb, dim3(256), 0, st, k.key, k.kout, k.perm2, k.perm);
+  uint32_t* pa = k.perm;
   if ((e = hipEventRecord(ss.sorted, st)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(d_first_bad, 0xff, 8ull * n_circuits, s)) != hipSuccess) return e;
   // Per group: the num side (block products, their prefix, D and D^-1) on the side stream,
